@@ -1,0 +1,146 @@
+"""ctypes binding of the CPU oracle (libpbg_oracle.so).  TEST INFRASTRUCTURE ONLY.
+
+Importable from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the
+product package (pybullet-gym_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
+ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4}
+ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
+            "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
+            "HumanoidPyBulletEnv-v0": "humanoid"}
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.pbg_oracle_info.argtypes = [ctypes.c_int, P]
+        L.pbg_oracle_reset.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+        L.pbg_oracle_step.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int]
+        L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
+        L.pbg_oracle_dynamics.argtypes = [ctypes.c_int, P, P, P]
+        L.pbg_oracle_link_com.argtypes = [ctypes.c_int, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def robot_id(name: str) -> int:
+    return ROBOT_IDS[ENV_KEYS.get(name, name)]
+
+
+class Info:
+    FIELDS = ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "OBS", "SD", "AD",
+              "floating", "kind", "substeps")
+
+    def __init__(self, rid):
+        out = np.zeros(16, dtype=np.int32)
+        assert lib().pbg_oracle_info(rid, _p(out)) == 0
+        for k, v in zip(self.FIELDS, out):
+            setattr(self, k, int(v))
+
+
+class OracleEnvs:
+    """Batch of n envs stepped by the CPU oracle (float64 physics)."""
+
+    def __init__(self, name: str, n: int, nthreads: int = 1):
+        self.rid = robot_id(name)
+        self.info = Info(self.rid)
+        self.n = n
+        self.nthreads = nthreads
+        self.state = np.zeros((n, self.info.SD), dtype=np.float64)
+        self.aux = np.zeros((n, self.info.AD), dtype=np.float64)
+
+    def reset(self, qinit: np.ndarray) -> np.ndarray:
+        qinit = np.ascontiguousarray(qinit, dtype=np.float64).reshape(self.n, self.info.NR)
+        obs = np.zeros((self.n, self.info.OBS), dtype=np.float32)
+        assert lib().pbg_oracle_reset(self.rid, self.n, _p(self.state), _p(self.aux), _p(qinit), _p(obs)) == 0
+        return obs
+
+    def step(self, act: np.ndarray):
+        act = np.ascontiguousarray(act, dtype=np.float32).reshape(self.n, self.info.NA)
+        obs = np.zeros((self.n, self.info.OBS), dtype=np.float32)
+        rew = np.zeros(self.n, dtype=np.float64)
+        done = np.zeros(self.n, dtype=np.uint8)
+        nc = np.zeros(self.n, dtype=np.int32)
+        assert lib().pbg_oracle_step(self.rid, self.n, _p(self.state), _p(self.aux), _p(act), _p(obs),
+                                     _p(rew), _p(done), _p(nc), self.nthreads) == 0
+        return obs, rew, done.astype(bool), nc
+
+
+def dynamics(name: str, state: np.ndarray):
+    rid = robot_id(name)
+    info = Info(rid)
+    M = np.zeros((info.NDOF, info.NDOF))
+    C = np.zeros(info.NDOF)
+    lib().pbg_oracle_dynamics(rid, _p(np.ascontiguousarray(state, dtype=np.float64)), _p(M), _p(C))
+    return M, C
+
+
+def link_com(name: str, state: np.ndarray):
+    rid = robot_id(name)
+    info = Info(rid)
+    out = np.zeros((info.NL + 1, 3))
+    lib().pbg_oracle_link_com(rid, _p(np.ascontiguousarray(state, dtype=np.float64)), _p(out))
+    return out
+
+
+class _PackIn(ctypes.Structure):
+    _fields_ = [("part_xyz", ctypes.c_void_p), ("n_parts", ctypes.c_int),
+                ("body_quat", ctypes.c_void_p), ("body_pos", ctypes.c_void_p),
+                ("body_vel", ctypes.c_void_p), ("jq", ctypes.c_void_p), ("jqd", ctypes.c_void_p),
+                ("feet_prev", ctypes.c_void_p), ("feet_new", ctypes.c_void_p), ("act", ctypes.c_void_p),
+                ("potential_old", ctypes.c_double), ("initial_z", ctypes.c_double)]
+
+
+class _PackOut(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_double), ("done", ctypes.c_uint8),
+                ("potential", ctypes.c_double), ("initial_z", ctypes.c_double),
+                ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5)]
+
+
+def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet_new, act,
+         potential_old, initial_z):
+    """Run the oracle's pack on explicit inputs (golden-vector tests)."""
+    rid = robot_id(name)
+    info = Info(rid)
+    arrs = dict(part_xyz=np.ascontiguousarray(part_xyz, dtype=np.float64),
+                body_quat=np.ascontiguousarray(body_quat, dtype=np.float64),
+                body_pos=np.ascontiguousarray(body_pos, dtype=np.float64),
+                body_vel=np.ascontiguousarray(body_vel, dtype=np.float64),
+                jq=np.ascontiguousarray(jq, dtype=np.float64), jqd=np.ascontiguousarray(jqd, dtype=np.float64),
+                feet_prev=np.ascontiguousarray(feet_prev, dtype=np.float32))
+    fn = None if feet_new is None else np.ascontiguousarray(feet_new, dtype=np.uint8)
+    ac = None if act is None else np.ascontiguousarray(act, dtype=np.float32)
+    pin = _PackIn(_p(arrs["part_xyz"]), len(arrs["part_xyz"]), _p(arrs["body_quat"]), _p(arrs["body_pos"]),
+                  _p(arrs["body_vel"]), _p(arrs["jq"]), _p(arrs["jqd"]), _p(arrs["feet_prev"]), _p(fn),
+                  _p(ac), float(potential_old), float(initial_z))
+    obs = np.zeros(info.OBS, dtype=np.float32)
+    feet_out = np.zeros(max(1, info.NF), dtype=np.float32)
+    pout = _PackOut()
+    pout.obs = _p(obs)
+    pout.feet_out = _p(feet_out)
+    assert lib().pbg_oracle_pack(rid, ctypes.byref(pin), ctypes.byref(pout)) == 0
+    return dict(obs=obs, reward=pout.reward, done=bool(pout.done), potential=pout.potential,
+                initial_z=pout.initial_z, feet=feet_out[:info.NF].copy(), rewards=list(pout.rewards))

@@ -1,0 +1,34 @@
+// Physics parameters shared by the HIP step kernel and the CPU oracle.
+//
+// Scene/World constants restate the reference (file:line under /root/reference).
+// Solver internals restate Bullet's btMultiBody / btMultiBodyConstraintSolver defaults,
+// which live in the third-party pybullet wheel (absent here): they are [EXT] and
+// unpinned by anything in this container.
+#pragma once
+
+#define PBG_GRAVITY 9.8                 // gym_locomotion_envs.py:19, gym_pendulum_envs.py:14
+#define PBG_CONTACT_ERP 0.9             // scene_bases.py:62 setDefaultContactERP(0.9)
+#define PBG_SOLVER_ITERATIONS 5         // scene_bases.py:65 numSolverIterations=5
+#define PBG_LIMIT_ERP 0.2               // [EXT] btContactSolverInfo::m_erp default
+#define PBG_LIMIT_MAX_IMPULSE 100.0     // [EXT] btMultiBodyJointLimitConstraint max impulse
+#define PBG_CONTACT_THRESHOLD 0.02      // [EXT] gContactBreakingThreshold
+#define PBG_LINEAR_DAMPING 0.04         // [EXT] btMultiBody m_linearDamping (k1 = k2)
+#define PBG_ANGULAR_DAMPING 0.04        // [EXT] btMultiBody m_angularDamping (k1 = k2)
+#define PBG_MAX_COORD_VELOCITY 100.0    // [EXT] btMultiBody m_maxCoordinateVelocity
+#define PBG_ANGULAR_MOTION_THRESHOLD 0.7853981633974483  // [EXT] 0.5*SIMD_HALF_PI
+#define PBG_WALK_TARGET_X 1000.0        // robot_locomotors.py:12 walk_target_x = 1e3
+#define PBG_WALK_TARGET_Y 0.0           // robot_locomotors.py:13
+#define PBG_OBS_CLIP 5.0                // robot_locomotors.py:64 np.clip(..., -5, +5)
+#define PBG_JOINT_AT_LIMIT 0.99f        // robot_locomotors.py:36 (float32 compare)
+
+// Per-env physical state record (float64 at the C-ABI, float32 inside the kernel):
+//   [0..2] base COM position  [3..6] base quaternion (x,y,z,w)
+//   [7..9] base COM linear velocity (world)  [10..12] base angular velocity (world)
+//   [13 .. 13+NJ)  joint positions q   [13+NJ .. 13+2NJ)  joint velocities qd
+// Fixed-base robots keep the 13 base words at their load values.
+#define PBG_BASE_WORDS 13
+
+// Per-env bookkeeping record (float64):
+//   [0] potential  [1] initial_z  [2] elapsed steps  [3] floor-in-parts flag
+//   [4 .. 4+NF) feet_contact (as written into the observation)
+#define PBG_AUX_WORDS 4

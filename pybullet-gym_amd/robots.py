@@ -1,0 +1,125 @@
+"""Per-robot environment constants, restated from the reference's robot/env classes.
+
+Every constant cites the reference line it restates.  These feed the model tables
+(``codegen.py``) that the HIP kernel and the CPU oracle share.
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from . import mjcf
+
+ALIVE_HOPPER = 0       # robot_locomotors.py:89-90   (+1 if z>0.8 and |pitch|<1 else -1)
+ALIVE_HALFCHEETAH = 1  # robot_locomotors.py:116-118 (+1 if |pitch|<1 and no contact on feet 1,2,4,5)
+ALIVE_ANT = 2          # robot_locomotors.py:137-138 (+1 if z>0.26 else -1)
+ALIVE_HUMANOID = 3     # robot_locomotors.py:191-192 (+2 if z>0.78 else -1)
+ALIVE_PENDULUM = 4     # gym_pendulum_envs.py:35-39  (reward 1, done |theta|>0.2)
+
+KIND_WALKER = 0
+KIND_PENDULUM = 1
+
+
+@dataclass
+class RobotSpec:
+    env_id: str
+    key: str
+    mjcf: str
+    robot_name: str
+    action_dim: int
+    obs_dim: int
+    kind: int
+    power: float = 1.0
+    foot_list: List[str] = field(default_factory=list)
+    alive: int = ALIVE_ANT
+    power_coef: Dict[str, float] = field(default_factory=dict)   # overrides of 100.0
+    motor_order: Optional[List[str]] = None                      # Humanoid.apply_action order
+    initial_z: Optional[float] = None                            # fixed z0 (Humanoid 0.8)
+    electricity_cost: float = -2.0                               # gym_locomotion_envs.py:48
+    stall_torque_cost: float = -0.1                              # gym_locomotion_envs.py:49
+    joints_at_limit_cost: float = -0.1                           # gym_locomotion_envs.py:52
+    timestep: float = 0.0165 / 4                                 # gym_locomotion_envs.py:19
+    frame_skip: int = 4
+    floor: bool = True
+    max_episode_steps: int = 1000                                # envs/__init__.py
+    self_collision: bool = True
+
+
+SPECS: Dict[str, RobotSpec] = OrderedDict()
+
+
+def _add(s: RobotSpec):
+    SPECS[s.key] = s
+
+
+# InvertedPendulum: robot_pendula.py:5-51, gym_pendulum_envs.py:7-42, envs/__init__.py:4-9
+_add(RobotSpec("InvertedPendulumPyBulletEnv-v0", "pendulum", "inverted_pendulum.xml", "cart",
+               action_dim=1, obs_dim=5, kind=KIND_PENDULUM, power=1.0, alive=ALIVE_PENDULUM,
+               timestep=0.0165, frame_skip=1, floor=False))
+# Hopper: robot_locomotors.py:82-90, envs/__init__.py:73-78
+_add(RobotSpec("HopperPyBulletEnv-v0", "hopper", "hopper.xml", "torso", action_dim=3, obs_dim=15,
+               kind=KIND_WALKER, power=0.75, foot_list=["foot"], alive=ALIVE_HOPPER))
+# HalfCheetah: robot_locomotors.py:109-127, envs/__init__.py:59-64
+_add(RobotSpec("HalfCheetahPyBulletEnv-v0", "halfcheetah", "half_cheetah.xml", "torso", action_dim=6,
+               obs_dim=26, kind=KIND_WALKER, power=0.90,
+               foot_list=["ffoot", "fshin", "fthigh", "bfoot", "bshin", "bthigh"], alive=ALIVE_HALFCHEETAH,
+               power_coef={"bthigh": 120.0, "bshin": 90.0, "bfoot": 60.0, "fthigh": 140.0,
+                           "fshin": 60.0, "ffoot": 30.0}))
+# Ant: robot_locomotors.py:130-138, envs/__init__.py:66-71
+_add(RobotSpec("AntPyBulletEnv-v0", "ant", "ant.xml", "torso", action_dim=8, obs_dim=28,
+               kind=KIND_WALKER, power=2.5,
+               foot_list=["front_left_foot", "front_right_foot", "left_back_foot", "right_back_foot"],
+               alive=ALIVE_ANT))
+# Humanoid: robot_locomotors.py:141-192, gym_locomotion_envs.py:146-151, envs/__init__.py:80-84
+_add(RobotSpec("HumanoidPyBulletEnv-v0", "humanoid", "humanoid_symmetric.xml", "torso", action_dim=17,
+               obs_dim=44, kind=KIND_WALKER, power=0.41, foot_list=["right_foot", "left_foot"],
+               alive=ALIVE_HUMANOID,
+               motor_order=["abdomen_z", "abdomen_y", "abdomen_x",
+                            "right_hip_x", "right_hip_z", "right_hip_y", "right_knee",
+                            "left_hip_x", "left_hip_z", "left_hip_y", "left_knee",
+                            "right_shoulder1", "right_shoulder2", "right_elbow",
+                            "left_shoulder1", "left_shoulder2", "left_elbow"],
+               power_coef={"abdomen_z": 100, "abdomen_y": 100, "abdomen_x": 100,
+                           "right_hip_x": 100, "right_hip_z": 100, "right_hip_y": 300, "right_knee": 200,
+                           "left_hip_x": 100, "left_hip_z": 100, "left_hip_y": 300, "left_knee": 200,
+                           "right_shoulder1": 75, "right_shoulder2": 75, "right_elbow": 75,
+                           "left_shoulder1": 75, "left_shoulder2": 75, "left_elbow": 75},
+               initial_z=0.8, electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1))
+
+ENV_IDS = {s.env_id: s for s in SPECS.values()}
+
+
+def spec_for(name: str) -> RobotSpec:
+    if name in SPECS:
+        return SPECS[name]
+    if name in ENV_IDS:
+        return ENV_IDS[name]
+    raise KeyError(f"unknown robot/env id {name!r}; known: {list(ENV_IDS)}")
+
+
+def add_to_scene_order(model: mjcf.RobotModel, robot_name: str):
+    """Restates XmlBasedRobot.addToScene (robot_bases.py:54-91) on the compiled topology.
+
+    Returns (parts, ordered_joint_links, robot_body) where parts is an ordered mapping
+    part_name -> link index (-1 = base), in Python dict insertion order."""
+    parts: "OrderedDict[str, int]" = OrderedDict()
+    ordered: List[int] = []
+    robot_body: Optional[int] = None
+    for j, link in enumerate(model.links):
+        parts[link.name] = j                                   # :72
+        if link.name == robot_name:                            # :74-75
+            robot_body = j
+        if j == 0 and robot_body is None:                      # :77-79
+            parts[robot_name] = -1
+            robot_body = -1
+        if link.joint_name[:6] == "ignore":                    # :81-83
+            continue
+        if link.joint_name[:8] != "jointfix":                  # :85-89
+            ordered.append(j)
+    return parts, ordered, robot_body
+
+
+def reference_asset_dir() -> str:
+    return os.path.join("/root/reference", "pybulletgym", "envs", "assets", "mjcf")
