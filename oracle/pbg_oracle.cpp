@@ -674,6 +674,9 @@ int pbg_oracle_info(int robot, int* out) {
   return 0;
 }
 
+static void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, double* rew,
+                         uint8_t* done);
+
 // Walker pack: calc_state (robot_locomotors.py:31-64) + the reward/done part of
 // WalkerBaseBulletEnv._step (gym_locomotion_envs.py:59-114).  With act == NULL only the
 // calc_state half runs (reset path).
@@ -681,6 +684,11 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
+  if (m.kind == 1) {  // pendulum: jq/jqd = (hinge, slider)
+    pendulum_obs(in->jq[0], in->jqd[0], in->jq[1], in->jqd[1], out->obs, &out->reward, &out->done);
+    if (!in->act) { out->reward = 0; out->done = 0; }
+    return 0;
+  }
   // joints: np.array([...], dtype=float32) of (pos_rel, vel_scaled) pairs  (robot_bases.py:306-321)
   float j[2 * MAXD];
   for (int i = 0; i < m.NO; i++) {
@@ -771,14 +779,21 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
 
 // Pendulum pack: calc_state + reward/done (robot_pendula.py:27-51, gym_pendulum_envs.py:26-39).
 // obs is float64 in the reference; written here as float32 (the C-ABI's obs dtype).
-static void pendulum_pack(const double* s, float* obs, double* rew, uint8_t* done) {
-  const double* q = s + PBG_BASE_WORDS;
-  const double* qd = q + 2;
-  double theta = q[1], theta_dot = qd[1], x = q[0], vx = qd[0];
+static void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, double* rew,
+                         uint8_t* done) {
+  // robot_pendula.py:32-46: non-finite vx / theta / theta_dot are replaced by 0
+  if (!isfinite(vx)) vx = 0.0;
+  if (!isfinite(theta)) theta = 0.0;
+  if (!isfinite(theta_dot)) theta_dot = 0.0;
   obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
   obs[4] = (float)theta_dot;
   if (rew) *rew = 1.0;
   if (done) *done = fabs(theta) > 0.2;
+}
+static void pendulum_pack(const double* s, float* obs, double* rew, uint8_t* done) {
+  const double* q = s + PBG_BASE_WORDS;
+  const double* qd = q + 2;
+  pendulum_obs(q[1], qd[1], q[0], qd[0], obs, rew, done);
 }
 
 // Gather the pack inputs from a physical state.

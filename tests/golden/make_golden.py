@@ -1,0 +1,365 @@
+"""Generate the pack golden vectors from the reference's own Python.  Runs HERE only.
+
+The reference's WalkerBaseBulletEnv / InvertedPendulumBulletEnv (and everything they
+call: robot_bases.py, robot_locomotors.py, robot_pendula.py, env_bases.py,
+scene_bases.py, scene_stadium.py) is imported from /root/reference unchanged.  Its
+third-party dependencies are absent here, so they are replaced by stub modules:
+
+* ``gym`` (0.9.5-style: Env.reset -> _reset, spaces.Box, utils.seeding.np_random),
+* ``pybullet`` (constants plus getEulerFromQuaternion, restated from pybullet.c),
+* ``pybullet_envs.bullet.bullet_client`` and ``pybullet_data``,
+
+and the physics client is a scripted fake (``FakeClient``) that serves link / joint /
+base states and contact lists drawn from a seeded RNG in the robot topology of
+``pybullet-gym_amd/models/<robot>.json``.  Whatever the reference's Python computes from
+those physics queries -- observation, reward terms, done, feet_contact, potential --
+is recorded together with the exact inputs it read, into ``tests/golden/pack_<robot>.npz``.
+
+These vectors pin the observation/reward/done pack (SURVEY.md section 8a rows a3,
+a5-a15, Appendix C).  They do not pin the physics (pybullet is not available).
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True  # never write into /root/reference
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+MODELS = os.path.join(REPO, "pybullet-gym_amd", "models")
+
+ROBOTS = {
+    "pendulum": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedPendulumBulletEnv"),
+    "hopper": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HopperBulletEnv"),
+    "halfcheetah": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HalfCheetahBulletEnv"),
+    "ant": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "AntBulletEnv"),
+    "humanoid": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidBulletEnv"),
+}
+
+
+# ----------------------------------------------------------------------------- stubs
+def euler_from_quaternion(q):
+    """pybullet.getEulerFromQuaternion as written in pybullet.c (double precision)."""
+    x, y, z, w = [float(v) for v in q]
+    sqx, sqy, sqz, squ = x * x, y * y, z * z, w * w
+    roll = math.atan2(2 * (y * z + w * x), squ - sqx - sqy + sqz)
+    sarg = -2 * (x * z - w * y)
+    pitch = -0.5 * 3.141592538 if sarg <= -1.0 else (0.5 * 3.141592538 if sarg >= 1.0 else math.asin(sarg))
+    yaw = math.atan2(2 * (x * y + w * z), squ + sqx - sqy - sqz)
+    return (roll, pitch, yaw)
+
+
+def quaternion_from_euler(e):
+    r, p, y = e
+    cr, sr, cp, sp, cy, sy = (math.cos(r / 2), math.sin(r / 2), math.cos(p / 2), math.sin(p / 2),
+                              math.cos(y / 2), math.sin(y / 2))
+    return (sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+            cr * cp * cy + sr * sp * sy)
+
+
+def install_stubs():
+    gym = types.ModuleType("gym")
+    gym.__version__ = "0.9.5"
+
+    class Env:
+        def reset(self):
+            return self._reset()
+
+        def seed(self, seed=None):
+            return self._seed(seed)
+
+    gym.Env = Env
+    spaces = types.ModuleType("gym.spaces")
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low, self.high = np.asarray(low), np.asarray(high)
+            self.shape = self.low.shape
+
+    spaces.Box = Box
+    utils = types.ModuleType("gym.utils")
+    seeding = types.ModuleType("gym.utils.seeding")
+
+    def np_random(seed=None):
+        seed = 0 if seed is None else seed
+        return np.random.RandomState(seed), seed
+
+    seeding.np_random = np_random
+    utils.seeding = seeding
+    envs = types.ModuleType("gym.envs")
+    registration = types.ModuleType("gym.envs.registration")
+    registration.register = lambda **kw: None
+    envs.registration = registration
+    gym.spaces, gym.utils, gym.envs = spaces, utils, envs
+    for name, mod in [("gym", gym), ("gym.spaces", spaces), ("gym.utils", utils),
+                      ("gym.utils.seeding", seeding), ("gym.envs", envs),
+                      ("gym.envs.registration", registration)]:
+        sys.modules[name] = mod
+
+    pb = types.ModuleType("pybullet")
+    for i, c in enumerate(["POSITION_CONTROL", "VELOCITY_CONTROL", "TORQUE_CONTROL", "COV_ENABLE_RENDERING",
+                           "COV_ENABLE_GUI", "COV_ENABLE_PLANAR_REFLECTION", "GUI", "DIRECT",
+                           "ER_BULLET_HARDWARE_OPENGL"]):
+        setattr(pb, c, i)
+    pb.URDF_USE_SELF_COLLISION = 8
+    pb.URDF_USE_SELF_COLLISION_EXCLUDE_ALL_PARENTS = 16
+    pb.getEulerFromQuaternion = euler_from_quaternion
+    pb.getQuaternionFromEuler = quaternion_from_euler
+    sys.modules["pybullet"] = pb
+    pe = types.ModuleType("pybullet_envs")
+    pbb = types.ModuleType("pybullet_envs.bullet")
+    bc = types.ModuleType("pybullet_envs.bullet.bullet_client")
+
+    class BulletClient:  # replaced per env by FakeClient
+        def __init__(self, connection_mode=None):
+            raise RuntimeError("stub")
+
+    bc.BulletClient = BulletClient
+    pe.bullet, pbb.bullet_client = pbb, bc
+    sys.modules.update({"pybullet_envs": pe, "pybullet_envs.bullet": pbb,
+                        "pybullet_envs.bullet.bullet_client": bc})
+    pdata = types.ModuleType("pybullet_data")
+    pdata.getDataPath = lambda: "/nonexistent"
+    sys.modules["pybullet_data"] = pdata
+
+
+# ----------------------------------------------------------------------------- fake physics
+def rand_quat(rng, tilt):
+    yaw = rng.uniform(-math.pi, math.pi)
+    roll, pitch = rng.normal(0, tilt), rng.normal(0, tilt)
+    q = np.array(quaternion_from_euler((roll, pitch, yaw)))
+    if rng.random() < 0.3:
+        q = -q  # a quaternion and its negation are the same rotation
+    return tuple(float(v) for v in q)
+
+
+class FakeClient:
+    """Scripted stand-in for pybullet's BulletClient: serves seeded synthetic states."""
+
+    def __init__(self, t, rng):
+        self.t = t
+        self.rng = rng
+        self._client = 7
+        self.floor_uid, self.robot_uid = (0, 1) if t["floor"] else (-99, 0)
+        self.L = t["NL"]
+        self.q = np.zeros(self.L)
+        self.qd = np.zeros(self.L)
+        self.saved = None
+        self.new_state(initial=True)
+
+    # --- state script
+    def new_state(self, initial=False):
+        rng, L = self.rng, self.L
+        big = rng.random() < 0.1
+        self.base_pos = (float(rng.uniform(-3, 3) if not big else rng.choice([-2000.0, 1500.0, 999.5])),
+                         float(rng.uniform(-3, 3)), float(rng.uniform(0.05, 1.6)))
+        self.base_orn = rand_quat(rng, 0.9 if rng.random() < 0.3 else 0.2)
+        vs = 30.0 if rng.random() < 0.1 else 2.0
+        self.base_lin = tuple(float(v) for v in rng.normal(0, vs, 3))
+        self.base_ang = tuple(float(v) for v in rng.normal(0, 2.0, 3))
+        self.link_pos = [tuple(float(v) for v in np.array(self.base_pos) + rng.normal(0, 0.5, 3)) for _ in range(L)]
+        self.link_orn = [rand_quat(rng, 0.7) for _ in range(L)]
+        self.link_lin = [tuple(float(v) for v in rng.normal(0, vs, 3)) for _ in range(L)]
+        self.link_ang = [tuple(float(v) for v in rng.normal(0, 2, 3)) for _ in range(L)]
+        if not initial:
+            for j in range(L):
+                lo, hi = self.t["_lo"][j], self.t["_hi"][j]
+                if lo < hi:
+                    span = hi - lo
+                    self.q[j] = rng.uniform(lo - 0.3 * span, hi + 0.3 * span)
+                else:
+                    self.q[j] = rng.uniform(-4, 4)
+                self.qd[j] = rng.normal(0, 5.0) if rng.random() > 0.05 else rng.choice([-120.0, 80.0])
+            if rng.random() < 0.03:
+                self.qd[rng.integers(L)] = float("nan")
+        self.contacts = [int(rng.random() < 0.4) for _ in range(L)]
+        self.self_contacts = [int(rng.random() < 0.2) for _ in range(L)]
+
+    # --- world setup
+    def configureDebugVisualizer(self, *a, **k): pass
+    def setGravity(self, *a, **k): pass
+    def setDefaultContactERP(self, *a, **k): pass
+    def setPhysicsEngineParameter(self, *a, **k): pass
+    def changeDynamics(self, *a, **k): pass
+    def changeVisualShape(self, *a, **k): pass
+    def setJointMotorControl2(self, *a, **k): pass
+    def loadSDF(self, path): return (self.floor_uid,)
+    def loadMJCF(self, path, flags=0): return (self.robot_uid,)
+    def saveState(self): return 3
+    def restoreState(self, sid): self.q[:] = 0.0; self.qd[:] = 0.0
+    def stepSimulation(self): self.new_state()
+
+    def getNumJoints(self, uid):
+        return self.L if uid == self.robot_uid else 0
+
+    def getBodyInfo(self, uid):
+        return (b"floor", b"floor_obj") if uid == self.floor_uid else (b"base", self.t["key"].encode())
+
+    def getJointInfo(self, uid, j):
+        t = self.t
+        lo, hi = t["_lo"][j], t["_hi"][j]
+        return (j, t["_jname"][j].encode(), t["link_jtype"][j], 7 + j, 6 + j, 1, 0.0, 0.0, lo, hi, 0.0, 0.0,
+                t["link_name"][j].encode(), (0.0, 0.0, 1.0), (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), t["link_parent"][j])
+
+    # --- state queries
+    def resetJointState(self, uid, j, targetValue=0.0, targetVelocity=0.0):
+        self.q[j], self.qd[j] = targetValue, targetVelocity
+
+    def getJointState(self, uid, j):
+        return (float(self.q[j]), float(self.qd[j]), (0.0,) * 6, 0.0)
+
+    def getBasePositionAndOrientation(self, uid):
+        if uid == self.floor_uid:
+            return ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+        return (self.base_pos, self.base_orn)
+
+    def getBaseVelocity(self, uid):
+        return (self.base_lin, self.base_ang)
+
+    def getLinkState(self, uid, j, computeLinkVelocity=0):
+        out = (self.link_pos[j], self.link_orn[j], (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), self.link_pos[j], self.link_orn[j])
+        if computeLinkVelocity:
+            out = out + (self.link_lin[j], self.link_ang[j])
+        return out
+
+    def getContactPoints(self, bodyA, bodyB=-1, linkIndexA=-2, linkIndexB=-2):
+        pts = []
+        if linkIndexA >= 0 and self.contacts[linkIndexA]:
+            pts.append((0, bodyA, self.floor_uid, linkIndexA, -1, (0, 0, 0), (0, 0, 0), (0, 0, 1), 0.001, 1.0))
+        if linkIndexA >= 0 and self.self_contacts[linkIndexA]:  # robot-robot contact: must not count
+            pts.append((0, bodyA, self.robot_uid, linkIndexA, (linkIndexA + 1) % self.L, (0, 0, 0), (0, 0, 0),
+                        (0, 0, 1), 0.001, 1.0))
+        return pts
+
+
+# ----------------------------------------------------------------------------- driver
+def load_tables(key):
+    with open(os.path.join(MODELS, f"{key}.json")) as f:
+        t = json.load(f)
+    L = t["NL"]
+    t["_lo"], t["_hi"], t["_jname"] = [0.0] * L, [-1.0] * L, []
+    for j in range(L):
+        d = t["link_dof"][j]
+        if d >= 0 and t["dof_limited"][d]:
+            t["_lo"][j], t["_hi"][j] = t["dof_lower"][d], t["dof_upper"][d]
+    # joint names as pybullet reports them (getJointInfo[1])
+    import importlib
+    sys.path.insert(0, REPO)
+    pkg = importlib.import_module("pybulletgym_amd")
+    from pybulletgym_amd import mjcf, robots
+    spec = robots.spec_for(key)
+    model = mjcf.compile_mjcf(os.path.join(robots.reference_asset_dir(), spec.mjcf), key)
+    t["_jname"] = [l.joint_name for l in model.links]
+    return t
+
+
+def generate(key, episodes=3, steps=40, seed=1234):
+    modname, clsname = ROBOTS[key]
+    import importlib
+    envmod = importlib.import_module(modname)
+    env_bases = importlib.import_module("pybulletgym.envs.roboschool.env_bases")
+    t = load_tables(key)
+    rng = np.random.default_rng(seed)
+    fake = FakeClient(t, rng)
+    env_bases.bullet_client.BulletClient = lambda connection_mode=None: fake
+    env = getattr(envmod, clsname)()
+    robot = env.robot
+    rec = {k: [] for k in ("kind", "part_xyz", "n_parts", "body_quat", "body_pos", "body_vel", "jq", "jqd",
+                           "feet_prev", "feet_new", "act", "potential_old", "initial_z_in", "obs", "reward",
+                           "done", "potential", "feet_out", "initial_z_out", "rewards")}
+    part_names = []
+    captured = {}
+    calc_cls = type(robot)
+    orig_calc = calc_cls.calc_state
+
+    def spy_calc_state(self):
+        if t["kind"] == 0:
+            captured["part_xyz"] = np.array([p.pose().xyz() for p in self.parts.values()], dtype=np.float64)
+            captured["part_names"] = list(self.parts.keys())
+            captured["body_quat"] = np.array(self.robot_body.pose().orientation(), dtype=np.float64)
+            captured["body_pos"] = np.array(self.robot_body.pose().xyz(), dtype=np.float64)
+            captured["body_vel"] = np.array(self.robot_body.speed(), dtype=np.float64)
+            js = [j.get_state() for j in self.ordered_joints]
+            captured["jq"] = np.array([s[0] for s in js]); captured["jqd"] = np.array([s[1] for s in js])
+            captured["feet_prev"] = np.array(self.feet_contact, dtype=np.float32)
+            captured["initial_z_in"] = np.nan if self.initial_z is None else float(self.initial_z)
+        else:
+            captured["jq"] = np.array([self.j1.get_state()[0], self.slider.get_state()[0]])
+            captured["jqd"] = np.array([self.j1.get_state()[1], self.slider.get_state()[1]])
+        return orig_calc(self)
+
+    calc_cls.calc_state = spy_calc_state
+    NPMAX = t["NP"] + 1
+    nf = max(1, t["NF"])
+
+    def push(kind, act, pot_old, obs, reward, done):
+        rec["kind"].append(kind)
+        if t["kind"] == 0:
+            px = np.zeros((NPMAX, 3))
+            n = len(captured["part_xyz"])
+            px[:n] = captured["part_xyz"]
+            rec["part_xyz"].append(px); rec["n_parts"].append(n)
+            for k in ("body_quat", "body_pos", "body_vel"):
+                rec[k].append(captured[k])
+            fp = np.zeros(nf, np.float32); fp[:t["NF"]] = captured["feet_prev"]
+            rec["feet_prev"].append(fp)
+            fo = np.zeros(nf, np.float32); fo[:t["NF"]] = robot.feet_contact
+            rec["feet_out"].append(fo)
+            fn = np.zeros(nf, np.uint8)
+            for i, f in enumerate(robot.foot_list):
+                fn[i] = fake.contacts[t["link_name"].index(f)]
+            rec["feet_new"].append(fn)
+            rec["initial_z_in"].append(captured["initial_z_in"])
+            rec["initial_z_out"].append(float(robot.initial_z))
+            part_names.append(captured["part_names"])
+        rec["jq"].append(captured["jq"]); rec["jqd"].append(captured["jqd"])
+        rec["act"].append(np.zeros(t["NA"], np.float32) if act is None else act)
+        rec["potential_old"].append(pot_old)
+        rec["obs"].append(np.asarray(obs))
+        rec["reward"].append(reward)
+        rec["done"].append(bool(done))
+        rec["potential"].append(float(getattr(env, "potential", 0.0)))
+        rw = getattr(env, "rewards", [0.0] * 5)
+        rr = np.zeros(5); rr[:len(rw)] = rw
+        rec["rewards"].append(rr)
+
+    arng = np.random.default_rng(seed + 1)
+    for ep in range(episodes):
+        obs = env.reset()
+        push(0, None, np.nan, obs, 0.0, False)
+        for s in range(steps):
+            if arng.random() < 0.05:
+                a = np.zeros(t["NA"], np.float32)
+            else:
+                a = arng.uniform(-1.5, 1.5, t["NA"]).astype(np.float32)
+            pot_old = float(getattr(env, "potential", 0.0))
+            obs, r, done, info = env.step(a)
+            push(1, a, pot_old, obs, float(r), done)
+    calc_cls.calc_state = orig_calc
+    out = {k: np.array(v) for k, v in rec.items() if len(v)}
+    out["part_names"] = np.array(["|".join(p) for p in part_names]) if part_names else np.array([])
+    out["numpy_version"] = np.array(np.__version__)
+    return out
+
+
+def main():
+    install_stubs()
+    sys.path.insert(0, REF)
+    for key in ROBOTS:
+        data = generate(key)
+        path = os.path.join(HERE, f"pack_{key}.npz")
+        np.savez_compressed(path, **data)
+        print(key, "calls", len(data["kind"]), "->", os.path.relpath(path, REPO))
+
+
+if __name__ == "__main__":
+    main()

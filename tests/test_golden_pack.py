@@ -1,0 +1,66 @@
+"""The oracle's observation/reward/done pack against golden vectors produced by the
+reference's own Python (tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+WALKERS = ["hopper", "halfcheetah", "ant", "humanoid"]
+
+
+def load(key):
+    return np.load(os.path.join(GOLDEN, f"pack_{key}.npz"))
+
+
+@pytest.mark.parametrize("key", WALKERS)
+def test_part_order_matches_reference(key):
+    """robot.parts dict order as the reference built it == the compiled part_link order."""
+    g = load(key)
+    t = __import__("json").load(open(os.path.join(os.path.dirname(__file__), "..", "pybullet-gym_amd",
+                                                  "models", f"{key}.json")))
+    first = g["part_names"][0].split("|")
+    later = g["part_names"][1].split("|")
+    assert first == t["part_names"]                 # first reset: before the floor joins
+    assert later == t["part_names"] + ["floor"]      # afterwards: floor appended
+
+
+@pytest.mark.parametrize("key", WALKERS)
+def test_oracle_pack_bit_exact(key):
+    g = load(key)
+    n = len(g["kind"])
+    for i in range(n):
+        step = g["kind"][i] == 1
+        out = oracle.pack(key, g["part_xyz"][i][: g["n_parts"][i]], g["body_quat"][i], g["body_pos"][i],
+                          g["body_vel"][i], g["jq"][i], g["jqd"][i], g["feet_prev"][i],
+                          g["feet_new"][i] if step else None, g["act"][i] if step else None,
+                          g["potential_old"][i], g["initial_z_in"][i])
+        ref_obs = g["obs"][i].astype(np.float32)
+        assert out["obs"].dtype == np.float32
+        np.testing.assert_array_equal(out["obs"].view(np.uint32), ref_obs.view(np.uint32), err_msg=f"call {i}")
+        assert out["potential"] == pytest.approx(g["potential"][i], abs=1e-9, rel=0)
+        assert out["initial_z"] == g["initial_z_out"][i]
+        if step:
+            assert out["done"] == bool(g["done"][i]), f"call {i}"
+            # reward is a float64 sum; tolerance covers BLAS dot ordering in linalg.norm
+            assert out["reward"] == pytest.approx(g["reward"][i], abs=1e-9, rel=0, nan_ok=True), f"call {i}"
+            np.testing.assert_allclose(out["rewards"], g["rewards"][i], atol=1e-9, rtol=0, equal_nan=True)
+            np.testing.assert_array_equal(out["feet"], g["feet_out"][i][: len(out["feet"])])
+
+
+def test_oracle_pack_pendulum():
+    """robot_pendula.py:27-51 + gym_pendulum_envs.py:26-39.  The reference's obs is float64;
+    the C-ABI carries float32, so the check is f32(reference) bit-exact."""
+    g = load("pendulum")
+    for i in range(len(g["kind"])):
+        step = g["kind"][i] == 1
+        out = oracle.pack("pendulum", np.zeros((1, 3)), np.zeros(4), np.zeros(3), np.zeros(3), g["jq"][i],
+                          g["jqd"][i], np.zeros(1), np.zeros(1) if step else None, g["act"][i] if step else None,
+                          0.0, 0.0)
+        ref = g["obs"][i].astype(np.float32)
+        np.testing.assert_array_equal(out["obs"].view(np.uint32), ref.view(np.uint32))
+        if step:
+            assert out["done"] == bool(g["done"][i])
+            assert out["reward"] == g["reward"][i]
