@@ -1,0 +1,108 @@
+/* pbg.h -- C-ABI of the MI355X batched locomotion stepper (libpbg_amd.so).
+ *
+ * The reference (josiahls/pybullet-gym) has no native boundary of its own: its hot path
+ * calls the pybullet C extension once per query, per env, through
+ * pybullet_envs.bullet.bullet_client.BulletClient (pybulletgym/envs/roboschool/
+ * env_bases.py:4,51-56).  This ABI replaces that whole per-env call sequence with one
+ * batched call per env step.  Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (HIP / PyTorch-ROCm tensors), row-major,
+ *     except where marked "host".  The caller owns every I/O buffer; the handle owns its
+ *     struct-of-arrays state.  Nothing allocates or synchronises inside step/reset.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream); work is async on it.
+ *   - Return 0 on success, a negative PBG_E_* code on failure; pbg_last_error() gives
+ *     the message (thread-local).
+ *   - One handle = the envs of one GPU.  Multi-GPU: one handle per rank, env_offset =
+ *     global index of the rank's first env (reset RNG streams depend on the global id).
+ */
+#ifndef PBG_H
+#define PBG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBG_OK 0
+#define PBG_E_ARG (-1)
+#define PBG_E_ENV (-2)
+#define PBG_E_HIP (-3)
+#define PBG_E_NOMEM (-4)
+
+typedef struct pbg_handle pbg_handle;
+
+typedef struct {
+  int robot_id;          /* 0 pendulum, 1 hopper, 2 halfcheetah, 3 ant, 4 humanoid */
+  int n_envs;
+  int action_dim;        /* action_space.shape[0]   (robot_bases.py:24-25) */
+  int obs_dim;           /* observation_space.shape[0] (robot_bases.py:26-27) */
+  int n_dof;             /* generalized velocities (6 floating-base + joint dofs) */
+  int n_joints;          /* joint dofs incl. `ignore*` joints */
+  int n_links;
+  int n_feet;
+  int state_words;       /* per-env physical state record (see pbg_get_state) */
+  int aux_words;         /* per-env bookkeeping record (see pbg_get_state) */
+  int substeps;          /* stepSimulation sub-steps per env step (scene_bases.py:65) */
+  int max_episode_steps; /* gym TimeLimit (envs/__init__.py) */
+  int reset_dofs;        /* joints randomised by reset (robot_locomotors.py:18-19) */
+  int floating;
+} pbg_info_t;
+
+typedef struct {
+  const float* act;   /* [n, action_dim] float32 */
+  float* obs;         /* [n, obs_dim] float32: next observation (post-reset if auto-reset) */
+  float* rew;         /* [n] float32 reward (computed in float64) */
+  uint8_t* done;      /* [n] terminated | truncated */
+  double* rew64;      /* nullable [n] float64 reward */
+  uint8_t* trunc;     /* nullable [n] TimeLimit truncation flag */
+  float* term_obs;    /* nullable [n, obs_dim] observation before an auto-reset */
+  int32_t* ncontact;  /* nullable [n] contact points in the last sub-step */
+  int autoreset;      /* reset envs that finished, inside the same launch */
+} pbg_step_io_t;
+
+/* gym.make(env_id) for n envs (envs/__init__.py:4-103 registry entries; the env's
+ * physics client is created here instead of lazily in BaseBulletEnv._reset,
+ * env_bases.py:46-56).  env_id: "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0",
+ * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "InvertedPendulumPyBulletEnv-v0". */
+int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out);
+/* BaseBulletEnv._close (env_bases.py:103-107) */
+void pbg_destroy(pbg_handle* h);
+/* action_space / observation_space / model sizes (robot_bases.py:24-27) */
+int pbg_info(const pbg_handle* h, pbg_info_t* out);
+
+/* WalkerBaseBulletEnv._reset (gym_locomotion_envs.py:22-39) + BaseBulletEnv._reset
+ * (env_bases.py:46-71) + robot_specific_reset (robot_locomotors.py:16-24):
+ * restoreState snapshot, resetJointState(U(-0.1,0.1)) on the ordered joints, calc_state.
+ * mask: nullable [n] uint8 (NULL = all envs).  init_q: nullable [n, reset_dofs] float32
+ * joint positions to use instead of the RNG (trace replay).  obs: [n, obs_dim]. */
+int pbg_reset(pbg_handle* h, const uint8_t* mask, const float* init_q, float* obs, void* stream);
+
+/* WalkerBaseBulletEnv._step (gym_locomotion_envs.py:54-114): apply_action
+ * (robot_locomotors.py:26-29) -> stepSimulation x substeps (scene_bases.py:75-76) ->
+ * calc_state / potential / alive / feet contacts / costs.  No auto-reset. */
+int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* done, void* stream);
+/* pbg_step with optional outputs and in-launch auto-reset (gym TimeLimit + reset). */
+int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
+
+/* pybullet saveState/restoreState (gym_locomotion_envs.py:25,36) generalised to trace
+ * replay / teacher forcing.  phys: [n, state_words] float64 records
+ *   [0..2] base COM pos, [3..6] base quat (x,y,z,w), [7..9] base COM lin vel (world),
+ *   [10..12] base ang vel (world), then q[n_joints], qd[n_joints];
+ * aux: [n, aux_words] float64 = [potential, initial_z, elapsed_steps, floor_in_parts,
+ *   feet_contact[n_feet]]  (aux may be NULL in set_state). */
+int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream);
+int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream);
+
+/* The observation/reward/done pack alone (calc_state + the reward half of _step) on
+ * explicit inputs, for golden-vector parity; layouts in pbg_pack_record_sizes. */
+int pbg_pack_record_sizes(const char* env_id, int* in_words, int* out_words);
+int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, void* stream);
+
+const char* pbg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBG_H */

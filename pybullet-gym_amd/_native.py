@@ -1,0 +1,80 @@
+"""ctypes binding of libpbg_amd.so (include/pbg.h).
+
+The library is the product: there is no CPU fallback.  If it is missing or fails to
+load, every entry point raises -- build it with ``python __graft_entry__.py`` (or
+``make -C pybullet-gym_amd``)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpbg_amd.so")
+
+ROBOT_IDS = {"InvertedPendulumPyBulletEnv-v0": 0, "HopperPyBulletEnv-v0": 1, "HalfCheetahPyBulletEnv-v0": 2,
+             "AntPyBulletEnv-v0": 3, "HumanoidPyBulletEnv-v0": 4}
+
+
+class PbgError(RuntimeError):
+    pass
+
+
+class Info(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "robot_id", "n_envs", "action_dim", "obs_dim", "n_dof", "n_joints", "n_links", "n_feet", "state_words",
+        "aux_words", "substeps", "max_episode_steps", "reset_dofs", "floating")]
+
+
+class StepIO(ctypes.Structure):
+    _fields_ = [("act", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("rew", ctypes.c_void_p),
+                ("done", ctypes.c_void_p), ("rew64", ctypes.c_void_p), ("trunc", ctypes.c_void_p),
+                ("term_obs", ctypes.c_void_p), ("ncontact", ctypes.c_void_p), ("autoreset", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libpbg_amd.so, failing loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PbgError(f"{LIB_PATH} not found: the HIP extension is not built "
+                       "(run `python __graft_entry__.py` or `make -C pybullet-gym_amd`)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, H = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
+    L.pbg_create.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(H)]
+    L.pbg_create.restype = I
+    L.pbg_destroy.argtypes = [H]
+    L.pbg_destroy.restype = None
+    L.pbg_info.argtypes = [H, ctypes.POINTER(Info)]
+    L.pbg_reset.argtypes = [H, P, P, P, P]
+    L.pbg_step.argtypes = [H, P, P, P, P, P]
+    L.pbg_step_ex.argtypes = [H, ctypes.POINTER(StepIO), P]
+    L.pbg_get_state.argtypes = [H, P, P, P]
+    L.pbg_set_state.argtypes = [H, P, P, P]
+    L.pbg_pack_record_sizes.argtypes = [ctypes.c_char_p, ctypes.POINTER(I), ctypes.POINTER(I)]
+    L.pbg_pack.argtypes = [ctypes.c_char_p, I, P, P, P]
+    L.pbg_last_error.restype = ctypes.c_char_p
+    for f in ("pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state", "pbg_set_state",
+              "pbg_pack_record_sizes", "pbg_pack"):
+        getattr(L, f).restype = I
+    _lib = L
+    return L
+
+
+EXPORTED = ("pbg_create", "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state",
+            "pbg_set_state", "pbg_pack_record_sizes", "pbg_pack", "pbg_last_error")
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().pbg_last_error().decode(errors="replace")
+        raise PbgError(f"{what} failed ({rc}): {msg}")
+
+
+def env_id_bytes(env_id: str) -> bytes:
+    if env_id not in ROBOT_IDS:
+        raise PbgError(f"unknown env id {env_id!r}; known: {sorted(ROBOT_IDS)}")
+    return env_id.encode()

@@ -104,6 +104,17 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
                     continue
                 pairs.append((la, ga, lb, gb))
 
+    # unique geoms referenced by pairs (for the kernel's per-geom world endpoints)
+    pgeoms = []
+    def gid(li, g):
+        for k, (l2, g2) in enumerate(pgeoms):
+            if l2 == li and g2 is g:
+                return k
+        pgeoms.append((li, g))
+        return len(pgeoms) - 1
+    pair_ga = [gid(p[0], p[1]) for p in pairs]
+    pair_gb = [gid(p[2], p[3]) for p in pairs]
+
     feet = [model.link_index(f) for f in spec.foot_list]
     inertia6 = lambda I: [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
     t = dict(
@@ -140,6 +151,9 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         pair_b0=[list(p[3].p0) for p in pairs], pair_b1=[list(p[3].p1) for p in pairs],
         pair_ra=[p[1].radius for p in pairs], pair_rb=[p[3].radius for p in pairs],
         pair_mu=[p[1].friction * p[3].friction for p in pairs],
+        NG=len(pgeoms), geom_link=[g[0] for g in pgeoms], geom_p0=[list(g[1].p0) for g in pgeoms],
+        geom_p1=[list(g[1].p1) for g in pgeoms], geom_r=[g[1].radius for g in pgeoms],
+        pair_ga=pair_ga, pair_gb=pair_gb,
     )
     return t
 
@@ -190,7 +204,7 @@ def emit_struct(t: Dict) -> str:
          f"  static constexpr int robot_id = {ROBOT_IDS[t['key']]};",
          f"  static constexpr int kind = {t['kind']};",
          f"  static constexpr bool floating = {'true' if t['floating'] else 'false'};"]
-    for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "OBS", "alive", "substeps",
+    for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "NG", "OBS", "alive", "substeps",
               "floor", "max_episode_steps", "robot_body"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
@@ -228,6 +242,12 @@ def emit_struct(t: Dict) -> str:
         L.append(_arr2(k, "double", t[k], 3))
     for k in ("pair_ra", "pair_rb", "pair_mu"):
         L.append(_arr1(k, "double", t[k]))
+    L.append(_arr1("pair_ga", "int", t["pair_ga"]))
+    L.append(_arr1("pair_gb", "int", t["pair_gb"]))
+    L.append(_arr1("geom_link", "int", t["geom_link"]))
+    L.append(_arr2("geom_p0", "double", t["geom_p0"], 3))
+    L.append(_arr2("geom_p1", "double", t["geom_p1"], 3))
+    L.append(_arr1("geom_r", "double", t["geom_r"]))
     L.append("};")
     return "\n".join(L)
 

@@ -1,0 +1,106 @@
+// Small fixed-size vector / matrix helpers and Philox4x32-10 for the step kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PBG_DEV __device__ __forceinline__
+
+struct f3 {
+  float x, y, z;
+};
+PBG_DEV f3 mk3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+PBG_DEV f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PBG_DEV f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PBG_DEV f3 operator-(f3 a) { return mk3(-a.x, -a.y, -a.z); }
+PBG_DEV f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
+PBG_DEV f3& operator+=(f3& a, f3 b) { a.x += b.x; a.y += b.y; a.z += b.z; return a; }
+PBG_DEV float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PBG_DEV f3 cross3(f3 a, f3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+PBG_DEV float norm3(f3 a) { return sqrtf(dot3(a, a)); }
+
+// row-major 3x3
+struct m3 {
+  float m[9];
+};
+PBG_DEV f3 mul(const m3& A, f3 v) {
+  return mk3(A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
+             A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z);
+}
+PBG_DEV m3 mul(const m3& A, const m3& B) {
+  m3 C;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      C.m[3 * i + j] = A.m[3 * i] * B.m[j] + A.m[3 * i + 1] * B.m[3 + j] + A.m[3 * i + 2] * B.m[6 + j];
+  return C;
+}
+PBG_DEV m3 quat_to_m3(float x, float y, float z, float w) {
+  m3 R;
+  R.m[0] = 1 - 2 * (y * y + z * z); R.m[1] = 2 * (x * y - w * z); R.m[2] = 2 * (x * z + w * y);
+  R.m[3] = 2 * (x * y + w * z); R.m[4] = 1 - 2 * (x * x + z * z); R.m[5] = 2 * (y * z - w * x);
+  R.m[6] = 2 * (x * z - w * y); R.m[7] = 2 * (y * z + w * x); R.m[8] = 1 - 2 * (x * x + y * y);
+  return R;
+}
+// rotation by angle about a unit axis given by compile-time constants
+PBG_DEV m3 axis_angle_m3(float ax, float ay, float az, float ang) {
+  float s, c;
+  sincosf(ang, &s, &c);
+  float t = 1 - c;
+  m3 R;
+  R.m[0] = t * ax * ax + c;      R.m[1] = t * ax * ay - s * az; R.m[2] = t * ax * az + s * ay;
+  R.m[3] = t * ax * ay + s * az; R.m[4] = t * ay * ay + c;      R.m[5] = t * ay * az - s * ax;
+  R.m[6] = t * ax * az - s * ay; R.m[7] = t * ay * az + s * ax; R.m[8] = t * az * az + c;
+  return R;
+}
+
+// symmetric 3x3 stored (xx, yy, zz, xy, xz, yz)
+struct s6 {
+  float a[6];
+};
+PBG_DEV f3 mul(const s6& S, f3 v) {
+  return mk3(S.a[0] * v.x + S.a[3] * v.y + S.a[4] * v.z, S.a[3] * v.x + S.a[1] * v.y + S.a[5] * v.z,
+             S.a[4] * v.x + S.a[5] * v.y + S.a[2] * v.z);
+}
+// R I R^T for body-frame inertia I6 (double constants)
+PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
+  float I[9] = {(float)I6[0], (float)I6[3], (float)I6[4], (float)I6[3], (float)I6[1],
+                (float)I6[5], (float)I6[4], (float)I6[5], (float)I6[2]};
+  float RI[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      RI[3 * i + j] = R.m[3 * i] * I[j] + R.m[3 * i + 1] * I[3 + j] + R.m[3 * i + 2] * I[6 + j];
+  s6 W;
+  W.a[0] = RI[0] * R.m[0] + RI[1] * R.m[1] + RI[2] * R.m[2];
+  W.a[1] = RI[3] * R.m[3] + RI[4] * R.m[4] + RI[5] * R.m[5];
+  W.a[2] = RI[6] * R.m[6] + RI[7] * R.m[7] + RI[8] * R.m[8];
+  W.a[3] = RI[0] * R.m[3] + RI[1] * R.m[4] + RI[2] * R.m[5];
+  W.a[4] = RI[0] * R.m[6] + RI[1] * R.m[7] + RI[2] * R.m[8];
+  W.a[5] = RI[3] * R.m[6] + RI[4] * R.m[7] + RI[5] * R.m[8];
+  return W;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u4 {
+  uint32_t x, y, z, w;
+};
+PBG_DEV u4 philox4x32_10(u4 ctr, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, ctr.x), lo0 = 0xD2511F53u * ctr.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, ctr.z), lo1 = 0xCD9E8D57u * ctr.z;
+    u4 n;
+    n.x = hi1 ^ ctr.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ ctr.w ^ k1;
+    n.w = lo0;
+    ctr = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return ctr;
+}
+// uniform in [0, 1) with 24 random bits
+PBG_DEV float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }

@@ -1,0 +1,1146 @@
+// pbg_step.hip -- batched locomotion-env step on MI355X (gfx950).
+//
+// Replaces, for N envs at once, the reference's per-env hot path
+//   WalkerBaseBulletEnv._step (pybulletgym/envs/roboschool/gym_locomotion_envs.py:54-114)
+//     -> robot.apply_action            (robot_locomotors.py:26-29; Humanoid :185-189)
+//     -> scene.global_step -> World.step -> pybullet.stepSimulation  (scene_bases.py:47-52,75-76)
+//     -> robot.calc_state / calc_potential / alive_bonus / feet contacts / costs  (:59-114)
+// and the reset path WalkerBaseBulletEnv._reset (gym_locomotion_envs.py:22-39).
+//
+// Design: one lane per env, robot topology baked in at compile time
+// (template on the generated tables of models_gen.h, every link/dof loop unrolled so
+// link state stays in VGPRs), struct-of-arrays float32 state in HBM ([word][env],
+// coalesced), float64 only for the numpy-exact observation/reward pack and the
+// potential.  Physics per sub-step: joint-space Featherstone dynamics (composite
+// rigid-body mass matrix about a robot-local reference point + recursive Newton-Euler
+// bias), sparsity-preserving Cholesky (leaf-first dof order, no fill-in), Bullet-style
+// sequential-impulse PGS run in Cholesky-transformed velocity space u = L^T nu (one
+// vector per constraint row), semi-implicit Euler.  Same algorithm as the CPU oracle
+// (oracle/pbg_oracle.cpp), which is the parity reference.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "models_gen.h"
+#include "pbg_math.h"
+#include "sim_params.h"
+
+namespace pbg {
+
+// ------------------------------------------------------------------ compile-time model facts
+template <class R>
+struct Dims {
+  static constexpr int NL = R::NL, NJ = R::NJ, NB = R::NL + 1, NDOF = R::NDOF;
+  static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;
+  static constexpr int NC = R::NS + R::NPAIR;  // contact capacity
+  static constexpr int count_limited() {
+    int c = 0;
+    for (int d = 0; d < R::NJ; d++) c += R::dof_limited[d];
+    return c;
+  }
+  static constexpr int NLIM = count_limited();
+  static constexpr int MAXROWS = 2 * NLIM + 3 * NC;
+  // GPU generalized-velocity order: joint dofs leaf-first (reverse preorder), base last.
+  static constexpr int gj(int d) { return NJ - 1 - d; }
+  static constexpr int gb(int k) { return NJ + k; }
+  // generalized index -> joint dof (or -1 for a base dof)
+  static constexpr int dof_of(int g) { return g < NJ ? NJ - 1 - g : -1; }
+  // joint dof d moves link l
+  static constexpr bool moves(int d, int l) { return l >= 0 && ((R::link_chain_mask[l] >> d) & 1u); }
+  // generalized indices i, k coupled in M (one's link is an ancestor-or-self of the other's)
+  static constexpr bool coupled(int i, int k) {
+    int di = dof_of(i), dk = dof_of(k);
+    if (di < 0 || dk < 0) return true;
+    return moves(di, R::dof_link[dk]) || moves(dk, R::dof_link[di]);
+  }
+  // generalized index g enters the Jacobian of a point on link l (-1 = base)
+  static constexpr bool in_chain(int g, int l) {
+    int d = dof_of(g);
+    if (d < 0) return true;
+    return moves(d, l);
+  }
+  // reference point body: base COM (floating) or the robot_body link COM (fixed base)
+  static constexpr int REF_BODY = R::floating ? 0 : R::robot_body + 1;
+};
+
+// ------------------------------------------------------------------ state record in registers
+template <class R>
+struct State {
+  float bp[3], bq[4], bv[3], bw[3];
+  float q[R::NJ > 0 ? R::NJ : 1], qd[R::NJ > 0 ? R::NJ : 1];
+};
+
+template <class R>
+PBG_DEV void load_state(State<R>& s, const float* __restrict__ st, int n, int e) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bp[i] = st[(size_t)i * n + e];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.bq[i] = st[(size_t)(3 + i) * n + e];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bv[i] = st[(size_t)(7 + i) * n + e];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bw[i] = st[(size_t)(10 + i) * n + e];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) s.q[d] = st[(size_t)(PBG_BASE_WORDS + d) * n + e];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) s.qd[d] = st[(size_t)(PBG_BASE_WORDS + R::NJ + d) * n + e];
+}
+template <class R>
+PBG_DEV void store_state(const State<R>& s, float* __restrict__ st, int n, int e) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) st[(size_t)i * n + e] = s.bp[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) st[(size_t)(3 + i) * n + e] = s.bq[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) st[(size_t)(7 + i) * n + e] = s.bv[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) st[(size_t)(10 + i) * n + e] = s.bw[i];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) st[(size_t)(PBG_BASE_WORDS + d) * n + e] = s.q[d];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) st[(size_t)(PBG_BASE_WORDS + R::NJ + d) * n + e] = s.qd[d];
+}
+
+// load snapshot (gym_locomotion_envs.py:23-25 restoreState) + reset noise on reset dofs
+template <class R>
+PBG_DEV void snapshot_state(State<R>& s) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bp[i] = (float)R::base_pos[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.bq[i] = (float)R::base_quat[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) { s.bv[i] = 0.f; s.bw[i] = 0.f; }
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) { s.q[d] = 0.f; s.qd[d] = 0.f; }
+}
+
+// ------------------------------------------------------------------ kinematics
+template <class R>
+struct Kin {
+  static constexpr int NB = R::NL + 1;
+  m3 Rm[NB];
+  f3 x[NB], c[NB];
+};
+template <class R>
+struct KinVel {
+  static constexpr int NB = R::NL + 1;
+  f3 w[NB], v[NB], al[NB], ac[NB];
+};
+
+// Forward kinematics (positions only).
+template <class R>
+PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
+  k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+  k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  k.c[0] = k.x[0];
+#pragma unroll
+  for (int l = 0; l < R::NL; l++) {
+    const int p = R::link_parent[l] + 1;
+    const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
+                             (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
+    const m3 R0 = mul(k.Rm[p], Ro);
+    const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
+                                            (float)R::link_offset_pos[l][2]));
+    const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
+    const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
+    const int jt = R::link_jtype[l], d = R::link_dof[l];
+    if (jt == 0) {
+      const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, s.q[d]);
+      k.Rm[l + 1] = mul(R0, Rj);
+      k.x[l + 1] = x0 + mul(R0, anl - mul(Rj, anl));
+    } else if (jt == 1) {
+      k.Rm[l + 1] = R0;
+      k.x[l + 1] = x0 + mul(R0, s.q[d] * axl);
+    } else {
+      k.Rm[l + 1] = R0;
+      k.x[l + 1] = x0;
+    }
+    k.c[l + 1] = k.x[l + 1] + mul(k.Rm[l + 1], mk3((float)R::link_com[l][0], (float)R::link_com[l][1],
+                                                  (float)R::link_com[l][2]));
+  }
+}
+
+// ------------------------------------------------------------------ per-substep scratch
+// Constraint rows live in a device workspace laid out [word][env] so that every lane's
+// access to "its" row word is one coalesced 256-B wave access.
+template <class R>
+struct Rows {
+  static constexpr int N = R::NDOF;
+  static constexpr int MR = Dims<R>::MAXROWS > 0 ? Dims<R>::MAXROWS : 1;
+  static constexpr int NC = Dims<R>::NC > 0 ? Dims<R>::NC : 1;
+  static constexpr int O_MEFF = MR * N, O_TGT = O_MEFF + MR, O_LAM = O_TGT + MR, O_HI = O_LAM + MR;
+  static constexpr int O_MU = O_HI + MR, WORDS = O_MU + NC;
+  float* __restrict__ base;  // already offset by env e
+  int n;
+  PBG_DEV float& y(int r, int i) const { return base[(size_t)(r * N + i) * n]; }
+  PBG_DEV float& meff(int r) const { return base[(size_t)(O_MEFF + r) * n]; }
+  PBG_DEV float& target(int r) const { return base[(size_t)(O_TGT + r) * n]; }
+  PBG_DEV float& lam(int r) const { return base[(size_t)(O_LAM + r) * n]; }
+  PBG_DEV float& hi(int r) const { return base[(size_t)(O_HI + r) * n]; }
+  PBG_DEV float& mu(int c) const { return base[(size_t)(O_MU + c) * n]; }
+};
+
+// ------------------------------------------------------------------ one physics sub-step
+// tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
+// of this sub-step's collision pass (feet contacts come from the last sub-step).
+template <class R>
+PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R>& rw) {
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
+  constexpr float dt = (float)R::dt_sub;
+  constexpr float g = (float)PBG_GRAVITY;
+
+  Kin<R> k;
+  fk_pos<R>(s, k);
+
+  // --- velocities, bias accelerations, joint axes (world) ------------------------------
+  f3 w[NB], v[NB], al[NB], ac[NB];
+  f3 ja[NJ > 0 ? NJ : 1], jo[NJ > 0 ? NJ : 1];
+  w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
+  v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
+  al[0] = mk3(0, 0, 0);
+  ac[0] = mk3(0, 0, 0);
+#pragma unroll
+  for (int l = 0; l < R::NL; l++) {
+    const int p = R::link_parent[l] + 1;
+    const int jt = R::link_jtype[l], d = R::link_dof[l];
+    const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
+    const f3 c = k.c[l + 1];
+    if (jt == 0 || jt == 1) {
+      // R0 = Rm[p] * Ro ; axis/anchor fixed in the parent
+      const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
+                               (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
+      const m3 R0 = mul(k.Rm[p], Ro);
+      const f3 a = mul(R0, mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]));
+      const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
+                                              (float)R::link_offset_pos[l][2]));
+      ja[d] = a;
+      if (jt == 0) {
+        const f3 o = x0 + mul(R0, mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1],
+                                      (float)R::link_anchor[l][2]));
+        jo[d] = o;
+        const f3 ro = o - cp;
+        const f3 vo = vp + cross3(wp, ro);
+        const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+        const f3 wl = wp + s.qd[d] * a;
+        const f3 all = alp + s.qd[d] * cross3(wp, a);
+        const f3 rc = c - o;
+        w[l + 1] = wl;
+        al[l + 1] = all;
+        v[l + 1] = vo + cross3(wl, rc);
+        ac[l + 1] = ao + cross3(all, rc) + cross3(wl, cross3(wl, rc));
+      } else {
+        jo[d] = x0;
+        const f3 r = c - cp;
+        w[l + 1] = wp;
+        al[l + 1] = alp;
+        v[l + 1] = vp + cross3(wp, r) + s.qd[d] * a;
+        ac[l + 1] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * s.qd[d]) * cross3(wp, a);
+      }
+    } else {
+      const f3 r = c - cp;
+      w[l + 1] = wp;
+      al[l + 1] = alp;
+      v[l + 1] = vp + cross3(wp, r);
+      ac[l + 1] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
+    }
+  }
+
+  // --- composite inertia + wrench per body about the reference point O -----------------
+  const f3 O = k.c[D::REF_BODY];
+  float cm[NB];
+  f3 cp1[NB], cF[NB], cN[NB];
+  s6 cJ[NB];
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    const double mb = b == 0 ? R::base_mass : R::link_mass[b - 1];
+    const double* I6 = b == 0 ? R::base_inertia : R::link_inertia[b - 1];
+    if (b == 0 && !R::floating) {
+      cm[0] = 0.f; cp1[0] = mk3(0, 0, 0); cF[0] = mk3(0, 0, 0); cN[0] = mk3(0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 6; i++) cJ[0].a[i] = 0.f;
+      continue;
+    }
+    const float m = (float)mb;
+    const s6 Iw = rotate_inertia(k.Rm[b], I6);
+    const f3 r = k.c[b] - O;
+    const float rr = dot3(r, r);
+    s6 J;
+    J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
+    J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
+    J.a[2] = Iw.a[2] + m * (rr - r.z * r.z);
+    J.a[3] = Iw.a[3] - m * r.x * r.y;
+    J.a[4] = Iw.a[4] - m * r.x * r.z;
+    J.a[5] = Iw.a[5] - m * r.y * r.z;
+    const f3 Iww = mul(Iw, w[b]);
+    const f3 f = m * (ac[b] - mk3(0, 0, -g)) +
+                 (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[b]))) * v[b];
+    const f3 n = mul(Iw, al[b]) + cross3(w[b], Iww) +
+                 ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
+    cm[b] = m;
+    cp1[b] = m * r;
+    cJ[b] = J;
+    cF[b] = f;
+    cN[b] = n + cross3(r, f);
+  }
+#pragma unroll
+  for (int l = R::NL - 1; l >= 0; l--) {  // leaves to root: subtree sums
+    const int p = R::link_parent[l] + 1, b = l + 1;
+    cm[p] += cm[b];
+    cp1[p] += cp1[b];
+    cF[p] += cF[b];
+    cN[p] += cN[b];
+#pragma unroll
+    for (int i = 0; i < 6; i++) cJ[p].a[i] += cJ[b].a[i];
+  }
+
+  // --- dof motion vectors about O --------------------------------------------------------
+  f3 sw[N], sv[N];
+#pragma unroll
+  for (int gi = 0; gi < N; gi++) {
+    const int d = D::dof_of(gi);
+    if (d >= 0) {
+      if (R::dof_jtype[d] == 0) { sw[gi] = ja[d]; sv[gi] = cross3(jo[d] - O, ja[d]); }
+      else { sw[gi] = mk3(0, 0, 0); sv[gi] = ja[d]; }
+    } else {
+      const int kk = gi - NJ;  // 0..2 linear, 3..5 angular
+      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
+      if (kk < 3) { sw[gi] = mk3(0, 0, 0); sv[gi] = e; }
+      else { sw[gi] = e; sv[gi] = mk3(0, 0, 0); }
+    }
+  }
+
+  // --- mass matrix (lower triangle, gi >= gk) and bias -----------------------------------
+  float L[N][N];
+  float rhs[N];
+#pragma unroll
+  for (int gi = 0; gi < N; gi++) {
+    // composite body owning dof gi (its link); base dofs use the whole-robot composite
+    const int di = D::dof_of(gi);
+    const int bi = di >= 0 ? R::dof_link[di] + 1 : 0;
+    // bias: C_gi = s_gi . (N, F) of its composite
+    rhs[gi] = -(dot3(sw[gi], cN[bi]) + dot3(sv[gi], cF[bi]));
+#pragma unroll
+    for (int gk = 0; gk <= gi; gk++) {
+      if (!D::coupled(gi, gk)) { L[gi][gk] = 0.f; continue; }
+      // deeper dof of the pair owns the composite: joints come leaf-first, so the smaller
+      // generalized index is the deeper (or equal) one; base dofs are the root.
+      const int dk = D::dof_of(gk);
+      const int bk = dk >= 0 ? R::dof_link[dk] + 1 : 0;
+      const f3 Jw_ = mul(cJ[bk], sw[gk]) + cross3(cp1[bk], sv[gk]);
+      const f3 Fv = cm[bk] * sv[gk] - cross3(cp1[bk], sw[gk]);
+      L[gi][gk] = dot3(sw[gi], Jw_) + dot3(sv[gi], Fv);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < NJ; d++) {
+    L[D::gj(d)][D::gj(d)] += (float)R::dof_armature[d];
+    rhs[D::gj(d)] += tau[d] - (float)R::dof_damping[d] * s.qd[d];
+  }
+
+  // --- Cholesky (no fill-in in leaf-first order) ---------------------------------------
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    float sjj = L[j][j];
+#pragma unroll
+    for (int kk = 0; kk < j; kk++)
+      if (D::coupled(j, kk)) sjj -= L[j][kk] * L[j][kk];
+    const float ljj = sqrtf(sjj);
+    const float inv = 1.0f / ljj;
+    L[j][j] = ljj;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      if (!D::coupled(i, j)) continue;
+      float t = L[i][j];
+#pragma unroll
+      for (int kk = 0; kk < j; kk++)
+        if (D::coupled(i, kk) && D::coupled(j, kk)) t -= L[i][kk] * L[j][kk];
+      L[i][j] = t * inv;
+    }
+  }
+
+  // --- unconstrained velocity: nu_pred = nu + dt * M^-1 (tau - C) ------------------------
+  float nu[N];
+#pragma unroll
+  for (int d = 0; d < NJ; d++) nu[D::gj(d)] = s.qd[d];
+  if (R::floating) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) { nu[NJ + i] = s.bv[i]; nu[NJ + 3 + i] = s.bw[i]; }
+  }
+  float yv[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {  // forward: L y = rhs
+    float t = rhs[i];
+#pragma unroll
+    for (int kk = 0; kk < i; kk++)
+      if (D::coupled(i, kk)) t -= L[i][kk] * yv[kk];
+    yv[i] = t / L[i][i];
+  }
+  float qdd[N];
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {  // backward: L^T x = y
+    float t = yv[i];
+#pragma unroll
+    for (int kk = i + 1; kk < N; kk++)
+      if (D::coupled(kk, i)) t -= L[kk][i] * qdd[kk];
+    qdd[i] = t / L[i][i];
+  }
+  float u[N];  // u = L^T nu_pred
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    float t = nu[i] + dt * qdd[i];
+    nu[i] = fminf(fmaxf(t, -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    float t = 0.f;
+#pragma unroll
+    for (int kk = i; kk < N; kk++)
+      if (D::coupled(kk, i)) t += L[kk][i] * nu[kk];
+    u[i] = t;
+  }
+
+  // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
+  int nr = 0;
+#pragma unroll
+  for (int d = 0; d < NJ; d++) {
+    if (!R::dof_limited[d]) continue;
+    const int gd = D::gj(d);
+    // y = L^-1 e_gd
+    float y[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if (i < gd || !D::coupled(i, gd)) { y[i] = 0.f; continue; }
+      float t = i == gd ? 1.f : 0.f;
+#pragma unroll
+      for (int kk = gd; kk < i; kk++)
+        if (D::coupled(i, kk) && D::coupled(kk, gd)) t -= L[i][kk] * y[kk];
+      y[i] = t / L[i][i];
+    }
+    float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
+    const float meff = D2 > 1e-12f ? 1.f / D2 : 0.f;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+      const float sg = side == 0 ? 1.f : -1.f;
+      const float pos = side == 0 ? s.q[d] - (float)R::dof_lower[d] : (float)R::dof_upper[d] - s.q[d];
+      const float vj = sg * vJ;
+      const float tgt = pos > 0.f ? vj - pos / dt : -(float)PBG_LIMIT_ERP * pos / dt;
+#pragma unroll
+      for (int i = 0; i < N; i++) rw.y(nr, i) = sg * y[i];
+      rw.meff(nr) = meff;
+      rw.target(nr) = tgt;
+      rw.lam(nr) = 0.f;
+      rw.hi(nr) = (float)PBG_LIMIT_MAX_IMPULSE;
+      nr++;
+    }
+  }
+  const int first_normal = nr;
+  int nc = 0;
+  // contact rows are staged: normals first (in contact order), frictions after.
+  // Each contact stores its normal row now and its two friction rows at MAXROWS-space
+  // offsets after all normals; friction rows are compacted once nc is known.
+  constexpr int FR0 = 2 * D::NLIM + D::NC;  // staging area for friction rows
+#pragma unroll
+  for (int sl = 0; sl < R::NS; sl++) {
+    const int b = R::slot_link[sl] + 1;
+    const f3 cc = k.x[b] + mul(k.Rm[b], mk3((float)R::slot_point[sl][0], (float)R::slot_point[sl][1],
+                                            (float)R::slot_point[sl][2]));
+    const float rad = (float)R::slot_radius[sl];
+    const float dist = cc.z - rad;
+    const bool act = dist < (float)PBG_CONTACT_THRESHOLD;
+    slot_active[sl] = act;
+    if (!act) continue;
+    const f3 P = mk3(cc.x, cc.y, cc.z - rad);
+    const f3 rP = P - O;
+    const int lnk = R::slot_link[sl];
+#pragma unroll
+    for (int dir = 0; dir < 3; dir++) {
+      // n = +z, t1 = (0,-1,0), t2 = (1,0,0)  (btPlaneSpace1 of +z)
+      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 mm = cross3(rP, nd);
+      float Jr[N];
+#pragma unroll
+      for (int i = 0; i < N; i++) Jr[i] = D::in_chain(i, lnk) ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : 0.f;
+      float y[N];
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        if (!D::in_chain(i, lnk)) { y[i] = 0.f; continue; }
+        float t = Jr[i];
+#pragma unroll
+        for (int kk = 0; kk < i; kk++)
+          if (D::coupled(i, kk) && D::in_chain(kk, lnk)) t -= L[i][kk] * y[kk];
+        y[i] = t / L[i][i];
+      }
+      float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+      for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
+      const int row = dir == 0 ? first_normal + nc : FR0 + 2 * nc + (dir - 1);
+#pragma unroll
+      for (int i = 0; i < N; i++) rw.y(row, i) = y[i];
+      rw.meff(row) = D2 > 1e-12f ? 1.f / D2 : 0.f;
+      rw.target(row) = dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f;
+      rw.lam(row) = 0.f;
+      rw.hi(row) = 3.0e38f;
+    }
+    rw.mu(nc) = (float)R::slot_mu[sl];
+    nc++;
+  }
+  // self-collision pairs (capsule-capsule / sphere) -- Humanoid.  World endpoints per
+  // geom are computed once (unrolled); the pair loop itself runs at run time.
+  if constexpr (R::NPAIR > 0) {
+    f3 G0[R::NG], G1[R::NG];
+#pragma unroll
+    for (int gg = 0; gg < R::NG; gg++) {
+      const int b = R::geom_link[gg] + 1;
+      G0[gg] = k.x[b] + mul(k.Rm[b], mk3((float)R::geom_p0[gg][0], (float)R::geom_p0[gg][1], (float)R::geom_p0[gg][2]));
+      G1[gg] = k.x[b] + mul(k.Rm[b], mk3((float)R::geom_p1[gg][0], (float)R::geom_p1[gg][1], (float)R::geom_p1[gg][2]));
+    }
+#pragma unroll 1
+    for (int pp = 0; pp < R::NPAIR; pp++) {
+      const int ga = R::pair_ga[pp], gb = R::pair_gb[pp];
+      const f3 a0 = G0[ga], a1 = G1[ga], b0 = G0[gb], b1 = G1[gb];
+      const f3 d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
+      const float aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
+      float ss, tt;
+      const float eps = 1e-12f;
+      if (aa <= eps && ee <= eps) { ss = tt = 0.f; }
+      else if (aa <= eps) { ss = 0.f; tt = fminf(fmaxf(ff / ee, 0.f), 1.f); }
+      else {
+        const float cc2 = dot3(d1, r0);
+        if (ee <= eps) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+        else {
+          const float bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
+          ss = den > eps ? fminf(fmaxf((bb2 * ff - cc2 * ee) / den, 0.f), 1.f) : 0.f;
+          tt = (bb2 * ss + ff) / ee;
+          if (tt < 0.f) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+          else if (tt > 1.f) { tt = 1.f; ss = fminf(fmaxf((bb2 - cc2) / aa, 0.f), 1.f); }
+        }
+      }
+      const f3 ca = a0 + ss * d1, cb = b0 + tt * d2;
+      const f3 dv = ca - cb;
+      const float dd = norm3(dv);
+      const float ra = (float)R::geom_r[ga], rb = (float)R::geom_r[gb];
+      const float dist = dd - ra - rb;
+      if (!(dist < (float)PBG_CONTACT_THRESHOLD)) continue;
+      const f3 nrm = dd > 1e-9f ? (1.f / dd) * dv : mk3(0, 0, 1);
+      const f3 PA = ca - ra * nrm, PB = cb + rb * nrm;
+      f3 t1, t2;  // btPlaneSpace1(nrm)
+      if (fabsf(nrm.z) > 0.7071067811865476f) {
+        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = 1.f / sqrtf(a2);
+        t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
+        t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+      } else {
+        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = 1.f / sqrtf(a2);
+        t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
+        t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+      }
+      const uint32_t ma = R::link_chain_mask[R::geom_link[ga]], mb = R::link_chain_mask[R::geom_link[gb]];
+      const f3 rA = PA - O, rB = PB - O;
+#pragma unroll 1
+      for (int dir = 0; dir < 3; dir++) {
+        const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
+        const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
+        float y[N];
+        float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+          const int di = D::dof_of(i);
+          const bool inA = di < 0 || ((ma >> di) & 1u), inB = di < 0 || ((mb >> di) & 1u);
+          float t = 0.f;
+          if (inA) t += dot3(nd, sv[i]) + dot3(mA, sw[i]);
+          if (inB) t -= dot3(nd, sv[i]) + dot3(mB, sw[i]);
+#pragma unroll
+          for (int kk = 0; kk < i; kk++)
+            if (D::coupled(i, kk)) t -= L[i][kk] * y[kk];
+          y[i] = t / L[i][i];
+          D2 += y[i] * y[i];
+          vJ += y[i] * u[i];
+        }
+        const int row = dir == 0 ? first_normal + nc : FR0 + 2 * nc + (dir - 1);
+#pragma unroll
+        for (int i = 0; i < N; i++) rw.y(row, i) = y[i];
+        rw.meff(row) = D2 > 1e-12f ? 1.f / D2 : 0.f;
+        rw.target(row) = dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f;
+        rw.lam(row) = 0.f;
+        rw.hi(row) = 3.0e38f;
+      }
+      rw.mu(nc) = (float)R::pair_mu[pp];
+      nc++;
+    }
+  }
+
+  // --- PGS: 5 sweeps in u-space (gym_locomotion_envs -> scene_bases.py:65 numSolverIterations=5)
+  const int n_fixed = first_normal + nc;  // limit rows + normal rows, contiguous
+  for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+    for (int r = 0; r < n_fixed; r++) {
+      float yu = 0.f;
+#pragma unroll
+      for (int i = 0; i < N; i++) yu += rw.y(r, i) * u[i];
+      const float lam0 = rw.lam(r);
+      const float nl = fminf(fmaxf(lam0 + rw.meff(r) * (rw.target(r) - yu), 0.f), rw.hi(r));
+      const float dl = nl - lam0;
+      rw.lam(r) = nl;
+#pragma unroll
+      for (int i = 0; i < N; i++) u[i] += rw.y(r, i) * dl;
+    }
+    for (int c = 0; c < nc; c++) {
+      const float ln = rw.lam(first_normal + c);
+      if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
+      const float lim = rw.mu(c) * ln;
+#pragma unroll
+      for (int f = 0; f < 2; f++) {
+        const int r = FR0 + 2 * c + f;
+        float yu = 0.f;
+#pragma unroll
+        for (int i = 0; i < N; i++) yu += rw.y(r, i) * u[i];
+        const float lam0 = rw.lam(r);
+        const float nl = fminf(fmaxf(lam0 + rw.meff(r) * (rw.target(r) - yu), -lim), lim);
+        const float dl = nl - lam0;
+        rw.lam(r) = nl;
+#pragma unroll
+        for (int i = 0; i < N; i++) u[i] += rw.y(r, i) * dl;
+      }
+    }
+  }
+
+  // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    float t = u[i];
+#pragma unroll
+    for (int kk = i + 1; kk < N; kk++)
+      if (D::coupled(kk, i)) t -= L[kk][i] * nu[kk];
+    nu[i] = t / L[i][i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) nu[i] = fminf(fmaxf(nu[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+#pragma unroll
+  for (int d = 0; d < NJ; d++) {
+    s.qd[d] = nu[D::gj(d)];
+    s.q[d] += dt * s.qd[d];
+  }
+  if (R::floating) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      s.bv[i] = nu[NJ + i];
+      s.bw[i] = nu[NJ + 3 + i];
+      s.bp[i] += dt * s.bv[i];
+    }
+    // exponential-map quaternion update with the world angular velocity  [EXT]
+    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
+    float ang = norm3(wv);
+    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    f3 ax;
+    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
+    else ax = (sinf(0.5f * ang * dt) / ang) * wv;
+    const float dw = cosf(0.5f * ang * dt);
+    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
+    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+    const float inv = 1.f / sqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
+    s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
+  }
+  return nc;
+}
+
+// ------------------------------------------------------------------ numpy-exact pack (float64)
+#pragma clang fp contract(off)
+PBG_DEV double np_sum_f64(const double* a, int n) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; i++) res += a[i];
+    return 0.0 + res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += a[i];
+  return 0.0 + res;
+}
+PBG_DEV float np_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float res = 0.0f;
+    for (int i = 0; i < n; i++) res += a[i];
+    return 0.0f + res;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += a[i];
+  return 0.0f + res;
+}
+PBG_DEV float clip5(float v) { return v < -5.0f ? -5.0f : (v > 5.0f ? 5.0f : v); }
+
+// Inputs of the walker pack -- what the reference reads back from pybullet after the step.
+template <class R>
+struct PackIn {
+  double part_x[R::NP + 1], part_y[R::NP + 1];
+  int n_parts;
+  double quat[4], pos[3], vel[3];
+  double jq[R::NO > 0 ? R::NO : 1], jqd[R::NO > 0 ? R::NO : 1];
+  float feet_prev[R::NF > 0 ? R::NF : 1];
+  uint32_t feet_new;  // bitmask
+  double potential_old, initial_z;  // initial_z NaN: take from this calc_state
+};
+struct PackOut {
+  double reward, potential, initial_z;
+  uint32_t feet_out;  // bitmask
+  bool done;
+};
+
+// robot_locomotors.py:31-64 calc_state + gym_locomotion_envs.py:59-114 reward/done.
+template <class R>
+PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, PackOut& out) {
+  float j[2 * (R::NO > 0 ? R::NO : 1)];
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) {
+    const int d = R::obs_dof[i];
+    double pos = in.jq[i], vel = in.jqd[i];
+    if (R::dof_lower[d] < R::dof_upper[d]) {
+      const double mid = 0.5 * (R::dof_lower[d] + R::dof_upper[d]);
+      pos = 2 * (pos - mid) / (R::dof_upper[d] - R::dof_lower[d]);
+    }
+    vel *= R::obs_vel_scale[i];
+    j[2 * i] = (float)pos;
+    j[2 * i + 1] = (float)vel;
+  }
+  int at_limit = 0;
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) at_limit += fabsf(j[2 * i]) > PBG_JOINT_AT_LIMIT;
+  const double bx = np_sum_f64(in.part_x, in.n_parts) / (double)in.n_parts;
+  const double by = np_sum_f64(in.part_y, in.n_parts) / (double)in.n_parts;
+  const double bz = in.pos[2];
+  const double* q = in.quat;
+  const double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+  const double roll = atan2(2 * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+  const double sarg = -2 * (q[0] * q[2] - q[3] * q[1]);
+  const double pitch = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
+  const double yaw = atan2(2 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+  const double z0 = isnan(in.initial_z) ? bz : in.initial_z;
+  const double dy = PBG_WALK_TARGET_Y - by, dx = PBG_WALK_TARGET_X - bx;
+  const double theta = atan2(dy, dx);
+  const double dist = sqrt(dy * dy + dx * dx);
+  const double ang = theta - yaw;
+  const double cy = cos(-yaw), sy = sin(-yaw);
+  const double vx = cy * in.vel[0] + -sy * in.vel[1] + 0.0 * in.vel[2];
+  const double vy = sy * in.vel[0] + cy * in.vel[1] + 0.0 * in.vel[2];
+  const double vz = 0.0 * in.vel[0] + 0.0 * in.vel[1] + 1.0 * in.vel[2];
+  const float more[8] = {(float)(bz - z0), (float)sin(ang), (float)cos(ang), (float)(0.3 * vx),
+                         (float)(0.3 * vy), (float)(0.3 * vz), (float)roll, (float)pitch};
+  bool has_nan = false;
+  int o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { obs[o] = clip5(more[i]); has_nan |= isnan(obs[o]); o++; }
+#pragma unroll
+  for (int i = 0; i < 2 * R::NO; i++) { obs[o] = clip5(j[i]); has_nan |= isnan(obs[o]); o++; }
+#pragma unroll
+  for (int i = 0; i < R::NF; i++) { obs[o] = clip5(in.feet_prev[i]); o++; }
+  out.initial_z = z0;
+  out.potential = -dist / (R::dt_sub * R::substeps);  // robot_locomotors.py:79; scene_bases.py:17
+  uint32_t fb = 0;
+#pragma unroll
+  for (int i = 0; i < R::NF; i++) fb |= (in.feet_prev[i] != 0.f ? 1u : 0u) << i;
+  out.feet_out = fb;
+  if (!act) { out.reward = 0.0; out.done = false; return; }
+  const float s0 = obs[0];
+  double alive;
+  if constexpr (R::alive == 0) {  // Hopper robot_locomotors.py:89-90
+    const double z = (double)s0 + z0;
+    alive = (z > 0.8 && fabs(pitch) < 1.0) ? 1.0 : -1.0;
+  } else if constexpr (R::alive == 1) {  // HalfCheetah :116-118 (previous-step feet_contact)
+    alive = (fabs(pitch) < 1.0 && !(in.feet_prev[1] != 0) && !(in.feet_prev[2] != 0) &&
+             !(in.feet_prev[4] != 0) && !(in.feet_prev[5] != 0)) ? 1.0 : -1.0;
+  } else if constexpr (R::alive == 2) {  // Ant :137-138
+    const double z = (double)s0 + z0;
+    alive = z > 0.26 ? 1.0 : -1.0;
+  } else {  // Humanoid :191-192; np.float32 + 0.8 stays float32 (NEP 50)
+    const float z = s0 + (float)z0;
+    alive = z > 0.78f ? 2.0 : -1.0;
+  }
+  out.done = alive < 0 || has_nan;
+  const double progress = out.potential - in.potential_old;
+  out.feet_out = in.feet_new;
+  float tmp[R::NA];
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) tmp[i] = fabsf(act[i] * j[2 * i + 1]);
+  const float mean_e = np_sum_f32(tmp, R::NA) / (float)R::NA;
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) tmp[i] = act[i] * act[i];
+  const float mean_s = np_sum_f32(tmp, R::NA) / (float)R::NA;
+  double elec = R::electricity_cost * (double)mean_e;
+  elec += R::stall_torque_cost * (double)mean_s;
+  const double jal = R::joints_at_limit_cost * (double)at_limit;
+  out.reward = ((((0.0 + alive) + progress) + elec) + jal) + 0.0;
+}
+
+// robot_pendula.py:27-51 + gym_pendulum_envs.py:35-39
+PBG_DEV void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, PackOut& out) {
+  if (!isfinite(vx)) vx = 0.0;
+  if (!isfinite(theta)) theta = 0.0;
+  if (!isfinite(theta_dot)) theta_dot = 0.0;
+  obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
+  obs[4] = (float)theta_dot;
+  out.reward = 1.0;
+  out.done = fabs(theta) > 0.2;
+  out.potential = 0.0; out.initial_z = 0.0; out.feet_out = 0;
+}
+#pragma clang fp contract(on)
+
+// M3 -> quaternion (x,y,z,w) in float64
+PBG_DEV void m3_to_quat_d(const m3& mf, double* q) {
+  double m[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) m[i] = mf.m[i];
+  const double t = m[0] + m[4] + m[8];
+  if (t > 0) {
+    const double s = sqrt(t + 1.0) * 2;
+    q[3] = 0.25 * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    const double s = sqrt(1.0 + m[0] - m[4] - m[8]) * 2;
+    q[3] = (m[7] - m[5]) / s; q[0] = 0.25 * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+  } else if (m[4] > m[8]) {
+    const double s = sqrt(1.0 + m[4] - m[0] - m[8]) * 2;
+    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = 0.25 * s; q[2] = (m[5] + m[7]) / s;
+  } else {
+    const double s = sqrt(1.0 + m[8] - m[0] - m[4]) * 2;
+    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = 0.25 * s;
+  }
+}
+
+// Gather pack inputs from the physical state (what pybullet's queries would return).
+template <class R>
+PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
+  Kin<R> k;
+  fk_pos<R>(s, k);
+  int np = 0;
+#pragma unroll
+  for (int p = 0; p < R::NP; p++) {
+    const f3 c = k.c[R::part_link[p] + 1];
+    in.part_x[np] = c.x;
+    in.part_y[np] = c.y;
+    np++;
+  }
+  if (R::floor && has_floor) { in.part_x[np] = 0.0; in.part_y[np] = 0.0; np++; }
+  in.n_parts = np;
+  constexpr int b = R::robot_body + 1;
+  m3_to_quat_d(k.Rm[b], in.quat);
+  in.pos[0] = k.c[b].x; in.pos[1] = k.c[b].y; in.pos[2] = k.c[b].z;
+  // robot_body COM velocity
+  f3 vel;
+  if constexpr (b == 0) {
+    vel = mk3(s.bv[0], s.bv[1], s.bv[2]);
+  } else {
+    // velocity of link b's COM: rigid/joint chain from the base (recomputed here)
+    f3 w[R::NL + 1], v[R::NL + 1];
+    w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
+    v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
+#pragma unroll
+    for (int l = 0; l < R::NL; l++) {
+      const int p = R::link_parent[l] + 1, jt = R::link_jtype[l], d = R::link_dof[l];
+      const f3 cp = k.c[p], c = k.c[l + 1];
+      if (jt == 0 || jt == 1) {
+        const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
+                                 (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
+        const m3 R0 = mul(k.Rm[p], Ro);
+        const f3 a = mul(R0, mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]));
+        const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
+                                                (float)R::link_offset_pos[l][2]));
+        if (jt == 0) {
+          const f3 o = x0 + mul(R0, mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1],
+                                        (float)R::link_anchor[l][2]));
+          const f3 vo = v[p] + cross3(w[p], o - cp);
+          w[l + 1] = w[p] + s.qd[d] * a;
+          v[l + 1] = vo + cross3(w[l + 1], c - o);
+        } else {
+          w[l + 1] = w[p];
+          v[l + 1] = v[p] + cross3(w[p], c - cp) + s.qd[d] * a;
+        }
+      } else {
+        w[l + 1] = w[p];
+        v[l + 1] = v[p] + cross3(w[p], c - cp);
+      }
+    }
+    vel = v[b];
+  }
+  in.vel[0] = vel.x; in.vel[1] = vel.y; in.vel[2] = vel.z;
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) { in.jq[i] = s.q[R::obs_dof[i]]; in.jqd[i] = s.qd[R::obs_dof[i]]; }
+}
+
+// ------------------------------------------------------------------ kernel arguments
+struct Buffers {
+  int n;                   // envs on this device
+  float* st;               // [SD][n] physical state, SoA
+  double* pot;             // [n] potential
+  float* z0;               // [n] initial_z
+  int* elapsed;            // [n] steps in episode
+  uint32_t* flags;         // [n] bit0 floor-in-parts, bits 8.. feet_contact
+  uint32_t* episode;       // [n] resets so far (RNG counter)
+  uint64_t seed;
+  int env_offset;          // global id of env 0 (multi-GPU sharding)
+};
+
+struct StepIO {
+  const float* act;        // [n][NA]
+  float* obs;              // [n][OBS]
+  float* rew;              // [n] float32 reward
+  double* rew64;           // [n] nullable float64 reward
+  uint8_t* done;           // [n] terminated | truncated
+  uint8_t* trunc;          // [n] nullable, TimeLimit truncation
+  float* term_obs;         // [n][OBS] nullable: obs before an auto-reset
+  int32_t* ncontact;       // [n] nullable: contacts in the last sub-step
+  int autoreset;
+};
+
+struct ResetIO {
+  const uint8_t* mask;     // [n] nullable = all
+  const float* init_q;     // [n][NR] nullable = Philox noise U(-0.1, 0.1)
+  float* obs;              // [n][OBS]
+};
+
+template <class R>
+PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
+                       double& pot, float& z0) {
+  snapshot_state<R>(s);
+  const uint32_t epi = B.episode[e];
+  B.episode[e] = epi + 1;
+  if (init_q) {
+#pragma unroll
+    for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = init_q[(size_t)e * R::NR + r];
+  } else {
+    // np_random.uniform(-0.1, 0.1) per ordered joint (robot_locomotors.py:18-19) -> Philox
+    const uint32_t gid = (uint32_t)(B.env_offset + e);
+#pragma unroll
+    for (int blk = 0; blk < (R::NR + 3) / 4; blk++) {
+      u4 ctr = {gid, epi, (uint32_t)blk, 0x5EEDu};
+      const u4 rnd = philox4x32_10(ctr, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
+      const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int r = 4 * blk + t;
+        if (r < R::NR) s.q[R::reset_dof[r]] = -0.1f + 0.2f * u01(rr[t]);
+      }
+    }
+  }
+  PackOut po;
+  if constexpr (R::kind == 1) {
+    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+    has_floor = true; pot = 0.0; z0 = 0.f;
+    return;
+  } else {
+  PackIn<R> in;
+  gather<R>(s, has_floor, in);
+#pragma unroll
+  for (int f = 0; f < R::NF; f++) in.feet_prev[f] = 0.f;
+  in.feet_new = 0;
+  in.potential_old = 0.0;
+  in.initial_z = R::initial_z_fixed;
+  walker_pack<R>(in, nullptr, obs, po);
+  pot = po.potential;
+  z0 = (float)po.initial_z;
+  has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
+  }
+}
+
+template <class R>
+__global__ __launch_bounds__(64) void reset_kernel(Buffers B, ResetIO io) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B.n) return;
+  if (io.mask && !io.mask[e]) return;
+  State<R> s;
+  bool has_floor = B.flags[e] & 1u;
+  double pot;
+  float z0;
+  float obs[R::OBS];
+  reset_env<R>(B, e, s, io.init_q, obs, has_floor, pot, z0);
+  store_state<R>(s, B.st, B.n, e);
+  B.pot[e] = pot;
+  B.z0[e] = z0;
+  B.elapsed[e] = 0;
+  B.flags[e] = has_floor ? 1u : 0u;  // feet_contact cleared (robot_locomotors.py:22)
+#pragma unroll
+  for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+}
+
+template <class R>
+__global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* __restrict__ scratch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B.n) return;
+  State<R> s;
+  load_state<R>(s, B.st, B.n, e);
+  float act[R::NA];
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
+  // apply_action: tau = power * power_coef * clip(a, -1, 1)   (robot_locomotors.py:26-29)
+  float tau[R::NJ];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) tau[d] = 0.f;
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) {
+    const float c = fminf(fmaxf(act[i], -1.f), 1.f);
+    tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
+  }
+  uint32_t slot_active[R::NS > 0 ? R::NS : 1];
+  Rows<R> rw;
+  rw.base = scratch + e;
+  rw.n = B.n;
+  int nc = 0;
+  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R>(s, tau, slot_active, rw);
+  if (io.ncontact) io.ncontact[e] = nc;
+  const int el = B.elapsed[e] + 1;
+  uint32_t flags = B.flags[e];
+  float obs[R::OBS];
+  PackOut po;
+  double pot_new = 0.0;
+  if constexpr (R::kind == 1) {
+    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+  } else {
+    PackIn<R> in;
+    gather<R>(s, flags & 1u, in);
+    uint32_t fnew = 0;
+#pragma unroll
+    for (int f = 0; f < R::NF; f++) {
+      bool c = false;
+#pragma unroll
+      for (int sl = 0; sl < R::NS; sl++)
+        if (R::slot_link[sl] == R::foot_link[f]) c |= slot_active[sl] != 0;
+      fnew |= (c ? 1u : 0u) << f;
+      in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
+    }
+    in.feet_new = fnew;
+    in.potential_old = B.pot[e];
+    in.initial_z = B.z0[e];
+    walker_pack<R>(in, act, obs, po);
+    pot_new = po.potential;
+    flags = (flags & 0xFFu) | (po.feet_out << 8);
+  }
+  const bool term = po.done;
+  const bool trunc = el >= R::max_episode_steps;  // gym TimeLimit (envs/__init__.py max_episode_steps)
+  io.rew[e] = (float)po.reward;
+  if (io.rew64) io.rew64[e] = po.reward;
+  io.done[e] = term || trunc;
+  if (io.trunc) io.trunc[e] = trunc && !term;
+  if (io.autoreset && (term || trunc)) {
+    if (io.term_obs) {
+#pragma unroll
+      for (int i = 0; i < R::OBS; i++) io.term_obs[(size_t)e * R::OBS + i] = obs[i];
+    }
+    bool has_floor = flags & 1u;
+    double pot;
+    float z0;
+    reset_env<R>(B, e, s, nullptr, obs, has_floor, pot, z0);
+    B.pot[e] = pot;
+    B.z0[e] = z0;
+    B.elapsed[e] = 0;
+    B.flags[e] = has_floor ? 1u : 0u;
+  } else {
+    B.pot[e] = pot_new;
+    B.elapsed[e] = el;
+    B.flags[e] = flags;
+  }
+  store_state<R>(s, B.st, B.n, e);
+#pragma unroll
+  for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+}
+
+// Pack on explicit inputs (golden-vector parity of the device pack).  Per env the input
+// record is float64: [part_xyz (NP+1)*3 | n_parts | quat 4 | pos 3 | vel 3 | jq NO | jqd NO |
+// feet_prev NF | feet_new NF | act NA | potential_old | initial_z_in | is_step]; the output
+// record: [obs OBS | reward | done | potential | initial_z | feet_out NF].
+template <class R>
+struct PackRec {
+  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3;
+  static constexpr int OUT = R::OBS + 4 + R::NF;
+};
+template <class R>
+__global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restrict__ inrec, double* __restrict__ outrec) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double* r = inrec + (size_t)e * PackRec<R>::IN;
+  double* w = outrec + (size_t)e * PackRec<R>::OUT;
+  float obs[R::OBS];
+  float act[R::NA];
+  PackOut po;
+  const int o_np = (R::NP + 1) * 3;
+  const int o_q = o_np + 1, o_pos = o_q + 4, o_vel = o_pos + 3, o_jq = o_vel + 3, o_jqd = o_jq + R::NO;
+  const int o_fp = o_jqd + R::NO, o_fn = o_fp + R::NF, o_act = o_fn + R::NF, o_pot = o_act + R::NA;
+  const bool is_step = r[o_pot + 2] != 0.0;
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) act[i] = (float)r[o_act + i];
+  if constexpr (R::kind == 1) {
+    pendulum_obs(r[o_jq], r[o_jqd], r[o_jq + 1], r[o_jqd + 1], obs, po);
+  } else {
+    PackIn<R> in;
+    in.n_parts = (int)r[o_np];
+    for (int p = 0; p < in.n_parts && p < R::NP + 1; p++) { in.part_x[p] = r[3 * p]; in.part_y[p] = r[3 * p + 1]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) in.quat[i] = r[o_q + i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { in.pos[i] = r[o_pos + i]; in.vel[i] = r[o_vel + i]; }
+#pragma unroll
+    for (int i = 0; i < R::NO; i++) { in.jq[i] = r[o_jq + i]; in.jqd[i] = r[o_jqd + i]; }
+    uint32_t fn = 0;
+#pragma unroll
+    for (int f = 0; f < R::NF; f++) { in.feet_prev[f] = (float)r[o_fp + f]; fn |= (r[o_fn + f] != 0.0 ? 1u : 0u) << f; }
+    in.feet_new = fn;
+    in.potential_old = r[o_pot];
+    in.initial_z = r[o_pot + 1];
+    walker_pack<R>(in, is_step ? act : nullptr, obs, po);
+  }
+  if (!is_step) { po.reward = 0.0; po.done = false; }
+#pragma unroll
+  for (int i = 0; i < R::OBS; i++) w[i] = (double)obs[i];
+  w[R::OBS] = po.reward;
+  w[R::OBS + 1] = po.done ? 1.0 : 0.0;
+  w[R::OBS + 2] = po.potential;
+  w[R::OBS + 3] = po.initial_z;
+#pragma unroll
+  for (int f = 0; f < R::NF; f++) w[R::OBS + 4 + f] = (po.feet_out >> f) & 1u;
+}
+
+// State record conversion: SoA float32 (+ bookkeeping) <-> AoS float64 records.
+template <class R>
+__global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __restrict__ phys, double* __restrict__ aux) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B.n) return;
+  constexpr int SD = Dims<R>::SD, AD = PBG_AUX_WORDS + R::NF;
+  for (int i = 0; i < SD; i++) phys[(size_t)e * SD + i] = (double)B.st[(size_t)i * B.n + e];
+  double* a = aux + (size_t)e * AD;
+  a[0] = B.pot[e];
+  a[1] = (double)B.z0[e];
+  a[2] = (double)B.elapsed[e];
+  a[3] = (double)(B.flags[e] & 1u);
+  for (int f = 0; f < R::NF; f++) a[4 + f] = (double)((B.flags[e] >> (8 + f)) & 1u);
+}
+template <class R>
+__global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* __restrict__ phys, const double* __restrict__ aux) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B.n) return;
+  constexpr int SD = Dims<R>::SD, AD = PBG_AUX_WORDS + R::NF;
+  for (int i = 0; i < SD; i++) B.st[(size_t)i * B.n + e] = (float)phys[(size_t)e * SD + i];
+  if (aux) {
+    const double* a = aux + (size_t)e * AD;
+    B.pot[e] = a[0];
+    B.z0[e] = (float)a[1];
+    B.elapsed[e] = (int)a[2];
+    uint32_t fl = a[3] != 0.0 ? 1u : 0u;
+    for (int f = 0; f < R::NF; f++) fl |= (a[4 + f] != 0.0 ? 1u : 0u) << (8 + f);
+    B.flags[e] = fl;
+  }
+}
+
+}  // namespace pbg

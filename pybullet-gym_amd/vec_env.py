@@ -1,0 +1,155 @@
+"""Batched, device-resident locomotion envs over libpbg_amd.so.
+
+``VecEnv(env_id, num_envs)`` holds the state of num_envs independent copies of one
+``*PyBulletEnv-v0`` env on one GPU and steps all of them with one kernel launch per
+``step()``.  Actions, observations, rewards and done flags are PyTorch-ROCm tensors
+that never leave HBM.  Semantics per env are those of the reference's
+``WalkerBaseBulletEnv`` (gym_locomotion_envs.py:22-114) behind gym's TimeLimit
+(envs/__init__.py ``max_episode_steps``), with gym-VectorEnv style auto-reset.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+from .spaces import Box
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+@dataclass
+class StepResult:
+    obs: torch.Tensor
+    reward: torch.Tensor
+    done: torch.Tensor
+    truncated: torch.Tensor
+    terminal_obs: torch.Tensor
+
+
+class VecEnv:
+    def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
+                 autoreset: bool = True):
+        if not torch.cuda.is_available():
+            raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.env_id = env_id
+        self.device = torch.device(device)
+        self.num_envs = int(num_envs)
+        self.autoreset = autoreset
+        L = _native.lib()
+        h = ctypes.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _native.check(L.pbg_create(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
+                                   ctypes.byref(h)), "pbg_create")
+        self._h = h
+        info = _native.Info()
+        _native.check(L.pbg_info(h, ctypes.byref(info)), "pbg_info")
+        self.info = info
+        # robot_bases.py:24-27
+        self.action_space = Box(-np.ones(info.action_dim, np.float32), np.ones(info.action_dim, np.float32))
+        self.observation_space = Box(np.full(info.obs_dim, -np.inf, np.float32), np.full(info.obs_dim, np.inf, np.float32))
+        kw = dict(device=self.device)
+        n = self.num_envs
+        self.obs = torch.zeros((n, info.obs_dim), dtype=torch.float32, **kw)
+        self.reward = torch.zeros(n, dtype=torch.float32, **kw)
+        self.done = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.truncated = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.terminal_obs = torch.zeros((n, info.obs_dim), dtype=torch.float32, **kw)
+        self.reward64 = None
+        self.ncontact = None
+        self._io = _native.StepIO()
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            _native.lib().pbg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- gym-like API
+    def reset(self, mask: torch.Tensor = None, init_q: torch.Tensor = None) -> torch.Tensor:
+        """Reset all envs (or those with mask != 0).  init_q: [n, reset_dofs] float32 joint
+        positions replacing the U(-0.1, 0.1) draw (trace replay)."""
+        if mask is not None:
+            mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        if init_q is not None:
+            init_q = init_q.to(device=self.device, dtype=torch.float32).contiguous()
+            assert init_q.shape == (self.num_envs, self.info.reset_dofs)
+        _native.check(_native.lib().pbg_reset(self._h, _ptr(mask), _ptr(init_q), _ptr(self.obs),
+                                              _stream(self.device)), "pbg_reset")
+        return self.obs
+
+    def step(self, actions: torch.Tensor, want_reward64: bool = False, want_contacts: bool = False) -> StepResult:
+        a = actions
+        if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        assert a.shape == (self.num_envs, self.info.action_dim), a.shape
+        io = self._io
+        io.act = a.data_ptr()
+        io.obs = self.obs.data_ptr()
+        io.rew = self.reward.data_ptr()
+        io.done = self.done.data_ptr()
+        io.trunc = self.truncated.data_ptr()
+        io.term_obs = self.terminal_obs.data_ptr() if self.autoreset else None
+        if want_reward64 and self.reward64 is None:
+            self.reward64 = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        if want_contacts and self.ncontact is None:
+            self.ncontact = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        io.rew64 = self.reward64.data_ptr() if want_reward64 else None
+        io.ncontact = self.ncontact.data_ptr() if want_contacts else None
+        io.autoreset = 1 if self.autoreset else 0
+        _native.check(_native.lib().pbg_step_ex(self._h, ctypes.byref(io), _stream(self.device)), "pbg_step")
+        return StepResult(self.obs, self.reward, self.done, self.truncated, self.terminal_obs)
+
+    # ---------------------------------------------------------------- state records
+    def get_state(self):
+        phys = torch.zeros((self.num_envs, self.info.state_words), dtype=torch.float64, device=self.device)
+        aux = torch.zeros((self.num_envs, self.info.aux_words), dtype=torch.float64, device=self.device)
+        _native.check(_native.lib().pbg_get_state(self._h, _ptr(phys), _ptr(aux), _stream(self.device)),
+                      "pbg_get_state")
+        return phys, aux
+
+    def set_state(self, phys: torch.Tensor, aux: torch.Tensor = None):
+        phys = phys.to(device=self.device, dtype=torch.float64).contiguous()
+        assert phys.shape == (self.num_envs, self.info.state_words)
+        if aux is not None:
+            aux = aux.to(device=self.device, dtype=torch.float64).contiguous()
+            assert aux.shape == (self.num_envs, self.info.aux_words)
+        _native.check(_native.lib().pbg_set_state(self._h, _ptr(phys), _ptr(aux), _stream(self.device)),
+                      "pbg_set_state")
+
+
+def pack(env_id: str, in_rec: torch.Tensor) -> torch.Tensor:
+    """Device observation/reward pack on explicit input records (golden-vector parity)."""
+    L = _native.lib()
+    iw, ow = ctypes.c_int(), ctypes.c_int()
+    _native.check(L.pbg_pack_record_sizes(_native.env_id_bytes(env_id), ctypes.byref(iw), ctypes.byref(ow)),
+                  "pbg_pack_record_sizes")
+    assert in_rec.dtype == torch.float64 and in_rec.shape[1] == iw.value, (in_rec.shape, iw.value)
+    in_rec = in_rec.contiguous()
+    out = torch.zeros((in_rec.shape[0], ow.value), dtype=torch.float64, device=in_rec.device)
+    _native.check(L.pbg_pack(_native.env_id_bytes(env_id), in_rec.shape[0], _ptr(in_rec), _ptr(out),
+                             _stream(in_rec.device)), "pbg_pack")
+    return out
+
+
+def pack_record_sizes(env_id: str):
+    L = _native.lib()
+    iw, ow = ctypes.c_int(), ctypes.c_int()
+    _native.check(L.pbg_pack_record_sizes(_native.env_id_bytes(env_id), ctypes.byref(iw), ctypes.byref(ow)),
+                  "pbg_pack_record_sizes")
+    return iw.value, ow.value
