@@ -1,0 +1,177 @@
+"""Headline benchmark: random-action rollout env-steps/s on AntPyBulletEnv-v0.
+
+BASELINE.json metric: "env steps/sec (whole node) at N parallel envs, Ant + Humanoid,
+1/2/4/8 MI355X"; the single-GPU workload is config[2], AntPyBulletEnv-v0 at 16,384
+envs per GPU (weak scaling: each rank owns 16,384 envs, no per-step collective).
+
+One "step" = one batched env step of every env on every GPU: apply_action, 4 physics
+sub-steps (Featherstone dynamics, contacts, 5-sweep PGS, integration), the
+observation/reward/done pack, TimeLimit + auto-reset -- one kernel launch per GPU.
+Actions are pre-generated U(-1, 1) float32 tensors already resident in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+ENV_ID = "AntPyBulletEnv-v0"
+ENVS_PER_GPU = 16384
+# Algorithmic HBM bytes per env-step: 4 * (2S + n + D + 2),
+# S = 35 state words, n = 8 actions, D = 28 obs, 2 = reward + done  ->  432 B.
+ALG_BYTES_PER_ENV_STEP = 4 * (2 * 35 + 8 + 28 + 2)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def cpu_baseline(seconds=12.0):
+    """The CPU oracle (float64 restatement of the same step) on the host's cores, on a
+    bounded sample: 4,096 Ant envs stepped until ~`seconds` of wall time."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    n = 4096
+    e = oracle.OracleEnvs(ENV_ID, n, nthreads=threads)
+    rng = np.random.default_rng(0)
+    e.reset(rng.uniform(-0.1, 0.1, (n, e.info.NR)))
+    acts = rng.uniform(-1, 1, (8, n, e.info.NA)).astype(np.float32)
+    e.step(acts[0])
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        e.step(acts[steps % 8])
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/pbg_oracle.cpp (float64) on {n} Ant envs x {steps} steps, "
+                      f"{threads} OpenMP threads, {dt:.1f} s; no auto-reset"}
+
+
+def load_traffic():
+    """HBM bytes per launch of the step kernel from the latest committed PMC summary."""
+    path = os.path.join(REPO, "profiles", "pmc_step_ant.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs-per-gpu", type=int, default=ENVS_PER_GPU)
+    ap.add_argument("--env", default=ENV_ID)
+    ap.add_argument("--gather", action="store_true", help="also time the RCCL obs all-gather (separately)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import pybulletgym_amd  # noqa: F401
+    from pybulletgym_amd.distributed import gather_flat
+    from pybulletgym_amd.vec_env import VecEnv
+
+    n = args.envs_per_gpu
+    env = VecEnv(args.env, n, device=dev, seed=0x5EED, env_offset=rank * n, autoreset=True)
+    env.reset()
+    na = env.info.action_dim
+    total = args.warmup + args.steps
+    pool = min(total, 256)  # distinct pre-generated action batches, cycled (256 x 512 KB)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    acts = torch.rand((pool, n, na), device=dev, generator=g, dtype=torch.float32) * 2 - 1
+
+    for i in range(args.warmup):
+        env.step(acts[i % pool])
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        env.step(acts[(args.warmup + i) % pool])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    gather_ms = None
+    if args.gather and world > 1:
+        for _ in range(3):
+            gather_flat(env.obs)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(20):
+            gather_flat(env.obs)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - t1) / 20 * 1e3
+
+    finite = bool(torch.isfinite(env.obs).all())
+    if rank == 0:
+        steps_total = world * n * args.steps
+        value = steps_total / elapsed
+        achieved = ALG_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
+        traffic = load_traffic()
+        out = {
+            "metric": "env steps/sec (whole node) at N parallel envs, AntPyBulletEnv-v0 random-action rollout",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: U(-1,1) float32 actions pre-generated in HBM; MJCF-compiled Ant model",
+            "config": {"workload": f"{args.env} random-action rollout, auto-reset (TimeLimit 1000)",
+                       "envs_per_gpu": n, "global_envs": world * n, "substeps": env.info.substeps,
+                       "solver_iterations": 5, "parallelism": f"env-sharded x{world}, no per-step collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": f"pbg::step_kernel<{args.env}>", "kernel_ms": kernel_ms,
+                         "alg_bytes_per_env_step": ALG_BYTES_PER_ENV_STEP},
+            "obs_finite": finite,
+        }
+        if gather_ms is not None:
+            out["allgather_obs_ms"] = gather_ms
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

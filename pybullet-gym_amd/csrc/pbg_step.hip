@@ -932,7 +932,7 @@ PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int r = 4 * blk + t;
-        if (r < R::NR) s.q[R::reset_dof[r]] = -0.1f + 0.2f * u01(rr[t]);
+        if (r < R::NR) s.q[R::reset_dof[r]] = fmaf(0.2f, u01(rr[t]), -0.1f);
       }
     }
   }

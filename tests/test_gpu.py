@@ -1,0 +1,214 @@
+"""GPU parity: the HIP path (libpbg_amd.so through its C-ABI) against the golden vectors
+and the CPU oracle.  Run on an MI355X:  python -m pytest tests -m gpu
+
+Tolerances (stated per test):
+  * pack on golden inputs: float32 obs bit-exact, done/feet exact, reward |d| <= 1e-9
+    (float64 sum; the slack covers the BLAS dot order in np.linalg.norm).
+  * reset (same init_q): obs |d| <= 1e-5 (float32 vs float64 forward kinematics).
+  * one teacher-forced env step (GPU float32 physics vs oracle float64 from the same
+    state): done flags identical; contact counts identical in >= 99.9% of env-steps;
+    median per-env obs error <= 1e-4 and 99th percentile <= 1e-2.  The tails come from
+    the contact/PGS sensitivity that the oracle shows against its OWN float32-rounded
+    state (tools/gpu_check.py prints both); SURVEY.md section 7 "chaotic divergence".
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import pybulletgym_amd  # noqa: F401
+from pybulletgym_amd import rng
+from pybulletgym_amd.vec_env import VecEnv, pack, pack_record_sizes
+
+pytestmark = pytest.mark.gpu
+
+ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
+        "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"]
+KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+# ------------------------------------------------------------------ pack vs reference golden vectors
+@pytest.mark.parametrize("env_id", ENVS)
+def test_device_pack_matches_reference_golden(env_id):
+    key = KEY[env_id]
+    g = np.load(os.path.join(GOLDEN, f"pack_{key}.npz"))
+    info = oracle.Info(oracle.robot_id(key))
+    iw, ow = pack_record_sizes(env_id)
+    n = len(g["kind"])
+    rec = np.zeros((n, iw))
+    NP1 = info.NP + 1
+    for i in range(n):
+        o = 0
+        if info.kind == 0:
+            px = np.zeros((NP1, 3))
+            px[: g["n_parts"][i]] = g["part_xyz"][i][: g["n_parts"][i]]
+            rec[i, : 3 * NP1] = px.ravel()
+            rec[i, 3 * NP1] = g["n_parts"][i]
+        o = 3 * NP1 + 1
+        if info.kind == 0:
+            rec[i, o:o + 4] = g["body_quat"][i]
+            rec[i, o + 4:o + 7] = g["body_pos"][i]
+            rec[i, o + 7:o + 10] = g["body_vel"][i]
+        o += 10
+        rec[i, o:o + info.NO] = g["jq"][i]
+        rec[i, o + info.NO:o + 2 * info.NO] = g["jqd"][i]
+        o += 2 * info.NO
+        if info.kind == 0:
+            rec[i, o:o + info.NF] = g["feet_prev"][i][: info.NF]
+            rec[i, o + info.NF:o + 2 * info.NF] = g["feet_new"][i][: info.NF]
+        o += 2 * info.NF
+        rec[i, o:o + info.NA] = g["act"][i]
+        o += info.NA
+        rec[i, o] = g["potential_old"][i]
+        rec[i, o + 1] = g["initial_z_in"][i] if info.kind == 0 else 0.0
+        rec[i, o + 2] = float(g["kind"][i] == 1)
+    out = pack(env_id, torch.from_numpy(rec).cuda()).cpu().numpy()
+    obs = out[:, : info.OBS].astype(np.float32)
+    ref = g["obs"].astype(np.float32)
+    np.testing.assert_array_equal(obs.view(np.uint32), ref.view(np.uint32))
+    step = g["kind"] == 1
+    np.testing.assert_array_equal(out[step, info.OBS + 1].astype(bool), g["done"][step])
+    np.testing.assert_allclose(out[step, info.OBS], g["reward"][step], atol=1e-9, rtol=0)
+    if info.kind == 0:
+        np.testing.assert_allclose(out[:, info.OBS + 2], g["potential"], atol=1e-9, rtol=0)
+        np.testing.assert_array_equal(out[:, info.OBS + 3], g["initial_z_out"])
+        np.testing.assert_array_equal(out[:, info.OBS + 4:], g["feet_out"][:, : info.NF])
+
+
+# ------------------------------------------------------------------ reset
+@pytest.mark.parametrize("env_id", ENVS)
+def test_reset_matches_oracle(env_id):
+    n = 128
+    env = VecEnv(env_id, n, seed=5, autoreset=False)
+    orc = oracle.OracleEnvs(env_id, n)
+    q0 = np.random.default_rng(0).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
+    obs = env.reset(init_q=torch.from_numpy(q0)).cpu().numpy()
+    obs_o = orc.reset(q0.astype(np.float64))
+    np.testing.assert_allclose(obs, obs_o, atol=1e-5, rtol=0)
+    phys, aux = env.get_state()
+    np.testing.assert_allclose(phys.cpu().numpy(), orc.state, atol=1e-7, rtol=0)
+    np.testing.assert_allclose(aux.cpu().numpy(), orc.aux, atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"])
+def test_rng_reset_matches_host_philox(env_id):
+    n, seed, off = 64, 1234, 1000
+    env = VecEnv(env_id, n, seed=seed, env_offset=off, autoreset=False)
+    env.reset()
+    env.reset()  # second episode
+    phys, _ = env.get_state()
+    t = oracle.Info(oracle.robot_id(KEY[env_id]))
+    import json
+    tab = json.load(open(os.path.join(os.path.dirname(__file__), "..", "pybullet-gym_amd", "models",
+                                      f"{KEY[env_id]}.json")))
+    q = phys.cpu().numpy()[:, 13:13 + t.NJ]
+    want = rng.reset_noise(seed, np.arange(off, off + n), 1, t.NR)
+    np.testing.assert_array_equal(q[:, tab["reset_dof"]].astype(np.float32), want)
+
+
+# ------------------------------------------------------------------ teacher-forced step parity
+@pytest.mark.parametrize("env_id", ENVS)
+def test_step_teacher_forced_parity(env_id):
+    n, steps = 256, 40
+    env = VecEnv(env_id, n, seed=3, autoreset=False)
+    orc = oracle.OracleEnvs(env_id, n, nthreads=8)
+    r = np.random.default_rng(1)
+    q0 = r.uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
+    env.reset(init_q=torch.from_numpy(q0))
+    errs, cmis, total = [], 0, 0
+    for _ in range(steps):
+        phys, aux = env.get_state()
+        orc.state[:] = phys.cpu().numpy()
+        orc.aux[:] = aux.cpu().numpy()
+        a = r.uniform(-1, 1, (n, env.info.action_dim)).astype(np.float32)
+        res = env.step(torch.from_numpy(a).cuda(), want_reward64=True, want_contacts=True)
+        og = res.obs.cpu().numpy()
+        dg = res.done.cpu().numpy().astype(bool)
+        cg = env.ncontact.cpu().numpy()
+        oo, ro, do, co = orc.step(a)
+        np.testing.assert_array_equal(dg, do)
+        cmis += int((cg != co).sum())
+        total += n
+        errs.append(np.abs(og - oo).max(axis=1))
+    e = np.concatenate(errs)
+    assert np.median(e) <= 1e-4, np.median(e)
+    assert np.percentile(e, 99) <= 1e-2, np.percentile(e, 99)
+    assert cmis <= 0.001 * total, (cmis, total)
+
+
+def test_free_running_short_horizon_ant():
+    """No teacher forcing: 10 steps from identical resets stay within 1e-3 (obs)."""
+    n = 128
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=3, autoreset=False)
+    orc = oracle.OracleEnvs("AntPyBulletEnv-v0", n)
+    r = np.random.default_rng(2)
+    q0 = r.uniform(-0.1, 0.1, (n, 8)).astype(np.float32)
+    env.reset(init_q=torch.from_numpy(q0))
+    orc.reset(q0.astype(np.float64))
+    for _ in range(10):
+        a = r.uniform(-1, 1, (n, 8)).astype(np.float32)
+        og = env.step(torch.from_numpy(a).cuda()).obs.cpu().numpy()
+        oo, _, _, _ = orc.step(a)
+    assert np.median(np.abs(og - oo).max(axis=1)) < 1e-3
+
+
+# ------------------------------------------------------------------ episode bookkeeping
+def test_autoreset_and_time_limit():
+    n = 64
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True)
+    env.reset()
+    phys, aux = env.get_state()
+    aux[:, 2] = 999.0  # elapsed: next step hits max_episode_steps = 1000
+    env.set_state(phys, aux)
+    res = env.step(torch.zeros((n, 8), device="cuda"))
+    assert res.done.all() and res.truncated.sum() >= 1
+    _, aux2 = env.get_state()
+    assert (aux2[:, 2] == 0).all()  # every env was reset in the same launch
+    # the returned obs is the reset obs: zero feet_contact (robot_locomotors.py:22)
+    assert (res.obs[:, -4:] == 0).all()
+    assert torch.isfinite(res.terminal_obs).all()
+
+
+def test_determinism_and_env_offset_invariance():
+    """Same seed -> bitwise identical rollouts; env i of a shard with env_offset k equals
+    env k+i of a bigger batch (sharding does not change trajectories)."""
+    def run(n, off):
+        env = VecEnv("HopperPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True)
+        env.reset()
+        g = torch.Generator(device="cuda").manual_seed(0)
+        acts = torch.rand((30, 64, 3), device="cuda", generator=g) * 2 - 1
+        outs = []
+        for t in range(30):
+            outs.append(env.step(acts[t][off:off + n].contiguous()).obs.clone())
+        return torch.stack(outs).cpu().numpy()
+    a = run(64, 0)
+    b = run(64, 0)
+    np.testing.assert_array_equal(a, b)
+    c = run(32, 32)
+    np.testing.assert_array_equal(a[:, 32:], c)
+
+
+def test_large_batch_stays_finite():
+    """BASELINE config sizes: Ant 16,384 envs for 200 random steps with auto-reset."""
+    n = 16384
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=4, autoreset=True)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    dones = 0
+    for _ in range(200):
+        res = env.step(torch.rand((n, 8), device="cuda", generator=g) * 2 - 1)
+        dones += int(res.done.sum())
+    assert torch.isfinite(res.obs).all() and torch.isfinite(res.reward).all()
+    assert res.obs.abs().max() <= 5.0
+    phys, _ = env.get_state()
+    assert torch.isfinite(phys).all()
+    assert dones < n * 200

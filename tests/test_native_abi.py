@@ -1,0 +1,47 @@
+"""The C-ABI library loads (no GPU needed) and exports every symbol include/pbg.h declares."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import pybulletgym_amd  # noqa: F401
+from pybulletgym_amd import _native
+
+HEADER = os.path.join(os.path.dirname(__file__), "..", "include", "pbg.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pbg_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared()
+    for n in ("pbg_create", "pbg_step", "pbg_reset", "pbg_destroy", "pbg_last_error"):
+        assert n in names
+
+
+@pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="libpbg_amd.so not built")
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for n in declared():
+        assert hasattr(lib, n), n
+    assert set(_native.EXPORTED) <= set(declared())
+
+
+@pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="libpbg_amd.so not built")
+def test_pack_record_sizes_without_gpu():
+    lib = _native.lib()
+    iw, ow = ctypes.c_int(), ctypes.c_int()
+    assert lib.pbg_pack_record_sizes(b"AntPyBulletEnv-v0", ctypes.byref(iw), ctypes.byref(ow)) == 0
+    assert ow.value == 28 + 4 + 4
+    assert lib.pbg_pack_record_sizes(b"NoSuchEnv-v0", ctypes.byref(iw), ctypes.byref(ow)) != 0
+    assert b"unknown env id" in lib.pbg_last_error()
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_native.PbgError):
+        _native.lib()
