@@ -68,12 +68,24 @@ struct pbg_handle {
   int rid, device, n;
   pbg::Buffers B;
   float* scratch;
+  int lds_rows;       // constraint rows kept in LDS per env
+  size_t lds_bytes;   // dynamic LDS per 64-lane workgroup
   pbg_info_t info;
 };
 
 extern "C" {
 
 const char* pbg_last_error(void) { return g_err; }
+
+#ifdef PBG_STAMPS
+// diagnostic build only: read and clear the per-phase wave-cycle sums
+int pbg_debug_stamps(unsigned long long* host_out) {
+  hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pbg::g_stamps), sizeof(unsigned long long) * 16);
+  unsigned long long z[16] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(pbg::g_stamps), z, sizeof(z));
+  return 0;
+}
+#endif
 
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
@@ -117,6 +129,22 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
     e |= hip_check(hipMemset(B.elapsed, 0, sizeof(int) * n), "hipMemset");
     e |= hip_check(hipMemset(B.flags, 0, sizeof(uint32_t) * n), "hipMemset");
     e |= hip_check(hipMemset(B.episode, 0, sizeof(uint32_t) * n), "hipMemset");
+    // LDS budget: all resident waves of a CU share 160 KiB; one wave per workgroup.
+    int cus = 256;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const int waves = (n_envs + 63) / 64;
+    const int wpc = (waves + cus - 1) / cus;
+    int maxlds = 163840;
+    const size_t budget = (size_t)maxlds / (size_t)(wpc > 0 ? wpc : 1);
+    using RW = pbg::Rows<R>;
+    long words = (long)(budget / (64 * sizeof(float))) - RW::NC;
+    int cap = (int)(words / RW::W);
+    if (cap > RW::MR) cap = RW::MR;
+    if (cap < 0) cap = 0;
+    h->lds_rows = cap;
+    h->lds_bytes = (size_t)64 * sizeof(float) * ((size_t)cap * RW::W + RW::NC);
+    e |= hip_check(hipFuncSetAttribute((const void*)pbg::step_kernel<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)h->lds_bytes), "hipFuncSetAttribute");
     e |= hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     return e ? PBG_E_HIP : PBG_OK;
   });
@@ -165,8 +193,8 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
   pbg::StepIO s{io->act, io->obs, io->rew, io->rew64, io->done, io->trunc, io->term_obs, io->ncontact, io->autoreset};
   return dispatch(h->rid, [&](auto r) -> int {
     using R = decltype(r);
-    hipLaunchKernelGGL(pbg::step_kernel<R>, dim3(grid_of(h->n)), dim3(64), 0, (hipStream_t)stream, h->B, s,
-                       h->scratch);
+    hipLaunchKernelGGL(pbg::step_kernel<R>, dim3(grid_of(h->n)), dim3(64), h->lds_bytes, (hipStream_t)stream, h->B,
+                       s, h->scratch, h->lds_rows);
     return hip_check(hipGetLastError(), "step_kernel launch");
   });
 }

@@ -27,6 +27,19 @@
 
 namespace pbg {
 
+// Diagnostic build only (-DPBG_STAMPS): per-phase wave-cycle sums (s_memtime), summed over
+// waves into g_stamps by lane 0.  Never compiled into the product library.
+#ifdef PBG_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP_DECL unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_acc[16] = {0};
+#define STAMP(i) { unsigned long long _n = __builtin_amdgcn_s_memtime(); _st_acc[i] += _n - _st_t; _st_t = _n; }
+#define STAMP_FLUSH if ((threadIdx.x & 63) == 0) { for (int _i = 0; _i < 16; _i++) atomicAdd(&g_stamps[_i], _st_acc[_i]); }
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#endif
+
 // ------------------------------------------------------------------ compile-time model facts
 template <class R>
 struct Dims {
@@ -161,30 +174,73 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
 }
 
 // ------------------------------------------------------------------ per-substep scratch
-// Constraint rows live in a device workspace laid out [word][env] so that every lane's
-// access to "its" row word is one coalesced 256-B wave access.
+// Constraint rows: row r = [y (NDOF) | meff | target | lambda | hi].  Rows 0..cap-1 live
+// in LDS (dynamic shared memory, [word][64 lanes]: conflict-free, ~100-cycle latency);
+// rows >= cap (rare: many simultaneous contacts) in a device workspace laid out
+// [word][env] so that each access is one coalesced wave access.  Row order:
+// limit rows [0, 2*NLIM), then contact c at 2*NLIM + 3c + {normal, t1, t2}.
 template <class R>
 struct Rows {
-  static constexpr int N = R::NDOF;
+  static constexpr int N = R::NDOF, W = N + 4;
   static constexpr int MR = Dims<R>::MAXROWS > 0 ? Dims<R>::MAXROWS : 1;
   static constexpr int NC = Dims<R>::NC > 0 ? Dims<R>::NC : 1;
-  static constexpr int O_MEFF = MR * N, O_TGT = O_MEFF + MR, O_LAM = O_TGT + MR, O_HI = O_LAM + MR;
-  static constexpr int O_MU = O_HI + MR, WORDS = O_MU + NC;
-  float* __restrict__ base;  // already offset by env e
-  int n;
-  PBG_DEV float& y(int r, int i) const { return base[(size_t)(r * N + i) * n]; }
-  PBG_DEV float& meff(int r) const { return base[(size_t)(O_MEFF + r) * n]; }
-  PBG_DEV float& target(int r) const { return base[(size_t)(O_TGT + r) * n]; }
-  PBG_DEV float& lam(int r) const { return base[(size_t)(O_LAM + r) * n]; }
-  PBG_DEV float& hi(int r) const { return base[(size_t)(O_HI + r) * n]; }
-  PBG_DEV float& mu(int c) const { return base[(size_t)(O_MU + c) * n]; }
+  static constexpr int WORDS = MR * W;  // global workspace words per env
+  float* lds;  // LDS base + lane
+  float* gbl;  // global workspace base + env
+  int n;       // global stride (envs)
+  int cap;     // rows resident in LDS
+  // per-contact friction coefficient, LDS words [cap*W, cap*W + NC)
+  PBG_DEV float& mu(int c) const { return lds[(size_t)(cap * W + c) * 64]; }
+  template <class P>
+  static PBG_DEV void put_at(P p, size_t st, const float* y, float meff, float target, float hi) {
+#pragma unroll
+    for (int i = 0; i < N; i++) p[i * st] = y[i];
+    p[N * st] = meff;
+    p[(N + 1) * st] = target;
+    p[(N + 2) * st] = 0.f;
+    p[(N + 3) * st] = hi;
+  }
+  template <class P>
+  static PBG_DEV void solve_at(P p, size_t st, float* u, float lo, float hi_override) {
+    float yv[N];
+    float yu = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++) { yv[i] = p[i * st]; yu += yv[i] * u[i]; }
+    const float meff = p[N * st], tgt = p[(N + 1) * st], lam0 = p[(N + 2) * st];
+    const float hi = hi_override >= 0.f ? hi_override : p[(N + 3) * st];
+    const float nl = fminf(fmaxf(lam0 + meff * (tgt - yu), lo), hi);
+    const float dl = nl - lam0;
+    p[(N + 2) * st] = nl;
+#pragma unroll
+    for (int i = 0; i < N; i++) u[i] += yv[i] * dl;
+  }
+  PBG_DEV void put(int r, const float* y, float meff, float target, float hi) const {
+    if (r < cap) put_at(lds + (size_t)r * W * 64, (size_t)64, y, meff, target, hi);
+    else put_at(gbl + (size_t)r * W * n, (size_t)n, y, meff, target, hi);
+  }
+  PBG_DEV float lam(int r) const {
+    if (r < cap) return lds[((size_t)r * W + N + 2) * 64];
+    return gbl[((size_t)r * W + N + 2) * n];
+  }
+  // one projected Gauss-Seidel update of row r in u-space, bounds [lo, hi] (hi < 0: row's own)
+  PBG_DEV void solve(int r, float* u, float lo, float hi_override) const {
+    if (r < cap) solve_at(lds + (size_t)r * W * 64, (size_t)64, u, lo, hi_override);
+    else solve_at(gbl + (size_t)r * W * n, (size_t)n, u, lo, hi_override);
+  }
 };
 
 // ------------------------------------------------------------------ one physics sub-step
 // tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
 // of this sub-step's collision pass (feet contacts come from the last sub-step).
+#ifdef PBG_STAMPS
+#define SUB_STAMP_ARGS , unsigned long long& _st_t, unsigned long long* _st_acc
+#define SUB_STAMP_PASS , _st_t, _st_acc
+#else
+#define SUB_STAMP_ARGS
+#define SUB_STAMP_PASS
+#endif
 template <class R>
-PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R>& rw) {
+PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R>& rw SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
   constexpr float dt = (float)R::dt_sub;
@@ -246,6 +302,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     }
   }
 
+  STAMP(0)
   // --- composite inertia + wrench per body about the reference point O -----------------
   const f3 O = k.c[D::REF_BODY];
   float cm[NB];
@@ -338,6 +395,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     rhs[D::gj(d)] += tau[d] - (float)R::dof_damping[d] * s.qd[d];
   }
 
+  STAMP(1)
   // --- Cholesky (no fill-in in leaf-first order) ---------------------------------------
 #pragma unroll
   for (int j = 0; j < N; j++) {
@@ -400,6 +458,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     u[i] = t;
   }
 
+  STAMP(2)
   // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
   int nr = 0;
 #pragma unroll
@@ -427,21 +486,19 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       const float pos = side == 0 ? s.q[d] - (float)R::dof_lower[d] : (float)R::dof_upper[d] - s.q[d];
       const float vj = sg * vJ;
       const float tgt = pos > 0.f ? vj - pos / dt : -(float)PBG_LIMIT_ERP * pos / dt;
+      float ys[N];
 #pragma unroll
-      for (int i = 0; i < N; i++) rw.y(nr, i) = sg * y[i];
-      rw.meff(nr) = meff;
-      rw.target(nr) = tgt;
-      rw.lam(nr) = 0.f;
-      rw.hi(nr) = (float)PBG_LIMIT_MAX_IMPULSE;
+      for (int i = 0; i < N; i++) ys[i] = sg * y[i];
+      rw.put(nr, ys, meff, tgt, (float)PBG_LIMIT_MAX_IMPULSE);
       nr++;
     }
   }
+  STAMP(3)
   const int first_normal = nr;
   int nc = 0;
   // contact rows are staged: normals first (in contact order), frictions after.
   // Each contact stores its normal row now and its two friction rows at MAXROWS-space
   // offsets after all normals; friction rows are compacted once nc is known.
-  constexpr int FR0 = 2 * D::NLIM + D::NC;  // staging area for friction rows
 #pragma unroll
   for (int sl = 0; sl < R::NS; sl++) {
     const int b = R::slot_link[sl] + 1;
@@ -476,13 +533,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       float D2 = 0.f, vJ = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
-      const int row = dir == 0 ? first_normal + nc : FR0 + 2 * nc + (dir - 1);
-#pragma unroll
-      for (int i = 0; i < N; i++) rw.y(row, i) = y[i];
-      rw.meff(row) = D2 > 1e-12f ? 1.f / D2 : 0.f;
-      rw.target(row) = dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f;
-      rw.lam(row) = 0.f;
-      rw.hi(row) = 3.0e38f;
+      rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? 1.f / D2 : 0.f,
+             dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f, 3.0e38f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
@@ -558,53 +610,29 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
           D2 += y[i] * y[i];
           vJ += y[i] * u[i];
         }
-        const int row = dir == 0 ? first_normal + nc : FR0 + 2 * nc + (dir - 1);
-#pragma unroll
-        for (int i = 0; i < N; i++) rw.y(row, i) = y[i];
-        rw.meff(row) = D2 > 1e-12f ? 1.f / D2 : 0.f;
-        rw.target(row) = dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f;
-        rw.lam(row) = 0.f;
-        rw.hi(row) = 3.0e38f;
+        rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? 1.f / D2 : 0.f,
+               dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f, 3.0e38f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;
     }
   }
 
+  STAMP(4)
   // --- PGS: 5 sweeps in u-space (gym_locomotion_envs -> scene_bases.py:65 numSolverIterations=5)
-  const int n_fixed = first_normal + nc;  // limit rows + normal rows, contiguous
   for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
-    for (int r = 0; r < n_fixed; r++) {
-      float yu = 0.f;
-#pragma unroll
-      for (int i = 0; i < N; i++) yu += rw.y(r, i) * u[i];
-      const float lam0 = rw.lam(r);
-      const float nl = fminf(fmaxf(lam0 + rw.meff(r) * (rw.target(r) - yu), 0.f), rw.hi(r));
-      const float dl = nl - lam0;
-      rw.lam(r) = nl;
-#pragma unroll
-      for (int i = 0; i < N; i++) u[i] += rw.y(r, i) * dl;
-    }
-    for (int c = 0; c < nc; c++) {
-      const float ln = rw.lam(first_normal + c);
+    for (int r = 0; r < first_normal; r++) rw.solve(r, u, 0.f, -1.f);               // joint limits
+    for (int c = 0; c < nc; c++) rw.solve(first_normal + 3 * c, u, 0.f, 3.0e38f);   // contact normals
+    for (int c = 0; c < nc; c++) {                                                  // frictions
+      const float ln = rw.lam(first_normal + 3 * c);
       if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
       const float lim = rw.mu(c) * ln;
-#pragma unroll
-      for (int f = 0; f < 2; f++) {
-        const int r = FR0 + 2 * c + f;
-        float yu = 0.f;
-#pragma unroll
-        for (int i = 0; i < N; i++) yu += rw.y(r, i) * u[i];
-        const float lam0 = rw.lam(r);
-        const float nl = fminf(fmaxf(lam0 + rw.meff(r) * (rw.target(r) - yu), -lim), lim);
-        const float dl = nl - lam0;
-        rw.lam(r) = nl;
-#pragma unroll
-        for (int i = 0; i < N; i++) u[i] += rw.y(r, i) * dl;
-      }
+      rw.solve(first_normal + 3 * c + 1, u, -lim, lim);
+      rw.solve(first_normal + 3 * c + 2, u, -lim, lim);
     }
   }
 
+  STAMP(5)
   // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
 #pragma unroll
   for (int i = N - 1; i >= 0; i--) {
@@ -644,6 +672,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     const float inv = 1.f / sqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
     s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
   }
+  STAMP(6)
   return nc;
 }
 
@@ -977,9 +1006,11 @@ __global__ __launch_bounds__(64) void reset_kernel(Buffers B, ResetIO io) {
 }
 
 template <class R>
-__global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* __restrict__ scratch) {
+__global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int lds_rows) {
+  extern __shared__ float lds_dyn[];
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
+  STAMP_DECL
   State<R> s;
   load_state<R>(s, B.st, B.n, e);
   float act[R::NA];
@@ -996,10 +1027,13 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   }
   uint32_t slot_active[R::NS > 0 ? R::NS : 1];
   Rows<R> rw;
-  rw.base = scratch + e;
+  rw.lds = lds_dyn + (threadIdx.x & 63);
+  rw.gbl = scratch + e;
   rw.n = B.n;
+  rw.cap = lds_rows;
   int nc = 0;
-  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R>(s, tau, slot_active, rw);
+  STAMP(7)
+  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R>(s, tau, slot_active, rw SUB_STAMP_PASS);
   if (io.ncontact) io.ncontact[e] = nc;
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
@@ -1028,6 +1062,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
+  STAMP(8)
   const bool term = po.done;
   const bool trunc = el >= R::max_episode_steps;  // gym TimeLimit (envs/__init__.py max_episode_steps)
   io.rew[e] = (float)po.reward;
@@ -1055,6 +1090,8 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   store_state<R>(s, B.st, B.n, e);
 #pragma unroll
   for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+  STAMP(9)
+  STAMP_FLUSH
 }
 
 // Pack on explicit inputs (golden-vector parity of the device pack).  Per env the input

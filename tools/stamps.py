@@ -1,0 +1,29 @@
+"""Per-phase wave-cycle shares of the step kernel (diagnostic -DPBG_STAMPS build)."""
+import ctypes, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch
+import pybulletgym_amd
+from pybulletgym_amd import _native
+_native.LIB_PATH = os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd_stamps.so")
+from pybulletgym_amd.vec_env import VecEnv
+L = _native.lib()
+L.pbg_debug_stamps.argtypes = [ctypes.c_void_p]
+names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS", "integrate", "act+load", "pack", "store"]
+for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]))]:
+    env = VecEnv(env_id, n, seed=1, autoreset=True)
+    env.reset()
+    acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
+    for i in range(10): env.step(acts[i])
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 16)()
+    L.pbg_debug_stamps(buf)
+    steps = 20
+    for i in range(steps): env.step(acts[10 + i])
+    torch.cuda.synchronize()
+    L.pbg_debug_stamps(buf)
+    waves = (n + 63) // 64
+    tot = sum(buf[i] for i in range(10))
+    print(f"{env_id} n={n}: cycles per wave per env-step = {tot / waves / steps:.0f}")
+    for i in range(10):
+        print(f"   {names[i]:16s} {buf[i] / waves / steps:10.0f}  {100.0 * buf[i] / tot:5.1f}%")
