@@ -1,4 +1,5 @@
-// pbg_capi.hip -- the C-ABI (include/pbg.h) over the step/reset kernels of pbg_step.hip.
+// pbg_capi.hip -- the C-ABI (include/pbg.h).  Owns handles and device buffers and
+// dispatches to the per-robot launchers of pbg_robot.hip (one translation unit each).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -6,7 +7,11 @@
 #include <new>
 
 #include "../../include/pbg.h"
-#include "pbg_step.hip"
+#include "models_gen.h"
+#include "pbg_launch.h"
+#include "pbg_records.h"
+#include "pbg_types.h"
+#include "sim_params.h"
 
 namespace {
 
@@ -29,63 +34,69 @@ int env_robot_id(const char* env_id) {
   return -1;
 }
 
-// compile-time robot dispatch
-template <class F>
-int dispatch(int rid, F&& f) {
-  switch (rid) {
-    case 0: return f(pbg_models::Pendulum{});
-    case 1: return f(pbg_models::Hopper{});
-    case 2: return f(pbg_models::HalfCheetah{});
-    case 3: return f(pbg_models::Ant{});
-    case 4: return f(pbg_models::Humanoid{});
-  }
-  return fail(PBG_E_ENV, "unknown robot id%s %ld", "", rid);
+struct Ops {
+  int (*plan)(int, int, pbg::Geometry*);
+  int (*step)(const pbg::Buffers&, const pbg::StepIO&, float*, const pbg::Geometry&, hipStream_t);
+  int (*reset)(const pbg::Buffers&, const pbg::ResetIO&, hipStream_t);
+  int (*get_state)(const pbg::Buffers&, double*, double*, hipStream_t);
+  int (*set_state)(const pbg::Buffers&, const double*, const double*, hipStream_t);
+  int (*pack)(int, const double*, double*, hipStream_t);
+  pbg_info_t info;
+  int pack_in, pack_out;
+};
+
+template <class R>
+pbg_info_t info_of(int rid) {
+  pbg_info_t I;
+  I.robot_id = rid; I.n_envs = 0; I.action_dim = R::NA; I.obs_dim = R::OBS; I.n_dof = R::NDOF;
+  I.n_joints = R::NJ; I.n_links = R::NL; I.n_feet = R::NF; I.state_words = pbg::Records<R>::SD;
+  I.aux_words = pbg::Records<R>::AD; I.substeps = R::substeps; I.max_episode_steps = R::max_episode_steps;
+  I.reset_dofs = R::NR; I.floating = R::floating;
+  return I;
+}
+
+#define PBG_OPS(NAME, RID)                                                                               \
+  Ops{pbg::plan_##NAME, pbg::launch_step_##NAME, pbg::launch_reset_##NAME, pbg::launch_get_state_##NAME, \
+      pbg::launch_set_state_##NAME, pbg::launch_pack_##NAME, info_of<pbg_models::NAME>(RID),             \
+      pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
+
+const Ops* ops(int rid) {
+  static const Ops table[5] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+                               PBG_OPS(Humanoid, 4)};
+  return (rid >= 0 && rid < 5) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
-    hipGetDevice(&prev);
-    if (prev != dev) hipSetDevice(dev);
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
   }
   ~DeviceGuard() {
-    int cur;
-    hipGetDevice(&cur);
-    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && cur != prev) (void)hipSetDevice(prev);
   }
 };
 
-int hip_check(hipError_t e, const char* what) {
-  if (e == hipSuccess) return PBG_OK;
+int hip_check(int e, const char* what) {
+  if (e == (int)hipSuccess) return PBG_OK;
   return fail(PBG_E_HIP, "%s: HIP error %ld", what, (long)e);
 }
-
-inline unsigned grid_of(int n) { return (unsigned)((n + 63) / 64); }
 
 }  // namespace
 
 struct pbg_handle {
   int rid, device, n;
+  const Ops* ops;
   pbg::Buffers B;
   float* scratch;
-  int lds_rows;       // constraint rows kept in LDS per env
-  size_t lds_bytes;   // dynamic LDS per 64-lane workgroup
+  pbg::Geometry geo;
   pbg_info_t info;
 };
 
 extern "C" {
 
 const char* pbg_last_error(void) { return g_err; }
-
-#ifdef PBG_STAMPS
-// diagnostic build only: read and clear the per-phase wave-cycle sums
-int pbg_debug_stamps(unsigned long long* host_out) {
-  hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pbg::g_stamps), sizeof(unsigned long long) * 16);
-  unsigned long long z[16] = {0};
-  hipMemcpyToSymbol(HIP_SYMBOL(pbg::g_stamps), z, sizeof(z));
-  return 0;
-}
-#endif
 
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
@@ -99,58 +110,40 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
   DeviceGuard dg(device);
   pbg_handle* h = new (std::nothrow) pbg_handle();
   if (!h) return fail(PBG_E_NOMEM, "pbg_create: out of host memory%s%ld");
+  const Ops* o = ops(rid);
   h->rid = rid;
   h->device = device;
   h->n = n_envs;
-  int rc = dispatch(rid, [&](auto r) -> int {
-    using R = decltype(r);
-    const size_t n = (size_t)n_envs;
-    pbg_info_t& I = h->info;
-    I.robot_id = rid; I.n_envs = n_envs; I.action_dim = R::NA; I.obs_dim = R::OBS; I.n_dof = R::NDOF;
-    I.n_joints = R::NJ; I.n_links = R::NL; I.n_feet = R::NF; I.state_words = pbg::Dims<R>::SD;
-    I.aux_words = PBG_AUX_WORDS + R::NF; I.substeps = R::substeps; I.max_episode_steps = R::max_episode_steps;
-    I.reset_dofs = R::NR; I.floating = R::floating;
-    pbg::Buffers& B = h->B;
-    B.n = n_envs;
-    B.seed = seed;
-    B.env_offset = env_offset;
-    int e = 0;
-    e |= hip_check(hipMalloc(&B.st, sizeof(float) * n * pbg::Dims<R>::SD), "hipMalloc state");
-    e |= hip_check(hipMalloc(&B.pot, sizeof(double) * n), "hipMalloc potential");
-    e |= hip_check(hipMalloc(&B.z0, sizeof(float) * n), "hipMalloc z0");
-    e |= hip_check(hipMalloc(&B.elapsed, sizeof(int) * n), "hipMalloc elapsed");
-    e |= hip_check(hipMalloc(&B.flags, sizeof(uint32_t) * n), "hipMalloc flags");
-    e |= hip_check(hipMalloc(&B.episode, sizeof(uint32_t) * n), "hipMalloc episode");
-    e |= hip_check(hipMalloc(&h->scratch, sizeof(float) * n * pbg::Rows<R>::WORDS), "hipMalloc scratch");
-    if (e) return PBG_E_NOMEM;
-    e |= hip_check(hipMemset(B.st, 0, sizeof(float) * n * pbg::Dims<R>::SD), "hipMemset");
+  h->ops = o;
+  h->info = o->info;
+  h->info.n_envs = n_envs;
+  pbg::Buffers& B = h->B;
+  B.n = n_envs;
+  B.seed = seed;
+  B.env_offset = env_offset;
+  const size_t n = (size_t)n_envs;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  int e = hip_check(o->plan(n_envs, cus, &h->geo), "kernel attributes");
+  e |= hip_check(hipMalloc(&B.st, sizeof(float) * n * h->info.state_words), "hipMalloc state");
+  e |= hip_check(hipMalloc(&B.pot, sizeof(double) * n), "hipMalloc potential");
+  e |= hip_check(hipMalloc(&B.z0, sizeof(float) * n), "hipMalloc z0");
+  e |= hip_check(hipMalloc(&B.elapsed, sizeof(int) * n), "hipMalloc elapsed");
+  e |= hip_check(hipMalloc(&B.flags, sizeof(uint32_t) * n), "hipMalloc flags");
+  e |= hip_check(hipMalloc(&B.episode, sizeof(uint32_t) * n), "hipMalloc episode");
+  e |= hip_check(hipMalloc(&h->scratch, sizeof(float) * n * h->geo.scratch_words_per_env), "hipMalloc scratch");
+  if (!e) {
+    e |= hip_check(hipMemset(B.st, 0, sizeof(float) * n * h->info.state_words), "hipMemset");
     e |= hip_check(hipMemset(B.pot, 0, sizeof(double) * n), "hipMemset");
     e |= hip_check(hipMemset(B.z0, 0, sizeof(float) * n), "hipMemset");
     e |= hip_check(hipMemset(B.elapsed, 0, sizeof(int) * n), "hipMemset");
     e |= hip_check(hipMemset(B.flags, 0, sizeof(uint32_t) * n), "hipMemset");
     e |= hip_check(hipMemset(B.episode, 0, sizeof(uint32_t) * n), "hipMemset");
-    // LDS budget: all resident waves of a CU share 160 KiB; one wave per workgroup.
-    int cus = 256;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const int waves = (n_envs + 63) / 64;
-    const int wpc = (waves + cus - 1) / cus;
-    int maxlds = 163840;
-    const size_t budget = (size_t)maxlds / (size_t)(wpc > 0 ? wpc : 1);
-    using RW = pbg::Rows<R>;
-    long words = (long)(budget / (64 * sizeof(float))) - RW::NC;
-    int cap = (int)(words / RW::W);
-    if (cap > RW::MR) cap = RW::MR;
-    if (cap < 0) cap = 0;
-    h->lds_rows = cap;
-    h->lds_bytes = (size_t)64 * sizeof(float) * ((size_t)cap * RW::W + RW::NC);
-    e |= hip_check(hipFuncSetAttribute((const void*)pbg::step_kernel<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)h->lds_bytes), "hipFuncSetAttribute");
     e |= hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    return e ? PBG_E_HIP : PBG_OK;
-  });
-  if (rc != PBG_OK) {
+  }
+  if (e) {
     pbg_destroy(h);
-    return rc;
+    return PBG_E_HIP;
   }
   *out = h;
   return PBG_OK;
@@ -159,13 +152,9 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
 void pbg_destroy(pbg_handle* h) {
   if (!h) return;
   DeviceGuard dg(h->device);
-  hipFree(h->B.st);
-  hipFree(h->B.pot);
-  hipFree(h->B.z0);
-  hipFree(h->B.elapsed);
-  hipFree(h->B.flags);
-  hipFree(h->B.episode);
-  hipFree(h->scratch);
+  void* bufs[] = {h->B.st, h->B.pot, h->B.z0, h->B.elapsed, h->B.flags, h->B.episode, h->scratch};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
   delete h;
 }
 
@@ -179,11 +168,7 @@ int pbg_reset(pbg_handle* h, const uint8_t* mask, const float* init_q, float* ob
   if (!h || !obs) return fail(PBG_E_ARG, "pbg_reset: NULL handle or obs%s%ld");
   DeviceGuard dg(h->device);
   pbg::ResetIO io{mask, init_q, obs};
-  return dispatch(h->rid, [&](auto r) -> int {
-    using R = decltype(r);
-    hipLaunchKernelGGL(pbg::reset_kernel<R>, dim3(grid_of(h->n)), dim3(64), 0, (hipStream_t)stream, h->B, io);
-    return hip_check(hipGetLastError(), "reset_kernel launch");
-  });
+  return hip_check(h->ops->reset(h->B, io, (hipStream_t)stream), "reset_kernel launch");
 }
 
 int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
@@ -191,61 +176,58 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
     return fail(PBG_E_ARG, "pbg_step: NULL handle or required buffer%s%ld");
   DeviceGuard dg(h->device);
   pbg::StepIO s{io->act, io->obs, io->rew, io->rew64, io->done, io->trunc, io->term_obs, io->ncontact, io->autoreset};
-  return dispatch(h->rid, [&](auto r) -> int {
-    using R = decltype(r);
-    hipLaunchKernelGGL(pbg::step_kernel<R>, dim3(grid_of(h->n)), dim3(64), h->lds_bytes, (hipStream_t)stream, h->B,
-                       s, h->scratch, h->lds_rows);
-    return hip_check(hipGetLastError(), "step_kernel launch");
-  });
+  return hip_check(h->ops->step(h->B, s, h->scratch, h->geo, (hipStream_t)stream), "step_kernel launch");
 }
 
 int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* done, void* stream) {
   pbg_step_io_t io;
   memset(&io, 0, sizeof(io));
-  io.act = act; io.obs = obs; io.rew = rew; io.done = done;
+  io.act = act;
+  io.obs = obs;
+  io.rew = rew;
+  io.done = done;
   return pbg_step_ex(h, &io, stream);
 }
 
 int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream) {
   if (!h || !phys || !aux) return fail(PBG_E_ARG, "pbg_get_state: NULL argument%s%ld");
   DeviceGuard dg(h->device);
-  return dispatch(h->rid, [&](auto r) -> int {
-    using R = decltype(r);
-    hipLaunchKernelGGL(pbg::get_state_kernel<R>, dim3(grid_of(h->n)), dim3(64), 0, (hipStream_t)stream, h->B, phys, aux);
-    return hip_check(hipGetLastError(), "get_state launch");
-  });
+  return hip_check(h->ops->get_state(h->B, phys, aux, (hipStream_t)stream), "get_state launch");
 }
 
 int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream) {
   if (!h || !phys) return fail(PBG_E_ARG, "pbg_set_state: NULL argument%s%ld");
   DeviceGuard dg(h->device);
-  return dispatch(h->rid, [&](auto r) -> int {
-    using R = decltype(r);
-    hipLaunchKernelGGL(pbg::set_state_kernel<R>, dim3(grid_of(h->n)), dim3(64), 0, (hipStream_t)stream, h->B, phys, aux);
-    return hip_check(hipGetLastError(), "set_state launch");
-  });
+  return hip_check(h->ops->set_state(h->B, phys, aux, (hipStream_t)stream), "set_state launch");
 }
 
 int pbg_pack_record_sizes(const char* env_id, int* in_words, int* out_words) {
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_pack_record_sizes: unknown env id '%s'%ld", env_id ? env_id : "(null)");
-  return dispatch(rid, [&](auto r) -> int {
-    using R = decltype(r);
-    if (in_words) *in_words = pbg::PackRec<R>::IN;
-    if (out_words) *out_words = pbg::PackRec<R>::OUT;
-    return PBG_OK;
-  });
+  if (in_words) *in_words = ops(rid)->pack_in;
+  if (out_words) *out_words = ops(rid)->pack_out;
+  return PBG_OK;
 }
+
+#ifdef PBG_STAMPS
+// diagnostic build only: read and clear the per-phase wave-cycle sums of one robot's kernel
+int pbg_debug_stamps(int rid, unsigned long long* host_out) {
+  switch (rid) {
+    case 0: return pbg::debug_stamps_Pendulum(host_out);
+    case 1: return pbg::debug_stamps_Hopper(host_out);
+    case 2: return pbg::debug_stamps_HalfCheetah(host_out);
+    case 3: return pbg::debug_stamps_Ant(host_out);
+    case 4: return pbg::debug_stamps_Humanoid(host_out);
+  }
+  return PBG_E_ENV;
+}
+#endif
 
 int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, void* stream) {
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_pack: unknown env id '%s'%ld", env_id ? env_id : "(null)");
   if (n <= 0 || !in_rec || !out_rec) return fail(PBG_E_ARG, "pbg_pack: bad arguments%s%ld");
-  return dispatch(rid, [&](auto r) -> int {
-    using R = decltype(r);
-    hipLaunchKernelGGL(pbg::pack_kernel<R>, dim3(grid_of(n)), dim3(64), 0, (hipStream_t)stream, n, in_rec, out_rec);
-    return hip_check(hipGetLastError(), "pack_kernel launch");
-  });
+  return hip_check(ops(rid)->pack(n, in_rec, out_rec, (hipStream_t)stream), "pack_kernel launch");
 }
 
 }  // extern "C"

@@ -1,0 +1,35 @@
+// Host-side launchers, one set per robot, each compiled in its own translation unit
+// (pbg_robot.hip with -DPBG_ROBOT=<Name>) so the five template instantiations build in
+// parallel.  pbg_capi.hip dispatches on the robot id.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pbg {
+struct Buffers;
+struct StepIO;
+struct ResetIO;
+
+struct Geometry {
+  int block;         // lanes (envs) per step workgroup: 16, 32 or 64
+  int lds_rows;      // constraint rows resident in LDS per env
+  size_t lds_bytes;  // dynamic LDS per step workgroup
+  size_t scratch_words_per_env;
+};
+
+#define PBG_DECLARE_ROBOT(NAME)                                                                            \
+  int plan_##NAME(int n_envs, int cus, Geometry* g);                                                       \
+  int launch_step_##NAME(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s); \
+  int launch_reset_##NAME(const Buffers& B, const ResetIO& io, hipStream_t s);                             \
+  int launch_get_state_##NAME(const Buffers& B, double* phys, double* aux, hipStream_t s);                 \
+  int launch_set_state_##NAME(const Buffers& B, const double* phys, const double* aux, hipStream_t s);     \
+  int launch_pack_##NAME(int n, const double* in, double* out, hipStream_t s);                              \
+  int debug_stamps_##NAME(unsigned long long* host_out);
+
+PBG_DECLARE_ROBOT(Pendulum)
+PBG_DECLARE_ROBOT(Hopper)
+PBG_DECLARE_ROBOT(HalfCheetah)
+PBG_DECLARE_ROBOT(Ant)
+PBG_DECLARE_ROBOT(Humanoid)
+}  // namespace pbg

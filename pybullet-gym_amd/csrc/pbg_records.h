@@ -1,0 +1,20 @@
+// Record sizes shared by the kernels and the C-ABI layer.
+#pragma once
+#include "sim_params.h"
+
+namespace pbg {
+// Pack on explicit inputs (golden-vector parity of the device pack).  Per env the input
+// record is float64: [part_xyz (NP+1)*3 | n_parts | quat 4 | pos 3 | vel 3 | jq NO | jqd NO |
+// feet_prev NF | feet_new NF | act NA | potential_old | initial_z_in | is_step]; the output
+// record: [obs OBS | reward | done | potential | initial_z | feet_out NF].
+template <class R>
+struct PackRec {
+  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3;
+  static constexpr int OUT = R::OBS + 4 + R::NF;
+};
+template <class R>
+struct Records {
+  static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;  // physical state words
+  static constexpr int AD = PBG_AUX_WORDS + R::NF;       // bookkeeping words
+};
+}  // namespace pbg

@@ -1,0 +1,86 @@
+// pbg_robot.hip -- per-robot kernel instantiations + launchers.  Compiled once per robot
+// with -DPBG_ROBOT=<Pendulum|Hopper|HalfCheetah|Ant|Humanoid>.
+#include <hip/hip_runtime.h>
+
+#include "pbg_launch.h"
+#include "pbg_step.hip"
+
+#ifndef PBG_ROBOT
+#error "compile with -DPBG_ROBOT=<robot struct name>"
+#endif
+#define PBG_CAT2(a, b) a##b
+#define PBG_CAT(a, b) PBG_CAT2(a, b)
+#define PBG_FN(prefix) PBG_CAT(prefix, PBG_ROBOT)
+
+namespace pbg {
+using R = pbg_models::PBG_ROBOT;
+
+static inline unsigned blocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
+
+// Geometry: one env per lane, one wave per workgroup.  With fewer than 64 envs per CU
+// the workgroup shrinks to 32 or 16 active lanes so every CU gets a wave (the step is
+// issue/latency bound: a wave's time barely depends on its active lanes).  All resident
+// workgroups of a CU share the 160 KiB LDS for their constraint rows.
+int PBG_FN(plan_)(int n_envs, int cus, Geometry* g) {
+  const int per_cu = (n_envs + cus - 1) / cus;
+  int b = 16;
+  while (b < per_cu && b < 64) b *= 2;
+  const int wgs = (n_envs + b - 1) / b;
+  const int wpc = (wgs + cus - 1) / cus;
+  const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
+  using RW = Rows<R, 64>;
+  long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC;
+  int cap = (int)(words / RW::W);
+  if (cap > RW::MR) cap = RW::MR;
+  if (cap < 0) cap = 0;
+  g->block = b;
+  g->lds_rows = cap;
+  g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)cap * RW::W + RW::NC);
+  g->scratch_words_per_env = RW::WORDS;
+  hipError_t e = hipSuccess;
+  if (b == 64) e = hipFuncSetAttribute((const void*)step_kernel<R, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+  else if (b == 32) e = hipFuncSetAttribute((const void*)step_kernel<R, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+  else e = hipFuncSetAttribute((const void*)step_kernel<R, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+  return (int)e;
+}
+
+int PBG_FN(launch_step_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  const dim3 grid(blocks(B.n, g.block)), blk(g.block);
+  if (g.block == 64) hipLaunchKernelGGL((step_kernel<R, 64>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+  else if (g.block == 32) hipLaunchKernelGGL((step_kernel<R, 32>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+  else hipLaunchKernelGGL((step_kernel<R, 16>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+  return (int)hipGetLastError();
+}
+
+int PBG_FN(launch_reset_)(const Buffers& B, const ResetIO& io, hipStream_t s) {
+  hipLaunchKernelGGL(reset_kernel<R>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, io);
+  return (int)hipGetLastError();
+}
+
+int PBG_FN(launch_get_state_)(const Buffers& B, double* phys, double* aux, hipStream_t s) {
+  hipLaunchKernelGGL(get_state_kernel<R>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, phys, aux);
+  return (int)hipGetLastError();
+}
+
+int PBG_FN(launch_set_state_)(const Buffers& B, const double* phys, const double* aux, hipStream_t s) {
+  hipLaunchKernelGGL(set_state_kernel<R>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, phys, aux);
+  return (int)hipGetLastError();
+}
+
+int PBG_FN(launch_pack_)(int n, const double* in, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(pack_kernel<R>, dim3(blocks(n, 64)), dim3(64), 0, s, n, in, out);
+  return (int)hipGetLastError();
+}
+
+int PBG_FN(debug_stamps_)(unsigned long long* host_out) {
+#ifdef PBG_STAMPS
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -3;
+  unsigned long long z[16] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -3;
+  return 0;
+#else
+  (void)host_out;
+  return -1;
+#endif
+}
+}  // namespace pbg

@@ -23,6 +23,8 @@
 
 #include "models_gen.h"
 #include "pbg_math.h"
+#include "pbg_records.h"
+#include "pbg_types.h"
 #include "sim_params.h"
 
 namespace pbg {
@@ -175,22 +177,23 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
 
 // ------------------------------------------------------------------ per-substep scratch
 // Constraint rows: row r = [y (NDOF) | meff | target | lambda | hi].  Rows 0..cap-1 live
-// in LDS (dynamic shared memory, [word][64 lanes]: conflict-free, ~100-cycle latency);
+// in LDS (dynamic shared memory, [word][lane]: conflict-free, ~100-cycle latency);
 // rows >= cap (rare: many simultaneous contacts) in a device workspace laid out
 // [word][env] so that each access is one coalesced wave access.  Row order:
 // limit rows [0, 2*NLIM), then contact c at 2*NLIM + 3c + {normal, t1, t2}.
-template <class R>
+template <class R, int LS = 64>
 struct Rows {
   static constexpr int N = R::NDOF, W = N + 4;
   static constexpr int MR = Dims<R>::MAXROWS > 0 ? Dims<R>::MAXROWS : 1;
   static constexpr int NC = Dims<R>::NC > 0 ? Dims<R>::NC : 1;
   static constexpr int WORDS = MR * W;  // global workspace words per env
+  static constexpr int ls = LS;  // LDS stride = lanes per workgroup
   float* lds;  // LDS base + lane
   float* gbl;  // global workspace base + env
   int n;       // global stride (envs)
   int cap;     // rows resident in LDS
   // per-contact friction coefficient, LDS words [cap*W, cap*W + NC)
-  PBG_DEV float& mu(int c) const { return lds[(size_t)(cap * W + c) * 64]; }
+  PBG_DEV float& mu(int c) const { return lds[(size_t)(cap * W + c) * ls]; }
   template <class P>
   static PBG_DEV void put_at(P p, size_t st, const float* y, float meff, float target, float hi) {
 #pragma unroll
@@ -215,16 +218,16 @@ struct Rows {
     for (int i = 0; i < N; i++) u[i] += yv[i] * dl;
   }
   PBG_DEV void put(int r, const float* y, float meff, float target, float hi) const {
-    if (r < cap) put_at(lds + (size_t)r * W * 64, (size_t)64, y, meff, target, hi);
+    if (r < cap) put_at(lds + (size_t)r * W * ls, (size_t)ls, y, meff, target, hi);
     else put_at(gbl + (size_t)r * W * n, (size_t)n, y, meff, target, hi);
   }
   PBG_DEV float lam(int r) const {
-    if (r < cap) return lds[((size_t)r * W + N + 2) * 64];
+    if (r < cap) return lds[((size_t)r * W + N + 2) * ls];
     return gbl[((size_t)r * W + N + 2) * n];
   }
   // one projected Gauss-Seidel update of row r in u-space, bounds [lo, hi] (hi < 0: row's own)
   PBG_DEV void solve(int r, float* u, float lo, float hi_override) const {
-    if (r < cap) solve_at(lds + (size_t)r * W * 64, (size_t)64, u, lo, hi_override);
+    if (r < cap) solve_at(lds + (size_t)r * W * ls, (size_t)ls, u, lo, hi_override);
     else solve_at(gbl + (size_t)r * W * n, (size_t)n, u, lo, hi_override);
   }
 };
@@ -239,8 +242,8 @@ struct Rows {
 #define SUB_STAMP_ARGS
 #define SUB_STAMP_PASS
 #endif
-template <class R>
-PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R>& rw SUB_STAMP_ARGS) {
+template <class R, int LS>
+PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
   constexpr float dt = (float)R::dt_sub;
@@ -910,37 +913,6 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
   for (int i = 0; i < R::NO; i++) { in.jq[i] = s.q[R::obs_dof[i]]; in.jqd[i] = s.qd[R::obs_dof[i]]; }
 }
 
-// ------------------------------------------------------------------ kernel arguments
-struct Buffers {
-  int n;                   // envs on this device
-  float* st;               // [SD][n] physical state, SoA
-  double* pot;             // [n] potential
-  float* z0;               // [n] initial_z
-  int* elapsed;            // [n] steps in episode
-  uint32_t* flags;         // [n] bit0 floor-in-parts, bits 8.. feet_contact
-  uint32_t* episode;       // [n] resets so far (RNG counter)
-  uint64_t seed;
-  int env_offset;          // global id of env 0 (multi-GPU sharding)
-};
-
-struct StepIO {
-  const float* act;        // [n][NA]
-  float* obs;              // [n][OBS]
-  float* rew;              // [n] float32 reward
-  double* rew64;           // [n] nullable float64 reward
-  uint8_t* done;           // [n] terminated | truncated
-  uint8_t* trunc;          // [n] nullable, TimeLimit truncation
-  float* term_obs;         // [n][OBS] nullable: obs before an auto-reset
-  int32_t* ncontact;       // [n] nullable: contacts in the last sub-step
-  int autoreset;
-};
-
-struct ResetIO {
-  const uint8_t* mask;     // [n] nullable = all
-  const float* init_q;     // [n][NR] nullable = Philox noise U(-0.1, 0.1)
-  float* obs;              // [n][OBS]
-};
-
 template <class R>
 PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
                        double& pot, float& z0) {
@@ -1005,7 +977,7 @@ __global__ __launch_bounds__(64) void reset_kernel(Buffers B, ResetIO io) {
   for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
 }
 
-template <class R>
+template <class R, int LS>
 __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int lds_rows) {
   extern __shared__ float lds_dyn[];
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1026,14 +998,14 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
   }
   uint32_t slot_active[R::NS > 0 ? R::NS : 1];
-  Rows<R> rw;
-  rw.lds = lds_dyn + (threadIdx.x & 63);
+  Rows<R, LS> rw;
+  rw.lds = lds_dyn + threadIdx.x;
   rw.gbl = scratch + e;
   rw.n = B.n;
   rw.cap = lds_rows;
   int nc = 0;
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R>(s, tau, slot_active, rw SUB_STAMP_PASS);
+  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R, LS>(s, tau, slot_active, rw SUB_STAMP_PASS);
   if (io.ncontact) io.ncontact[e] = nc;
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
@@ -1098,11 +1070,6 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
 // record is float64: [part_xyz (NP+1)*3 | n_parts | quat 4 | pos 3 | vel 3 | jq NO | jqd NO |
 // feet_prev NF | feet_new NF | act NA | potential_old | initial_z_in | is_step]; the output
 // record: [obs OBS | reward | done | potential | initial_z | feet_out NF].
-template <class R>
-struct PackRec {
-  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3;
-  static constexpr int OUT = R::OBS + 4 + R::NF;
-};
 template <class R>
 __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restrict__ inrec, double* __restrict__ outrec) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;

@@ -8,7 +8,7 @@ from pybulletgym_amd import _native
 _native.LIB_PATH = os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd_stamps.so")
 from pybulletgym_amd.vec_env import VecEnv
 L = _native.lib()
-L.pbg_debug_stamps.argtypes = [ctypes.c_void_p]
+L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
 names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS", "integrate", "act+load", "pack", "store"]
 for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]))]:
     env = VecEnv(env_id, n, seed=1, autoreset=True)
@@ -17,12 +17,13 @@ for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] o
     for i in range(10): env.step(acts[i])
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
-    L.pbg_debug_stamps(buf)
+    rid = _native.ROBOT_IDS[env_id]
+    L.pbg_debug_stamps(rid, buf)
     steps = 20
     for i in range(steps): env.step(acts[10 + i])
     torch.cuda.synchronize()
-    L.pbg_debug_stamps(buf)
-    waves = (n + 63) // 64
+    L.pbg_debug_stamps(rid, buf)
+    waves = (n + env.block - 1) // env.block if hasattr(env, 'block') else (n + 63) // 64
     tot = sum(buf[i] for i in range(10))
     print(f"{env_id} n={n}: cycles per wave per env-step = {tot / waves / steps:.0f}")
     for i in range(10):
