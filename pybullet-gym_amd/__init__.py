@@ -1,2 +1,21 @@
 """pybulletgym_amd: MI355X-native batched stepper for the roboschool locomotion envs of
-josiahls/pybullet-gym.  Import as ``import pybulletgym_amd``."""
+josiahls/pybullet-gym (InvertedPendulum, Hopper, HalfCheetah, Ant, Humanoid
+``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
+
+    from pybulletgym_amd import VecEnv, make
+    envs = VecEnv("AntPyBulletEnv-v0", 16384)      # device-resident batch, one launch per step
+    env = make("AntPyBulletEnv-v0")                  # single env, gym.Env-style surface
+"""
+ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
+           "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0")
+
+
+def __getattr__(name):
+    # lazy: keep `import pybulletgym_amd` cheap and torch-free for the model compiler
+    if name == "VecEnv":
+        from .vec_env import VecEnv
+        return VecEnv
+    if name in ("make", "register_with_gym"):
+        from . import envs
+        return getattr(envs, name)
+    raise AttributeError(name)

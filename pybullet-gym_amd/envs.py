@@ -1,0 +1,343 @@
+"""Drop-in mirror of the reference's env / robot / scene class surface.
+
+The reference's user-facing API is ``gym.make('AntPyBulletEnv-v0')`` returning a
+``WalkerBaseBulletEnv`` whose ``reset()`` / ``step(a)`` drive pybullet
+(pybulletgym/envs/roboschool/{env_bases,gym_locomotion_envs,gym_pendulum_envs,
+robot_locomotors,robot_pendula,scene_bases,scene_stadium}.py).  The same class names,
+constructor signatures, class constants and return types live here; the physics and
+the observation/reward pack run in the HIP step kernel (one env = a VecEnv of size 1).
+For throughput use ``pybulletgym_amd.VecEnv`` directly: thousands of envs per launch.
+
+Out of scope (not on the hot path): rendering/cameras (``render`` returns an empty array
+as the reference does for non-rgb modes), multiplayer scenes, HUD.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import robots as _robots
+from .spaces import Box
+
+
+# ----------------------------------------------------------------------------- scenes
+class Scene:
+    """scene_bases.py:8-52.  dt = timestep * frame_skip; the sub-stepped World.step is
+    fused into the step kernel, so global_step() is not callable on its own."""
+    multiplayer = False
+
+    def __init__(self, bullet_client=None, gravity=9.8, timestep=0.0165 / 4, frame_skip=4):
+        self.gravity = gravity
+        self.timestep = timestep
+        self.frame_skip = frame_skip
+        self.dt = self.timestep * self.frame_skip
+        self.numSolverIterations = 5  # scene_bases.py:65
+
+    def global_step(self):
+        raise NotImplementedError("the physics step is fused into the batched kernel; call env.step(a)")
+
+
+class SingleRobotEmptyScene(Scene):
+    """scene_bases.py:54-55 (pendulum: no floor)."""
+    multiplayer = False
+
+
+class StadiumScene(Scene):
+    """scene_stadium.py:10-35: the floor plane, lateral friction 0.8, restitution 0.5."""
+    multiplayer = False
+    zero_at_running_strip_start_line = True
+    stadium_halflen = 105 * 0.25
+    stadium_halfwidth = 50 * 0.25
+    floor_lateral_friction = 0.8
+    floor_restitution = 0.5
+
+
+# ----------------------------------------------------------------------------- robots
+class XmlBasedRobot:
+    """robot_bases.py:10-30: action/observation spaces from the dims."""
+    self_collision = True
+
+    def __init__(self, robot_name, action_dim, obs_dim, self_collision=True):
+        high = np.ones([action_dim], dtype=np.float32)
+        self.action_space = Box(-high, high)
+        high = np.inf * np.ones([obs_dim], dtype=np.float32)
+        self.observation_space = Box(-high, high)
+        self.robot_name = robot_name
+        self.self_collision = self_collision
+
+
+class MJCFBasedRobot(XmlBasedRobot):
+    """robot_bases.py:97-129."""
+
+    def __init__(self, model_xml, robot_name, action_dim, obs_dim, self_collision=True):
+        XmlBasedRobot.__init__(self, robot_name, action_dim, obs_dim, self_collision)
+        self.model_xml = model_xml
+
+
+class WalkerBase(XmlBasedRobot):
+    """robot_locomotors.py:7-79 constants (target, power)."""
+
+    def __init__(self, power):
+        self.power = power
+        self.walk_target_x = 1e3
+        self.walk_target_y = 0
+        self.body_xyz = [0, 0, 0]
+
+
+def _robot_class(key, base_cls):
+    spec = _robots.spec_for(key)
+
+    bases = (WalkerBase, MJCFBasedRobot) if spec.kind == _robots.KIND_WALKER else (MJCFBasedRobot,)
+
+    class _R(*bases):
+        foot_list = list(spec.foot_list)
+
+        def __init__(self):
+            if spec.kind == _robots.KIND_WALKER:
+                WalkerBase.__init__(self, power=spec.power)
+            MJCFBasedRobot.__init__(self, spec.mjcf, spec.robot_name, action_dim=spec.action_dim,
+                                    obs_dim=spec.obs_dim)
+            self.spec = spec
+
+    _R.__name__ = base_cls
+    return _R
+
+
+Hopper = _robot_class("hopper", "Hopper")                    # robot_locomotors.py:82-90
+HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
+Ant = _robot_class("ant", "Ant")                             # :130-138
+Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
+InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
+
+
+def _alive_bonus_hopper(self, z, pitch):
+    return +1 if z > 0.8 and abs(pitch) < 1.0 else -1
+
+
+def _alive_bonus_ant(self, z, pitch):
+    return +1 if z > 0.26 else -1
+
+
+def _alive_bonus_humanoid(self, z, pitch):
+    return +2 if z > 0.78 else -1
+
+
+Hopper.alive_bonus = _alive_bonus_hopper
+Ant.alive_bonus = _alive_bonus_ant
+Humanoid.alive_bonus = _alive_bonus_humanoid
+
+
+# ----------------------------------------------------------------------------- envs
+class BaseBulletEnv:
+    """env_bases.py:9-121 surface: reset() -> obs, step(a) -> (obs, reward, done, {}),
+    seed(), render(), close().  One env on one GPU via the batched kernel."""
+    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 60}
+    env_id = None
+
+    def __init__(self, robot, render=False, device="cuda:0"):
+        self.robot = robot
+        self.isRender = render
+        self.action_space = robot.action_space
+        self.observation_space = robot.observation_space
+        self.device = device
+        self._seed_value = 0
+        self._vec = None
+        self.scene = None
+        self.reward = 0.0
+        self.frame = 0
+
+    def _make_vec(self):
+        from .vec_env import VecEnv
+        self._vec = VecEnv(self.env_id, 1, device=self.device, seed=self._seed_value, autoreset=False)
+
+    def seed(self, seed=None):
+        self._seed_value = 0 if seed is None else int(seed)
+        self.action_space.seed(seed)
+        if self._vec is not None:
+            self._vec.close()
+            self._vec = None
+        return [self._seed_value]
+
+    def reset(self):
+        if self._vec is None:
+            self._make_vec()
+        self.frame = 0
+        self.reward = 0.0
+        obs = self._vec.reset()
+        return self._obs_out(obs)
+
+    def step(self, a):
+        import torch
+        if self._vec is None:
+            raise RuntimeError("call reset() before step()")
+        a = np.asarray(a, dtype=np.float32).reshape(1, -1)
+        assert np.isfinite(a).all()  # robot_locomotors.py:27
+        res = self._vec.step(torch.from_numpy(a), want_reward64=True)
+        r = float(self._vec.reward64[0])
+        done = bool(res.done[0])
+        self.frame += 1
+        self.reward += r
+        return self._obs_out(res.obs), r, done, {}
+
+    def _obs_out(self, obs):
+        return obs[0].cpu().numpy()
+
+    def render(self, mode="human", close=False):
+        return np.array([])  # env_bases.py:73-77 for non-rgb modes; rendering is out of scope
+
+    def close(self):
+        if self._vec is not None:
+            self._vec.close()
+            self._vec = None
+
+    def HUD(self, state, a, done):
+        pass
+
+    # gym < 0.9.6 spelling used by the reference (env_bases.py:114-121)
+    _reset = reset
+    _step = step
+    _seed = seed
+    _close = close
+    _render = render
+
+
+class WalkerBaseBulletEnv(BaseBulletEnv):
+    """gym_locomotion_envs.py:8-119: reward-term constants as class attributes."""
+    electricity_cost = -2.0
+    stall_torque_cost = -0.1
+    foot_collision_cost = -1.0
+    foot_ground_object_names = set(["floor"])
+    joints_at_limit_cost = -0.1
+
+    def __init__(self, robot, render=False, device="cuda:0"):
+        BaseBulletEnv.__init__(self, robot, render, device)
+        self.camera_x = 0
+        self.walk_target_x = 1e3
+        self.walk_target_y = 0
+        self.stateId = -1
+        self.scene = self.create_single_player_scene(None)
+
+    def create_single_player_scene(self, bullet_client):
+        self.stadium_scene = StadiumScene(bullet_client, gravity=9.8, timestep=0.0165 / 4, frame_skip=4)
+        return self.stadium_scene
+
+
+class HopperBulletEnv(WalkerBaseBulletEnv):
+    env_id = "HopperPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = Hopper()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+
+
+class HalfCheetahBulletEnv(WalkerBaseBulletEnv):
+    env_id = "HalfCheetahPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = HalfCheetah()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+
+
+class AntBulletEnv(WalkerBaseBulletEnv):
+    env_id = "AntPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = Ant()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+
+
+class HumanoidBulletEnv(WalkerBaseBulletEnv):
+    env_id = "HumanoidPyBulletEnv-v0"
+
+    def __init__(self, robot=None, render=False, device="cuda:0"):
+        # gym_locomotion_envs.py:147 shares one default Humanoid() between instances; each
+        # env here owns its own robot record (the batched state is per env anyway).
+        self.robot = robot if robot is not None else Humanoid()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        self.electricity_cost = 4.25 * WalkerBaseBulletEnv.electricity_cost
+        self.stall_torque_cost = 4.25 * WalkerBaseBulletEnv.stall_torque_cost
+
+
+class InvertedPendulumBulletEnv(BaseBulletEnv):
+    """gym_pendulum_envs.py:7-42: obs float64 [x, vx, cos(theta), sin(theta), theta_dot]."""
+    env_id = "InvertedPendulumPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = InvertedPendulum()
+        BaseBulletEnv.__init__(self, self.robot, render, device)
+        self.stateId = -1
+        self.scene = self.create_single_player_scene(None)
+
+    def create_single_player_scene(self, bullet_client):
+        return SingleRobotEmptyScene(bullet_client, gravity=9.8, timestep=0.0165, frame_skip=1)
+
+    def _obs_out(self, obs):
+        return obs[0].cpu().numpy().astype(np.float64)
+
+
+ENV_CLASSES = {
+    "InvertedPendulumPyBulletEnv-v0": InvertedPendulumBulletEnv,
+    "HopperPyBulletEnv-v0": HopperBulletEnv,
+    "HalfCheetahPyBulletEnv-v0": HalfCheetahBulletEnv,
+    "AntPyBulletEnv-v0": AntBulletEnv,
+    "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
+}
+# envs/__init__.py:4-103 registry facts
+MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
+REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
+                    "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
+
+
+class TimeLimit:
+    """gym's TimeLimit wrapper as applied by the registry (max_episode_steps)."""
+
+    def __init__(self, env, max_episode_steps):
+        self.env = env
+        self._max = max_episode_steps
+        self._elapsed = 0
+        self.action_space, self.observation_space = env.action_space, env.observation_space
+
+    def reset(self):
+        self._elapsed = 0
+        return self.env.reset()
+
+    def step(self, a):
+        obs, r, done, info = self.env.step(a)
+        self._elapsed += 1
+        if self._elapsed >= self._max:
+            info["TimeLimit.truncated"] = not done
+            done = True
+        return obs, r, done, info
+
+    def seed(self, seed=None):
+        return self.env.seed(seed)
+
+    def close(self):
+        return self.env.close()
+
+    def __getattr__(self, k):
+        return getattr(self.env, k)
+
+
+def make(env_id: str, device="cuda:0"):
+    """gym.make(env_id) equivalent: the env class behind gym's TimeLimit."""
+    if env_id not in ENV_CLASSES:
+        raise KeyError(f"unknown env id {env_id!r}; known: {sorted(ENV_CLASSES)}")
+    return TimeLimit(ENV_CLASSES[env_id](device=device), MAX_EPISODE_STEPS[env_id])
+
+
+def register_with_gym():
+    """Register the ids with gym's registry when gym is importable (it is optional)."""
+    try:
+        from gym.envs.registration import register
+    except Exception:
+        return False
+    for env_id, cls in ENV_CLASSES.items():
+        kw = dict(id=env_id, entry_point=f"pybulletgym_amd.envs:{cls.__name__}",
+                  max_episode_steps=MAX_EPISODE_STEPS[env_id])
+        if env_id in REWARD_THRESHOLD:
+            kw["reward_threshold"] = REWARD_THRESHOLD[env_id]
+        try:
+            register(**kw)
+        except Exception:
+            pass
+    return True

@@ -212,3 +212,36 @@ def test_large_batch_stays_finite():
     phys, _ = env.get_state()
     assert torch.isfinite(phys).all()
     assert dones < n * 200
+
+
+# ------------------------------------------------------------------ gym-style facade
+@pytest.mark.parametrize("env_id", ENVS)
+def test_sanity_check_every_env(env_id):
+    """gym_sanity_check.py:1-18: make, reset, one step of np.random.random(shape)."""
+    from pybulletgym_amd import make
+    env = make(env_id)
+    obs = env.reset()
+    assert obs.shape == env.observation_space.shape
+    obs, r, done, info = env.step(np.random.random(env.action_space.shape))
+    assert isinstance(r, float) and isinstance(done, bool) and isinstance(info, dict)
+    assert obs.dtype == (np.float64 if "Pendulum" in env_id else np.float32)
+    env.close()
+
+
+def test_facade_matches_vecenv_and_time_limit():
+    from pybulletgym_amd import make
+    env = make("HopperPyBulletEnv-v0")
+    env.seed(3)
+    o = env.reset()
+    vec = VecEnv("HopperPyBulletEnv-v0", 1, seed=3, autoreset=False)
+    ov = vec.reset()
+    np.testing.assert_array_equal(o, ov[0].cpu().numpy())
+    a = np.array([0.3, -0.2, 0.5], np.float32)
+    o1, r1, d1, _ = env.step(a)
+    res = vec.step(torch.from_numpy(a.reshape(1, 3)), want_reward64=True)
+    np.testing.assert_array_equal(o1, res.obs[0].cpu().numpy())
+    assert r1 == float(vec.reward64[0])
+    env.env._vec.set_state(*env.env._vec.get_state())
+    env._elapsed = 999
+    _, _, done, info = env.step(a)
+    assert done
