@@ -74,6 +74,14 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
                 m |= 1 << links[a].dof
         chain_mask.append(m)
 
+    # link ancestor masks: bit j set if link j is link l or one of its ancestors
+    anc_mask = []
+    for li in range(L):
+        m = 1 << li
+        for a in model.ancestors(li):
+            m |= 1 << a
+        anc_mask.append(m)
+
     # floor contact slots: sphere -> centre, capsule -> both segment endpoints
     slots = []
     if spec.floor:
@@ -136,6 +144,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         link_axis=[list(l.axis) for l in links], link_anchor=[list(l.anchor) for l in links],
         link_mass=[l.mass for l in links], link_com=[list(l.com) for l in links],
         link_inertia=[inertia6(l.inertia) for l in links], link_chain_mask=chain_mask,
+        link_anc_mask=anc_mask,
         dof_lower=dof["lower"], dof_upper=dof["upper"], dof_limited=dof["limited"],
         dof_damping=dof["damping"], dof_armature=dof["armature"], dof_jtype=dof["jtype"],
         dof_link=dof["link"],
@@ -216,6 +225,7 @@ def emit_struct(t: Dict) -> str:
     for k in ("link_parent", "link_jtype", "link_dof"):
         L.append(_arr1(k, "int", t[k]))
     L.append(_arr1("link_chain_mask", "unsigned", t["link_chain_mask"]))
+    L.append(_arr1("link_anc_mask", "unsigned", t["link_anc_mask"]))
     for k in ("link_offset_pos", "link_axis", "link_anchor", "link_com"):
         L.append(_arr2(k, "double", t[k], 3))
     L.append(_arr2("link_offset_quat", "double", t["link_offset_quat"], 4))

@@ -16,7 +16,12 @@ PBG_DEV f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
 PBG_DEV f3& operator+=(f3& a, f3 b) { a.x += b.x; a.y += b.y; a.z += b.z; return a; }
 PBG_DEV float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PBG_DEV f3 cross3(f3 a, f3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-PBG_DEV float norm3(f3 a) { return sqrtf(dot3(a, a)); }
+// Physics-side fast reciprocal / sqrt (v_rcp_f32 / v_sqrt_f32 / v_rsq_f32, ~1 ulp); the
+// numpy-exact pack keeps IEEE division and sqrt.
+PBG_DEV float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+PBG_DEV float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+PBG_DEV float norm3(f3 a) { return fast_sqrt(dot3(a, a)); }
 
 // row-major 3x3
 struct m3 {

@@ -29,20 +29,37 @@
 
 namespace pbg {
 
+// Scheduling fence between phases: keeps the scheduler from interleaving whole phases
+// (which stretches live ranges past the register file).
+#ifndef PBG_NO_PHASE_BARRIERS
+#define PBG_PHASE_BARRIER __builtin_amdgcn_sched_barrier(0);
+#else
+#define PBG_PHASE_BARRIER
+#endif
+
 // Diagnostic build only (-DPBG_STAMPS): per-phase wave-cycle sums (s_memtime), summed over
 // waves into g_stamps by lane 0.  Never compiled into the product library.
 #ifdef PBG_STAMPS
 __device__ unsigned long long g_stamps[16];
 #define STAMP_DECL unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_acc[16] = {0};
-#define STAMP(i) { unsigned long long _n = __builtin_amdgcn_s_memtime(); _st_acc[i] += _n - _st_t; _st_t = _n; }
+#define STAMP(i) { __builtin_amdgcn_sched_barrier(0); unsigned long long _n = __builtin_amdgcn_s_memtime(); _st_acc[i] += _n - _st_t; _st_t = _n; __builtin_amdgcn_sched_barrier(0); }
 #define STAMP_FLUSH if ((threadIdx.x & 63) == 0) { for (int _i = 0; _i < 16; _i++) atomicAdd(&g_stamps[_i], _st_acc[_i]); }
 #else
 #define STAMP_DECL
-#define STAMP(i)
+#define STAMP(i) PBG_PHASE_BARRIER
 #define STAMP_FLUSH
 #endif
 
 // ------------------------------------------------------------------ compile-time model facts
+template <int A, int B>
+struct BoolTab {
+  bool v[A][B];
+};
+template <int A, int B>
+struct IntTab {
+  int v[A][B];
+};
+
 template <class R>
 struct Dims {
   static constexpr int NL = R::NL, NJ = R::NJ, NB = R::NL + 1, NDOF = R::NDOF;
@@ -61,21 +78,80 @@ struct Dims {
   // generalized index -> joint dof (or -1 for a base dof)
   static constexpr int dof_of(int g) { return g < NJ ? NJ - 1 - g : -1; }
   // joint dof d moves link l
-  static constexpr bool moves(int d, int l) { return l >= 0 && ((R::link_chain_mask[l] >> d) & 1u); }
-  // generalized indices i, k coupled in M (one's link is an ancestor-or-self of the other's)
-  static constexpr bool coupled(int i, int k) {
+  static constexpr bool moves_(int d, int l) { return l >= 0 && ((R::link_chain_mask[l] >> d) & 1u); }
+  static constexpr bool coupled_(int i, int k) {
     int di = dof_of(i), dk = dof_of(k);
     if (di < 0 || dk < 0) return true;
-    return moves(di, R::dof_link[dk]) || moves(dk, R::dof_link[di]);
+    return moves_(di, R::dof_link[dk]) || moves_(dk, R::dof_link[di]);
   }
-  // generalized index g enters the Jacobian of a point on link l (-1 = base)
-  static constexpr bool in_chain(int g, int l) {
+  static constexpr bool in_chain_(int g, int l) {
     int d = dof_of(g);
     if (d < 0) return true;
-    return moves(d, l);
+    return moves_(d, l);
   }
+  static constexpr double body_mass(int b) { return b == 0 ? (R::floating ? R::base_mass : 0.0) : R::link_mass[b - 1]; }
+  static constexpr bool anc_or_self_(int a, int b) {
+    return a == b || a == 0 || (a > 0 && b > 0 && ((R::link_anc_mask[b - 1] >> (a - 1)) & 1u));
+  }
+  // ---- lookup tables, built at compile time (plain constant-array loads after unrolling;
+  // a constexpr *function* with loops is not reliably folded in device code)
+  static constexpr BoolTab<NDOF, NDOF> make_coupled() {
+    BoolTab<NDOF, NDOF> t{};
+    for (int i = 0; i < NDOF; i++)
+      for (int k = 0; k < NDOF; k++) t.v[i][k] = coupled_(i, k);
+    return t;
+  }
+  static constexpr BoolTab<NDOF, NB> make_in_chain() {
+    BoolTab<NDOF, NB> t{};
+    for (int i = 0; i < NDOF; i++)
+      for (int l = -1; l < NL; l++) t.v[i][l + 1] = in_chain_(i, l);
+    return t;
+  }
+  static constexpr BoolTab<NB, NB> make_anc() {
+    BoolTab<NB, NB> t{};
+    for (int a = 0; a < NB; a++)
+      for (int b = 0; b < NB; b++) t.v[a][b] = anc_or_self_(a, b);
+    return t;
+  }
+  static constexpr int count_nnz() {
+    int c = 0;
+    for (int i = 0; i < NDOF; i++)
+      for (int k = 0; k <= i; k++) c += coupled_(i, k);
+    return c;
+  }
+  static constexpr int NNZ = count_nnz();
+  static constexpr IntTab<NDOF, NDOF> make_lidx() {
+    IntTab<NDOF, NDOF> t{};
+    int c = 0;
+    for (int a = 0; a < NDOF; a++)
+      for (int b = 0; b < NDOF; b++) t.v[a][b] = NNZ;
+    for (int a = 0; a < NDOF; a++)
+      for (int b = 0; b <= a; b++)
+        if (coupled_(a, b)) t.v[a][b] = c++;
+    return t;
+  }
+  static constexpr BoolTab<NDOF, NDOF> COUPLED = make_coupled();
+  static constexpr BoolTab<NDOF, NB> IN_CHAIN = make_in_chain();
+  static constexpr BoolTab<NB, NB> ANC = make_anc();
+  static constexpr IntTab<NDOF, NDOF> LIDX = make_lidx();
+  // generalized indices i, k coupled in M (one's link is an ancestor-or-self of the other's)
+  static constexpr bool coupled(int i, int k) { return COUPLED.v[i][k]; }
+  // generalized index g enters the Jacobian of a point on link l (-1 = base)
+  static constexpr bool in_chain(int g, int l) { return IN_CHAIN.v[g][l + 1]; }
+  // body a is body b or an ancestor of it (0 = base)
+  static constexpr bool anc_or_self(int a, int b) { return ANC.v[a][b]; }
+  static constexpr int lidx(int i, int k) { return LIDX.v[i][k]; }
   // reference point body: base COM (floating) or the robot_body link COM (fixed base)
   static constexpr int REF_BODY = R::floating ? 0 : R::robot_body + 1;
+  // body b owns a composite: the floating base, or a link carrying a joint dof
+  static constexpr bool is_owner(int b) { return b == 0 ? R::floating : R::link_dof[b - 1] >= 0; }
+  // every body with mass comes after the reference body in DFS order (O is set first)
+  static constexpr bool ref_first() {
+    for (int b = 0; b < REF_BODY; b++)
+      if (body_mass(b) > 0.0) return false;
+    return true;
+  }
+  static_assert(ref_first(), "massive body before the reference body");
 };
 
 // ------------------------------------------------------------------ state record in registers
@@ -142,9 +218,9 @@ struct KinVel {
   f3 w[NB], v[NB], al[NB], ac[NB];
 };
 
-// Forward kinematics (positions only).
-template <class R>
-PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
+// Forward kinematics (positions; optionally the world axis / anchor of every joint dof).
+template <class R, bool AXES = false>
+PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, f3* ja = nullptr, f3* jo = nullptr) {
   k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
   k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
   k.c[0] = k.x[0];
@@ -163,9 +239,11 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
       const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, s.q[d]);
       k.Rm[l + 1] = mul(R0, Rj);
       k.x[l + 1] = x0 + mul(R0, anl - mul(Rj, anl));
+      if constexpr (AXES) { ja[d] = mul(R0, axl); jo[d] = x0 + mul(R0, anl); }
     } else if (jt == 1) {
       k.Rm[l + 1] = R0;
       k.x[l + 1] = x0 + mul(R0, s.q[d] * axl);
+      if constexpr (AXES) { ja[d] = mul(R0, axl); jo[d] = x0; }
     } else {
       k.Rm[l + 1] = R0;
       k.x[l + 1] = x0;
@@ -173,6 +251,20 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k) {
     k.c[l + 1] = k.x[l + 1] + mul(k.Rm[l + 1], mk3((float)R::link_com[l][0], (float)R::link_com[l][1],
                                                   (float)R::link_com[l][2]));
   }
+}
+
+// Opaque copy of the positional state: forces a recomputation instead of keeping values
+// of an earlier phase live across the solve (register pressure).
+template <class R>
+PBG_DEV State<R> opaque_positions(const State<R>& s) {
+  State<R> t = s;
+#pragma unroll
+  for (int i = 0; i < 3; i++) asm volatile("" : "+v"(t.bp[i]));
+#pragma unroll
+  for (int i = 0; i < 4; i++) asm volatile("" : "+v"(t.bq[i]));
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) asm volatile("" : "+v"(t.q[d]));
+  return t;
 }
 
 // ------------------------------------------------------------------ per-substep scratch
@@ -235,6 +327,25 @@ struct Rows {
 // ------------------------------------------------------------------ one physics sub-step
 // tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
 // of this sub-step's collision pass (feet contacts come from the last sub-step).
+// dof motion vectors (angular, linear-at-O) in generalized order
+template <class R>
+PBG_DEV void motion_vectors(const f3* ja, const f3* jo, f3 O, f3* sw, f3* sv) {
+  using D = Dims<R>;
+#pragma unroll
+  for (int gi = 0; gi < R::NDOF; gi++) {
+    const int d = D::dof_of(gi);
+    if (d >= 0) {
+      if (R::dof_jtype[d] == 0) { sw[gi] = ja[d]; sv[gi] = cross3(jo[d] - O, ja[d]); }
+      else { sw[gi] = mk3(0, 0, 0); sv[gi] = ja[d]; }
+    } else {
+      const int kk = gi - R::NJ;  // 0..2 linear, 3..5 angular
+      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
+      if (kk < 3) { sw[gi] = mk3(0, 0, 0); sv[gi] = e; }
+      else { sw[gi] = e; sv[gi] = mk3(0, 0, 0); }
+    }
+  }
+}
+
 #ifdef PBG_STAMPS
 #define SUB_STAMP_ARGS , unsigned long long& _st_t, unsigned long long* _st_acc
 #define SUB_STAMP_PASS , _st_t, _st_acc
@@ -247,132 +358,135 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
   constexpr float dt = (float)R::dt_sub;
+  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
   constexpr float g = (float)PBG_GRAVITY;
 
-  Kin<R> k;
-  fk_pos<R>(s, k);
-
-  // --- velocities, bias accelerations, joint axes (world) ------------------------------
-  f3 w[NB], v[NB], al[NB], ac[NB];
+  // --- phase A: one forward pass over the bodies: kinematics, velocities, bias
+  // accelerations, and each body's inertia + wrench about the reference point O added
+  // straight into the composites of its dof-owning ancestors.  No per-body array
+  // survives the pass (register pressure); positions are recomputed for contacts.
   f3 ja[NJ > 0 ? NJ : 1], jo[NJ > 0 ? NJ : 1];
-  w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
-  v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
-  al[0] = mk3(0, 0, 0);
-  ac[0] = mk3(0, 0, 0);
-#pragma unroll
-  for (int l = 0; l < R::NL; l++) {
-    const int p = R::link_parent[l] + 1;
-    const int jt = R::link_jtype[l], d = R::link_dof[l];
-    const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
-    const f3 c = k.c[l + 1];
-    if (jt == 0 || jt == 1) {
-      // R0 = Rm[p] * Ro ; axis/anchor fixed in the parent
-      const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
-                               (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
-      const m3 R0 = mul(k.Rm[p], Ro);
-      const f3 a = mul(R0, mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]));
-      const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
-                                              (float)R::link_offset_pos[l][2]));
-      ja[d] = a;
-      if (jt == 0) {
-        const f3 o = x0 + mul(R0, mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1],
-                                      (float)R::link_anchor[l][2]));
-        jo[d] = o;
-        const f3 ro = o - cp;
-        const f3 vo = vp + cross3(wp, ro);
-        const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
-        const f3 wl = wp + s.qd[d] * a;
-        const f3 all = alp + s.qd[d] * cross3(wp, a);
-        const f3 rc = c - o;
-        w[l + 1] = wl;
-        al[l + 1] = all;
-        v[l + 1] = vo + cross3(wl, rc);
-        ac[l + 1] = ao + cross3(all, rc) + cross3(wl, cross3(wl, rc));
-      } else {
-        jo[d] = x0;
-        const f3 r = c - cp;
-        w[l + 1] = wp;
-        al[l + 1] = alp;
-        v[l + 1] = vp + cross3(wp, r) + s.qd[d] * a;
-        ac[l + 1] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * s.qd[d]) * cross3(wp, a);
-      }
-    } else {
-      const f3 r = c - cp;
-      w[l + 1] = wp;
-      al[l + 1] = alp;
-      v[l + 1] = vp + cross3(wp, r);
-      ac[l + 1] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
-    }
-  }
-
-  STAMP(0)
-  // --- composite inertia + wrench per body about the reference point O -----------------
-  const f3 O = k.c[D::REF_BODY];
   float cm[NB];
   f3 cp1[NB], cF[NB], cN[NB];
   s6 cJ[NB];
 #pragma unroll
   for (int b = 0; b < NB; b++) {
-    const double mb = b == 0 ? R::base_mass : R::link_mass[b - 1];
-    const double* I6 = b == 0 ? R::base_inertia : R::link_inertia[b - 1];
-    if (b == 0 && !R::floating) {
-      cm[0] = 0.f; cp1[0] = mk3(0, 0, 0); cF[0] = mk3(0, 0, 0); cN[0] = mk3(0, 0, 0);
+    if (!D::is_owner(b)) continue;
+    cm[b] = 0.f; cp1[b] = mk3(0, 0, 0); cF[b] = mk3(0, 0, 0); cN[b] = mk3(0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < 6; i++) cJ[0].a[i] = 0.f;
-      continue;
-    }
-    const float m = (float)mb;
-    const s6 Iw = rotate_inertia(k.Rm[b], I6);
-    const f3 r = k.c[b] - O;
-    const float rr = dot3(r, r);
-    s6 J;
-    J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
-    J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
-    J.a[2] = Iw.a[2] + m * (rr - r.z * r.z);
-    J.a[3] = Iw.a[3] - m * r.x * r.y;
-    J.a[4] = Iw.a[4] - m * r.x * r.z;
-    J.a[5] = Iw.a[5] - m * r.y * r.z;
-    const f3 Iww = mul(Iw, w[b]);
-    const f3 f = m * (ac[b] - mk3(0, 0, -g)) +
-                 (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[b]))) * v[b];
-    const f3 n = mul(Iw, al[b]) + cross3(w[b], Iww) +
-                 ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
-    cm[b] = m;
-    cp1[b] = m * r;
-    cJ[b] = J;
-    cF[b] = f;
-    cN[b] = n + cross3(r, f);
+    for (int i = 0; i < 6; i++) cJ[b].a[i] = 0.f;
   }
+  f3 O = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  {
+    Kin<R> k;
+    f3 w[NB], v[NB], al[NB], ac[NB];
+    k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+    k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
+    k.c[0] = k.x[0];
+    w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
+    v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
+    al[0] = mk3(0, 0, 0);
+    ac[0] = mk3(0, 0, 0);
 #pragma unroll
-  for (int l = R::NL - 1; l >= 0; l--) {  // leaves to root: subtree sums
-    const int p = R::link_parent[l] + 1, b = l + 1;
-    cm[p] += cm[b];
-    cp1[p] += cp1[b];
-    cF[p] += cF[b];
-    cN[p] += cN[b];
+    for (int b = 0; b < NB; b++) {
+      if (b > 0) {
+        const int l = b - 1;
+        const int p = R::link_parent[l] + 1;
+        const int jt = R::link_jtype[l], d = R::link_dof[l];
+        const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
+                                 (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
+        const m3 R0 = mul(k.Rm[p], Ro);
+        const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
+                                                (float)R::link_offset_pos[l][2]));
+        const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
+        const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
+        if (jt == 0) {
+          const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, s.q[d]);
+          k.Rm[b] = mul(R0, Rj);
+          k.x[b] = x0 + mul(R0, anl - mul(Rj, anl));
+        } else if (jt == 1) {
+          k.Rm[b] = R0;
+          k.x[b] = x0 + mul(R0, s.q[d] * axl);
+        } else {
+          k.Rm[b] = R0;
+          k.x[b] = x0;
+        }
+        k.c[b] = k.x[b] + mul(k.Rm[b], mk3((float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]));
+        const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
+        const f3 c = k.c[b];
+        if (jt == 0 || jt == 1) {
+          const f3 a = mul(R0, axl);
+          ja[d] = a;
+          if (jt == 0) {
+            const f3 o = x0 + mul(R0, anl);
+            jo[d] = o;
+            const f3 ro = o - cp;
+            const f3 vo = vp + cross3(wp, ro);
+            const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+            const f3 wl = wp + s.qd[d] * a;
+            const f3 all = alp + s.qd[d] * cross3(wp, a);
+            const f3 rc = c - o;
+            w[b] = wl;
+            al[b] = all;
+            v[b] = vo + cross3(wl, rc);
+            ac[b] = ao + cross3(all, rc) + cross3(wl, cross3(wl, rc));
+          } else {
+            jo[d] = x0;
+            const f3 r = c - cp;
+            w[b] = wp;
+            al[b] = alp;
+            v[b] = vp + cross3(wp, r) + s.qd[d] * a;
+            ac[b] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * s.qd[d]) * cross3(wp, a);
+          }
+        } else {
+          const f3 r = c - cp;
+          w[b] = wp;
+          al[b] = alp;
+          v[b] = vp + cross3(wp, r);
+          ac[b] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
+        }
+      }
+      if (b == D::REF_BODY) O = k.c[b];
+      if (D::body_mass(b) > 0.0) {
+        const float m = (float)D::body_mass(b);
+        const s6 Iw = rotate_inertia(k.Rm[b], b == 0 ? R::base_inertia : R::link_inertia[b > 0 ? b - 1 : 0]);
+        const f3 r = k.c[b] - O;
+        const float rr = dot3(r, r);
+        s6 J;
+        J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
+        J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
+        J.a[2] = Iw.a[2] + m * (rr - r.z * r.z);
+        J.a[3] = Iw.a[3] - m * r.x * r.y;
+        J.a[4] = Iw.a[4] - m * r.x * r.z;
+        J.a[5] = Iw.a[5] - m * r.y * r.z;
+        const f3 Iww = mul(Iw, w[b]);
+        const f3 f = m * (ac[b] - mk3(0, 0, -g)) +
+                     (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[b]))) * v[b];
+        const f3 n = mul(Iw, al[b]) + cross3(w[b], Iww) +
+                     ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
+        const f3 pr = m * r, Nn = n + cross3(r, f);
 #pragma unroll
-    for (int i = 0; i < 6; i++) cJ[p].a[i] += cJ[b].a[i];
+        for (int a = 0; a < NB; a++) {
+          if (!D::is_owner(a) || !D::anc_or_self(a, b)) continue;
+          cm[a] += m;
+          cp1[a] += pr;
+          cF[a] += f;
+          cN[a] += Nn;
+#pragma unroll
+          for (int i = 0; i < 6; i++) cJ[a].a[i] += J.a[i];
+        }
+      }
+      PBG_PHASE_BARRIER
+    }
   }
 
-  // --- dof motion vectors about O --------------------------------------------------------
-  f3 sw[N], sv[N];
-#pragma unroll
-  for (int gi = 0; gi < N; gi++) {
-    const int d = D::dof_of(gi);
-    if (d >= 0) {
-      if (R::dof_jtype[d] == 0) { sw[gi] = ja[d]; sv[gi] = cross3(jo[d] - O, ja[d]); }
-      else { sw[gi] = mk3(0, 0, 0); sv[gi] = ja[d]; }
-    } else {
-      const int kk = gi - NJ;  // 0..2 linear, 3..5 angular
-      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
-      if (kk < 3) { sw[gi] = mk3(0, 0, 0); sv[gi] = e; }
-      else { sw[gi] = e; sv[gi] = mk3(0, 0, 0); }
-    }
-  }
-
+  STAMP(0)
   // --- mass matrix (lower triangle, gi >= gk) and bias -----------------------------------
-  float L[N][N];
+  float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
   float rhs[N];
+  {
+  f3 sw[N], sv[N];
+  motion_vectors<R>(ja, jo, O, sw, sv);
 #pragma unroll
   for (int gi = 0; gi < N; gi++) {
     // composite body owning dof gi (its link); base dofs use the whole-robot composite
@@ -382,41 +496,44 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     rhs[gi] = -(dot3(sw[gi], cN[bi]) + dot3(sv[gi], cF[bi]));
 #pragma unroll
     for (int gk = 0; gk <= gi; gk++) {
-      if (!D::coupled(gi, gk)) { L[gi][gk] = 0.f; continue; }
+      if (!D::coupled(gi, gk)) continue;
       // deeper dof of the pair owns the composite: joints come leaf-first, so the smaller
       // generalized index is the deeper (or equal) one; base dofs are the root.
       const int dk = D::dof_of(gk);
       const int bk = dk >= 0 ? R::dof_link[dk] + 1 : 0;
       const f3 Jw_ = mul(cJ[bk], sw[gk]) + cross3(cp1[bk], sv[gk]);
       const f3 Fv = cm[bk] * sv[gk] - cross3(cp1[bk], sw[gk]);
-      L[gi][gk] = dot3(sw[gi], Jw_) + dot3(sv[gi], Fv);
+      L[D::lidx(gi, gk)] = dot3(sw[gi], Jw_) + dot3(sv[gi], Fv);
     }
+  }
   }
 #pragma unroll
   for (int d = 0; d < NJ; d++) {
-    L[D::gj(d)][D::gj(d)] += (float)R::dof_armature[d];
+    L[D::lidx(D::gj(d), D::gj(d))] += (float)R::dof_armature[d];
     rhs[D::gj(d)] += tau[d] - (float)R::dof_damping[d] * s.qd[d];
   }
 
   STAMP(1)
-  // --- Cholesky (no fill-in in leaf-first order) ---------------------------------------
+  // --- Cholesky (no fill-in in leaf-first order); Ld = 1 / diag(L) ----------------------
+  float Ld[N];
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    float sjj = L[j][j];
+    float sjj = L[D::lidx(j, j)];
 #pragma unroll
     for (int kk = 0; kk < j; kk++)
-      if (D::coupled(j, kk)) sjj -= L[j][kk] * L[j][kk];
-    const float ljj = sqrtf(sjj);
-    const float inv = 1.0f / ljj;
-    L[j][j] = ljj;
+      if (D::coupled(j, kk)) sjj -= L[D::lidx(j, kk)] * L[D::lidx(j, kk)];
+    const float ljj = fast_sqrt(sjj);
+    const float inv = fast_rcp(ljj);
+    Ld[j] = inv;
+    L[D::lidx(j, j)] = ljj;
 #pragma unroll
     for (int i = j + 1; i < N; i++) {
       if (!D::coupled(i, j)) continue;
-      float t = L[i][j];
+      float t = L[D::lidx(i, j)];
 #pragma unroll
       for (int kk = 0; kk < j; kk++)
-        if (D::coupled(i, kk) && D::coupled(j, kk)) t -= L[i][kk] * L[j][kk];
-      L[i][j] = t * inv;
+        if (D::coupled(i, kk) && D::coupled(j, kk)) t -= L[D::lidx(i, kk)] * L[D::lidx(j, kk)];
+      L[D::lidx(i, j)] = t * inv;
     }
   }
 
@@ -434,8 +551,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     float t = rhs[i];
 #pragma unroll
     for (int kk = 0; kk < i; kk++)
-      if (D::coupled(i, kk)) t -= L[i][kk] * yv[kk];
-    yv[i] = t / L[i][i];
+      if (D::coupled(i, kk)) t -= L[D::lidx(i, kk)] * yv[kk];
+    yv[i] = t * Ld[i];
   }
   float qdd[N];
 #pragma unroll
@@ -443,8 +560,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     float t = yv[i];
 #pragma unroll
     for (int kk = i + 1; kk < N; kk++)
-      if (D::coupled(kk, i)) t -= L[kk][i] * qdd[kk];
-    qdd[i] = t / L[i][i];
+      if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * qdd[kk];
+    qdd[i] = t * Ld[i];
   }
   float u[N];  // u = L^T nu_pred
 #pragma unroll
@@ -457,7 +574,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     float t = 0.f;
 #pragma unroll
     for (int kk = i; kk < N; kk++)
-      if (D::coupled(kk, i)) t += L[kk][i] * nu[kk];
+      if (D::coupled(kk, i)) t += L[D::lidx(kk, i)] * nu[kk];
     u[i] = t;
   }
 
@@ -476,19 +593,19 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       float t = i == gd ? 1.f : 0.f;
 #pragma unroll
       for (int kk = gd; kk < i; kk++)
-        if (D::coupled(i, kk) && D::coupled(kk, gd)) t -= L[i][kk] * y[kk];
-      y[i] = t / L[i][i];
+        if (D::coupled(i, kk) && D::coupled(kk, gd)) t -= L[D::lidx(i, kk)] * y[kk];
+      y[i] = t * Ld[i];
     }
     float D2 = 0.f, vJ = 0.f;
 #pragma unroll
     for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
-    const float meff = D2 > 1e-12f ? 1.f / D2 : 0.f;
+    const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
 #pragma unroll
     for (int side = 0; side < 2; side++) {
       const float sg = side == 0 ? 1.f : -1.f;
       const float pos = side == 0 ? s.q[d] - (float)R::dof_lower[d] : (float)R::dof_upper[d] - s.q[d];
       const float vj = sg * vJ;
-      const float tgt = pos > 0.f ? vj - pos / dt : -(float)PBG_LIMIT_ERP * pos / dt;
+      const float tgt = pos > 0.f ? vj - pos * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * pos;
       float ys[N];
 #pragma unroll
       for (int i = 0; i < N; i++) ys[i] = sg * y[i];
@@ -499,6 +616,18 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   STAMP(3)
   const int first_normal = nr;
   int nc = 0;
+  // positions, joint axes and motion vectors again: recomputing them is cheaper than
+  // keeping phase A's copies live through the factorisation
+  Kin<R> k;
+  f3 sw[N], sv[N];
+  {
+    const State<R> sp = opaque_positions<R>(s);
+    f3 ja2[NJ > 0 ? NJ : 1], jo2[NJ > 0 ? NJ : 1];
+    fk_pos<R, true>(sp, k, ja2, jo2);
+    const f3 O2 = k.c[D::REF_BODY];
+    motion_vectors<R>(ja2, jo2, O2, sw, sv);
+    O = O2;
+  }
   // contact rows are staged: normals first (in contact order), frictions after.
   // Each contact stores its normal row now and its two friction rows at MAXROWS-space
   // offsets after all normals; friction rows are compacted once nc is known.
@@ -530,14 +659,14 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         float t = Jr[i];
 #pragma unroll
         for (int kk = 0; kk < i; kk++)
-          if (D::coupled(i, kk) && D::in_chain(kk, lnk)) t -= L[i][kk] * y[kk];
-        y[i] = t / L[i][i];
+          if (D::coupled(i, kk) && D::in_chain(kk, lnk)) t -= L[D::lidx(i, kk)] * y[kk];
+        y[i] = t * Ld[i];
       }
       float D2 = 0.f, vJ = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
-      rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? 1.f / D2 : 0.f,
-             dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f, 3.0e38f);
+      rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f, 3.0e38f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
@@ -579,15 +708,15 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       const float ra = (float)R::geom_r[ga], rb = (float)R::geom_r[gb];
       const float dist = dd - ra - rb;
       if (!(dist < (float)PBG_CONTACT_THRESHOLD)) continue;
-      const f3 nrm = dd > 1e-9f ? (1.f / dd) * dv : mk3(0, 0, 1);
+      const f3 nrm = dd > 1e-9f ? fast_rcp(dd) * dv : mk3(0, 0, 1);
       const f3 PA = ca - ra * nrm, PB = cb + rb * nrm;
       f3 t1, t2;  // btPlaneSpace1(nrm)
       if (fabsf(nrm.z) > 0.7071067811865476f) {
-        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = 1.f / sqrtf(a2);
+        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
         t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
         t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
       } else {
-        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = 1.f / sqrtf(a2);
+        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
         t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
         t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
       }
@@ -608,13 +737,13 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
           if (inB) t -= dot3(nd, sv[i]) + dot3(mB, sw[i]);
 #pragma unroll
           for (int kk = 0; kk < i; kk++)
-            if (D::coupled(i, kk)) t -= L[i][kk] * y[kk];
-          y[i] = t / L[i][i];
+            if (D::coupled(i, kk)) t -= L[D::lidx(i, kk)] * y[kk];
+          y[i] = t * Ld[i];
           D2 += y[i] * y[i];
           vJ += y[i] * u[i];
         }
-        rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? 1.f / D2 : 0.f,
-               dir == 0 ? (dist > 0.f ? vJ - dist / dt : -(float)PBG_CONTACT_ERP * dist / dt) : 0.f, 3.0e38f);
+        rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+               dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f, 3.0e38f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;
@@ -642,8 +771,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     float t = u[i];
 #pragma unroll
     for (int kk = i + 1; kk < N; kk++)
-      if (D::coupled(kk, i)) t -= L[kk][i] * nu[kk];
-    nu[i] = t / L[i][i];
+      if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * nu[kk];
+    nu[i] = t * Ld[i];
   }
 #pragma unroll
   for (int i = 0; i < N; i++) nu[i] = fminf(fmaxf(nu[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
@@ -672,7 +801,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
     const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
     const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-    const float inv = 1.f / sqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
+    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
     s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
   }
   STAMP(6)
