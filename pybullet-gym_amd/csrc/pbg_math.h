@@ -5,6 +5,19 @@
 
 #define PBG_DEV __device__ __forceinline__
 
+#include <utility>
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Guarantees a
+// constant induction variable where `#pragma unroll` may give up on big bodies.
+template <int B, class F, int... I>
+PBG_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, B + I>{}), ...);
+}
+template <int B, int E, class F>
+PBG_DEV void static_for(F&& f) {
+  if constexpr (E > B) static_for_impl<B>(f, std::make_integer_sequence<int, E - B>{});
+}
+
 struct f3 {
   float x, y, z;
 };

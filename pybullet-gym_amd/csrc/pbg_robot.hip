@@ -29,13 +29,13 @@ int PBG_FN(plan_)(int n_envs, int cus, Geometry* g) {
   const int wpc = (wgs + cus - 1) / cus;
   const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
   using RW = Rows<R, 64>;
-  long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC;
+  long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC - RW::LIMW;
   int cap = (int)(words / RW::W);
   if (cap > RW::MR) cap = RW::MR;
   if (cap < 0) cap = 0;
   g->block = b;
   g->lds_rows = cap;
-  g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)cap * RW::W + RW::NC);
+  g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
   g->scratch_words_per_env = RW::WORDS;
   hipError_t e = hipSuccess;
   if (b == 64) e = hipFuncSetAttribute((const void*)step_kernel<R, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);

@@ -71,7 +71,6 @@ struct Dims {
     return c;
   }
   static constexpr int NLIM = count_limited();
-  static constexpr int MAXROWS = 2 * NLIM + 3 * NC;
   // GPU generalized-velocity order: joint dofs leaf-first (reverse preorder), base last.
   static constexpr int gj(int d) { return NJ - 1 - d; }
   static constexpr int gb(int k) { return NJ + k; }
@@ -152,6 +151,42 @@ struct Dims {
     return true;
   }
   static_assert(ref_first(), "massive body before the reference body");
+  // ---- joint-limit rows: limited dofs in dof order, sparse pattern of y = L^-1 e_g
+  static constexpr IntTab<(NLIM > 0 ? NLIM : 1), NDOF + 3> make_lim() {
+    // row li: [0] dof, [1] pattern size, [2] LDS word offset, [3..] generalized indices
+    IntTab<(NLIM > 0 ? NLIM : 1), NDOF + 3> t{};
+    int li = 0, off = 0;
+    for (int d = 0; d < NJ; d++) {
+      if (!R::dof_limited[d]) continue;
+      const int g = gj(d);
+      int np = 0;
+      for (int i = g; i < NDOF; i++)
+        if (coupled_(i, g)) t.v[li][3 + np++] = i;
+      t.v[li][0] = d;
+      t.v[li][1] = np;
+      t.v[li][2] = off;
+      off += np + 5;  // y | meff | target_lo | target_hi | lambda_lo | lambda_hi
+      li++;
+    }
+    return t;
+  }
+  static constexpr IntTab<(NLIM > 0 ? NLIM : 1), NDOF + 3> LIM = make_lim();
+  static constexpr int limw() {
+    int w = 0;
+    for (int li = 0; li < NLIM; li++) w += LIM.v[li][1] + 5;
+    return w;
+  }
+  static constexpr int LIMW = limw();
+  // pattern membership / position by generalized index (fixed-trip loops unroll reliably)
+  static constexpr IntTab<(NLIM > 0 ? NLIM : 1), NDOF> make_limpos() {
+    IntTab<(NLIM > 0 ? NLIM : 1), NDOF> t{};
+    for (int li = 0; li < (NLIM > 0 ? NLIM : 1); li++)
+      for (int i = 0; i < NDOF; i++) t.v[li][i] = -1;
+    for (int li = 0; li < NLIM; li++)
+      for (int j = 0; j < LIM.v[li][1]; j++) t.v[li][LIM.v[li][3 + j]] = j;
+    return t;
+  }
+  static constexpr IntTab<(NLIM > 0 ? NLIM : 1), NDOF> LIMPOS = make_limpos();
 };
 
 // ------------------------------------------------------------------ state record in registers
@@ -268,59 +303,67 @@ PBG_DEV State<R> opaque_positions(const State<R>& s) {
 }
 
 // ------------------------------------------------------------------ per-substep scratch
-// Constraint rows: row r = [y (NDOF) | meff | target | lambda | hi].  Rows 0..cap-1 live
-// in LDS (dynamic shared memory, [word][lane]: conflict-free, ~100-cycle latency);
-// rows >= cap (rare: many simultaneous contacts) in a device workspace laid out
-// [word][env] so that each access is one coalesced wave access.  Row order:
-// limit rows [0, 2*NLIM), then contact c at 2*NLIM + 3c + {normal, t1, t2}.
+// Constraint rows, per lane in LDS (dynamic shared memory, [word][lane]: conflict-free):
+//   [joint-limit block | contact rows 0..cap-1 | mu per contact]
+// Joint-limit rows are compile-time: one block per limited dof holding the sparse
+// y = L^-1 e_g (only the dof and its ancestors + base are non-zero), m_eff and the
+// lower/upper targets and impulses -- the two rows of a joint share y and are solved
+// back to back.  Contact c owns rows 3c + {normal, t1, t2}, y dense; contact rows beyond
+// the LDS capacity (rare: many simultaneous contacts) go to a device workspace laid out
+// [word][env] (coalesced).
+typedef __attribute__((address_space(3))) float lds_float;  // explicit LDS pointers
+
 template <class R, int LS = 64>
 struct Rows {
-  static constexpr int N = R::NDOF, W = N + 4;
-  static constexpr int MR = Dims<R>::MAXROWS > 0 ? Dims<R>::MAXROWS : 1;
-  static constexpr int NC = Dims<R>::NC > 0 ? Dims<R>::NC : 1;
+  using D = Dims<R>;
+  static constexpr int N = R::NDOF, W = N + 3;  // contact row: y | meff | target | lambda
+  static constexpr int MR = 3 * D::NC > 0 ? 3 * D::NC : 1;
+  static constexpr int NC = D::NC > 0 ? D::NC : 1;
   static constexpr int WORDS = MR * W;  // global workspace words per env
   static constexpr int ls = LS;  // LDS stride = lanes per workgroup
-  float* lds;  // LDS base + lane
-  float* gbl;  // global workspace base + env
+  static constexpr int LIMW = D::LIMW;
+  lds_float* lds;  // LDS base + lane
+  float* gbl;      // global workspace base + env
   int n;       // global stride (envs)
-  int cap;     // rows resident in LDS
-  // per-contact friction coefficient, LDS words [cap*W, cap*W + NC)
-  PBG_DEV float& mu(int c) const { return lds[(size_t)(cap * W + c) * ls]; }
+  int cap;     // contact rows resident in LDS
+  PBG_DEV lds_float& lim(int w) const { return lds[(size_t)w * ls]; }
+  PBG_DEV lds_float& mu(int c) const { return lds[(size_t)(LIMW + cap * W + c) * ls]; }
   template <class P>
-  static PBG_DEV void put_at(P p, size_t st, const float* y, float meff, float target, float hi) {
+  static PBG_DEV void put_at(P p, size_t st, const float* y, float meff, float target) {
 #pragma unroll
     for (int i = 0; i < N; i++) p[i * st] = y[i];
     p[N * st] = meff;
     p[(N + 1) * st] = target;
     p[(N + 2) * st] = 0.f;
-    p[(N + 3) * st] = hi;
   }
   template <class P>
-  static PBG_DEV void solve_at(P p, size_t st, float* u, float lo, float hi_override) {
+  static PBG_DEV void solve_at(P p, size_t st, float* u, float lo, float hi) {
     float yv[N];
-    float yu = 0.f;
 #pragma unroll
-    for (int i = 0; i < N; i++) { yv[i] = p[i * st]; yu += yv[i] * u[i]; }
+    for (int i = 0; i < N; i++) yv[i] = p[i * st];
     const float meff = p[N * st], tgt = p[(N + 1) * st], lam0 = p[(N + 2) * st];
-    const float hi = hi_override >= 0.f ? hi_override : p[(N + 3) * st];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial sums: shorter dependency chain
+#pragma unroll
+    for (int i = 0; i < N; i++) acc[i & 3] += yv[i] * u[i];
+    const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     const float nl = fminf(fmaxf(lam0 + meff * (tgt - yu), lo), hi);
     const float dl = nl - lam0;
     p[(N + 2) * st] = nl;
 #pragma unroll
     for (int i = 0; i < N; i++) u[i] += yv[i] * dl;
   }
-  PBG_DEV void put(int r, const float* y, float meff, float target, float hi) const {
-    if (r < cap) put_at(lds + (size_t)r * W * ls, (size_t)ls, y, meff, target, hi);
-    else put_at(gbl + (size_t)r * W * n, (size_t)n, y, meff, target, hi);
+  PBG_DEV void put(int r, const float* y, float meff, float target) const {
+    if (r < cap) put_at(lds + (size_t)(LIMW + r * W) * ls, (size_t)ls, y, meff, target);
+    else put_at(gbl + (size_t)r * W * n, (size_t)n, y, meff, target);
   }
   PBG_DEV float lam(int r) const {
-    if (r < cap) return lds[((size_t)r * W + N + 2) * ls];
+    if (r < cap) return lds[(size_t)(LIMW + r * W + N + 2) * ls];
     return gbl[((size_t)r * W + N + 2) * n];
   }
-  // one projected Gauss-Seidel update of row r in u-space, bounds [lo, hi] (hi < 0: row's own)
-  PBG_DEV void solve(int r, float* u, float lo, float hi_override) const {
-    if (r < cap) solve_at(lds + (size_t)r * W * ls, (size_t)ls, u, lo, hi_override);
-    else solve_at(gbl + (size_t)r * W * n, (size_t)n, u, lo, hi_override);
+  // one projected Gauss-Seidel update of contact row r in u-space, bounds [lo, hi]
+  PBG_DEV void solve(int r, float* u, float lo, float hi) const {
+    if (r < cap) solve_at(lds + (size_t)(LIMW + r * W) * ls, (size_t)ls, u, lo, hi);
+    else solve_at(gbl + (size_t)r * W * n, (size_t)n, u, lo, hi);
   }
 };
 
@@ -580,12 +623,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 
   STAMP(2)
   // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
-  int nr = 0;
-#pragma unroll
-  for (int d = 0; d < NJ; d++) {
-    if (!R::dof_limited[d]) continue;
-    const int gd = D::gj(d);
-    // y = L^-1 e_gd
+  static_for<0, D::NLIM>([&](auto li_c) {
+    constexpr int li = decltype(li_c)::value;
+    constexpr int d = D::LIM.v[li][0], np = D::LIM.v[li][1], off = D::LIM.v[li][2];
+    constexpr int gd = D::gj(d);
+    // y = L^-1 e_gd, non-zero only on the pattern (the dof, its ancestors, the base)
     float y[N];
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -600,21 +642,21 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
     for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
+    // lower row J = +e_d (pos = q - lo), upper row J = -e_d (pos = hi - q)
+    const float plo = s.q[d] - (float)R::dof_lower[d], phi = (float)R::dof_upper[d] - s.q[d];
+    const float tlo = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
+    const float thi = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
 #pragma unroll
-    for (int side = 0; side < 2; side++) {
-      const float sg = side == 0 ? 1.f : -1.f;
-      const float pos = side == 0 ? s.q[d] - (float)R::dof_lower[d] : (float)R::dof_upper[d] - s.q[d];
-      const float vj = sg * vJ;
-      const float tgt = pos > 0.f ? vj - pos * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * pos;
-      float ys[N];
-#pragma unroll
-      for (int i = 0; i < N; i++) ys[i] = sg * y[i];
-      rw.put(nr, ys, meff, tgt, (float)PBG_LIMIT_MAX_IMPULSE);
-      nr++;
-    }
-  }
+    for (int i = 0; i < N; i++)
+      if (D::LIMPOS.v[li][i] >= 0) rw.lim(off + D::LIMPOS.v[li][i]) = y[i];
+    rw.lim(off + np) = meff;
+    rw.lim(off + np + 1) = tlo;
+    rw.lim(off + np + 2) = thi;
+    rw.lim(off + np + 3) = 0.f;
+    rw.lim(off + np + 4) = 0.f;
+  });
   STAMP(3)
-  const int first_normal = nr;
+  constexpr int first_normal = 0;
   int nc = 0;
   // positions, joint axes and motion vectors again: recomputing them is cheaper than
   // keeping phase A's copies live through the factorisation
@@ -631,16 +673,16 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   // contact rows are staged: normals first (in contact order), frictions after.
   // Each contact stores its normal row now and its two friction rows at MAXROWS-space
   // offsets after all normals; friction rows are compacted once nc is known.
-#pragma unroll
-  for (int sl = 0; sl < R::NS; sl++) {
-    const int b = R::slot_link[sl] + 1;
+  static_for<0, R::NS>([&](auto sl_c) {
+    constexpr int sl = decltype(sl_c)::value;
+    constexpr int b = R::slot_link[sl] + 1;
     const f3 cc = k.x[b] + mul(k.Rm[b], mk3((float)R::slot_point[sl][0], (float)R::slot_point[sl][1],
                                             (float)R::slot_point[sl][2]));
     const float rad = (float)R::slot_radius[sl];
     const float dist = cc.z - rad;
     const bool act = dist < (float)PBG_CONTACT_THRESHOLD;
     slot_active[sl] = act;
-    if (!act) continue;
+    if (!act) return;
     const f3 P = mk3(cc.x, cc.y, cc.z - rad);
     const f3 rP = P - O;
     const int lnk = R::slot_link[sl];
@@ -666,11 +708,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
       rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f, 3.0e38f);
+             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
-  }
+  });
   // self-collision pairs (capsule-capsule / sphere) -- Humanoid.  World endpoints per
   // geom are computed once (unrolled); the pair loop itself runs at run time.
   if constexpr (R::NPAIR > 0) {
@@ -743,7 +785,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
           vJ += y[i] * u[i];
         }
         rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-               dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f, 3.0e38f);
+               dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;
@@ -753,7 +795,35 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   STAMP(4)
   // --- PGS: 5 sweeps in u-space (gym_locomotion_envs -> scene_bases.py:65 numSolverIterations=5)
   for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
-    for (int r = 0; r < first_normal; r++) rw.solve(r, u, 0.f, -1.f);               // joint limits
+    // joint limits: lower then upper row of each limited dof, sharing y (compile-time)
+    static_for<0, D::NLIM>([&](auto li_c) {
+      constexpr int li = decltype(li_c)::value;
+      constexpr int np = D::LIM.v[li][1], off = D::LIM.v[li][2];
+      float yv[N];
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int j = D::LIMPOS.v[li][i];
+        if (j < 0) continue;
+        yv[i] = rw.lim(off + j);
+        acc[j & 3] += yv[i] * u[i];
+      }
+      const float meff = rw.lim(off + np), tlo = rw.lim(off + np + 1), thi = rw.lim(off + np + 2);
+      const float llo = rw.lim(off + np + 3), lhi = rw.lim(off + np + 4);
+      const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      const float nlo = fminf(fmaxf(llo + meff * (tlo - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+      const float dlo = nlo - llo;
+      // upper row sees u after the lower update: (-y).u' = -(yu + (y.y) dlo) = -(yu + dlo / meff)
+      const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
+      const float nhi = fminf(fmaxf(lhi + meff * (thi + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+      const float dhi = nhi - lhi;
+      rw.lim(off + np + 3) = nlo;
+      rw.lim(off + np + 4) = nhi;
+      const float dl = dlo - dhi;
+#pragma unroll
+      for (int i = 0; i < N; i++)
+        if (D::LIMPOS.v[li][i] >= 0) u[i] += yv[i] * dl;
+    });
     for (int c = 0; c < nc; c++) rw.solve(first_normal + 3 * c, u, 0.f, 3.0e38f);   // contact normals
     for (int c = 0; c < nc; c++) {                                                  // frictions
       const float ln = rw.lam(first_normal + 3 * c);
@@ -1128,7 +1198,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   }
   uint32_t slot_active[R::NS > 0 ? R::NS : 1];
   Rows<R, LS> rw;
-  rw.lds = lds_dyn + threadIdx.x;
+  rw.lds = (lds_float*)lds_dyn + threadIdx.x;
   rw.gbl = scratch + e;
   rw.n = B.n;
   rw.cap = lds_rows;
