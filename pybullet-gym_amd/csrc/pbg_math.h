@@ -36,6 +36,25 @@ PBG_DEV float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 PBG_DEV float norm3(f3 a) { return fast_sqrt(dot3(a, a)); }
 
+// sin/cos for the moderate arguments of the physics (joint angles, exp-map half angles):
+// 3-part Cody-Waite reduction by pi/2 + minimax polynomials on [-pi/4, pi/4], a few ulp
+// for |x| < 1e5.  Branch-free and short: the library sincosf carries a Payne-Hanek
+// large-argument path that, executed as selects, costs ~50 instructions per call.
+PBG_DEV void sincos_fast(float x, float* sp, float* cp) {
+  const float k = __builtin_rintf(x * 0.636619772367581343f);
+  float r = __builtin_fmaf(-k, 1.5703125f, x);
+  r = __builtin_fmaf(-k, 4.837512969970703125e-4f, r);
+  r = __builtin_fmaf(-k, 7.54978995489188216e-8f, r);
+  const float r2 = r * r;
+  const float sr = __builtin_fmaf(r * r2, __builtin_fmaf(r2, __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float cr = __builtin_fmaf(r2 * r2, __builtin_fmaf(r2, __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                                  __builtin_fmaf(-0.5f, r2, 1.0f));
+  const int q = (int)k;
+  const float s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+  *sp = (q & 2) ? -s0 : s0;
+  *cp = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // row-major 3x3
 struct m3 {
   float m[9];
@@ -63,12 +82,52 @@ PBG_DEV m3 quat_to_m3(float x, float y, float z, float w) {
 // rotation by angle about a unit axis given by compile-time constants
 PBG_DEV m3 axis_angle_m3(float ax, float ay, float az, float ang) {
   float s, c;
-  sincosf(ang, &s, &c);
+  sincos_fast(ang, &s, &c);
   float t = 1 - c;
   m3 R;
   R.m[0] = t * ax * ax + c;      R.m[1] = t * ax * ay - s * az; R.m[2] = t * ax * az + s * ay;
   R.m[3] = t * ax * ay + s * az; R.m[4] = t * ay * ay + c;      R.m[5] = t * ay * az - s * ax;
   R.m[6] = t * ax * az - s * ay; R.m[7] = t * ay * az + s * ax; R.m[8] = t * az * az + c;
+  return R;
+}
+
+// ---- products with compile-time model constants.  After inlining/unrolling the
+// constant c is known, so a 0 / +-1 factor costs nothing: kmul returns -0 for c == 0 and
+// x + (-0) == x exactly, so whole terms fold away (no fast-math needed).
+PBG_DEV float kmul(float c, float x) { return c == 0.f ? -0.f : (c == 1.f ? x : (c == -1.f ? -x : c * x)); }
+// A * c for a constant vector c
+PBG_DEV f3 mulc(const m3& A, float cx, float cy, float cz) {
+  return mk3(kmul(cx, A.m[0]) + kmul(cy, A.m[1]) + kmul(cz, A.m[2]), kmul(cx, A.m[3]) + kmul(cy, A.m[4]) + kmul(cz, A.m[5]),
+             kmul(cx, A.m[6]) + kmul(cy, A.m[7]) + kmul(cz, A.m[8]));
+}
+PBG_DEV f3 mulc(const m3& A, f3 c) { return mulc(A, c.x, c.y, c.z); }
+// A * C for a constant matrix C (row-major)
+PBG_DEV m3 mulc(const m3& A, const m3& C) {
+  m3 O;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      O.m[3 * i + j] = kmul(C.m[j], A.m[3 * i]) + kmul(C.m[3 + j], A.m[3 * i + 1]) + kmul(C.m[6 + j], A.m[3 * i + 2]);
+  return O;
+}
+// constant quaternion (x,y,z,w) -> matrix, folded at compile time
+PBG_DEV m3 quat_to_m3c(double x, double y, double z, double w) {
+  m3 R;
+  R.m[0] = (float)(1 - 2 * (y * y + z * z)); R.m[1] = (float)(2 * (x * y - w * z)); R.m[2] = (float)(2 * (x * z + w * y));
+  R.m[3] = (float)(2 * (x * y + w * z)); R.m[4] = (float)(1 - 2 * (x * x + z * z)); R.m[5] = (float)(2 * (y * z - w * x));
+  R.m[6] = (float)(2 * (x * z - w * y)); R.m[7] = (float)(2 * (y * z + w * x)); R.m[8] = (float)(1 - 2 * (x * x + y * y));
+  return R;
+}
+// rotation about a constant unit axis
+PBG_DEV m3 axis_angle_m3c(float ax, float ay, float az, float ang) {
+  float s, c;
+  sincos_fast(ang, &s, &c);
+  const float t = 1 - c;
+  m3 R;
+  R.m[0] = kmul(ax * ax, t) + c;       R.m[1] = kmul(ax * ay, t) - kmul(az, s); R.m[2] = kmul(ax * az, t) + kmul(ay, s);
+  R.m[3] = kmul(ax * ay, t) + kmul(az, s); R.m[4] = kmul(ay * ay, t) + c;       R.m[5] = kmul(ay * az, t) - kmul(ax, s);
+  R.m[6] = kmul(ax * az, t) - kmul(ay, s); R.m[7] = kmul(ay * az, t) + kmul(ax, s); R.m[8] = kmul(az * az, t) + c;
   return R;
 }
 
@@ -89,7 +148,7 @@ PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++)
-      RI[3 * i + j] = R.m[3 * i] * I[j] + R.m[3 * i + 1] * I[3 + j] + R.m[3 * i + 2] * I[6 + j];
+      RI[3 * i + j] = kmul(I[j], R.m[3 * i]) + kmul(I[3 + j], R.m[3 * i + 1]) + kmul(I[6 + j], R.m[3 * i + 2]);
   s6 W;
   W.a[0] = RI[0] * R.m[0] + RI[1] * R.m[1] + RI[2] * R.m[2];
   W.a[1] = RI[3] * R.m[3] + RI[4] * R.m[4] + RI[5] * R.m[5];

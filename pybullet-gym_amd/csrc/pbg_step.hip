@@ -143,6 +143,15 @@ struct Dims {
   // reference point body: base COM (floating) or the robot_body link COM (fixed base)
   static constexpr int REF_BODY = R::floating ? 0 : R::robot_body + 1;
   // body b owns a composite: the floating base, or a link carrying a joint dof
+  // body-frame inertia (xx, yy, zz, xy, xz, yz) of body b by value: a pointer into the
+  // model table is loaded at run time
+  struct Inertia6 { double v[6]; };
+  template <int b>
+  static constexpr Inertia6 inertia() {
+    Inertia6 I{};
+    for (int i = 0; i < 6; i++) I.v[i] = b == 0 ? R::base_inertia[i] : R::link_inertia[b > 0 ? b - 1 : 0][i];
+    return I;
+  }
   static constexpr bool is_owner(int b) { return b == 0 ? R::floating : R::link_dof[b - 1] >= 0; }
   // every body with mass comes after the reference body in DFS order (O is set first)
   static constexpr bool ref_first() {
@@ -259,33 +268,30 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, f3* ja = nullptr, f3* jo = nul
   k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
   k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
   k.c[0] = k.x[0];
-#pragma unroll
-  for (int l = 0; l < R::NL; l++) {
+  static_for<0, R::NL>([&](auto l_c) {
+    constexpr int l = decltype(l_c)::value;
     const int p = R::link_parent[l] + 1;
-    const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
-                             (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
-    const m3 R0 = mul(k.Rm[p], Ro);
-    const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
-                                            (float)R::link_offset_pos[l][2]));
+    const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+    const m3 R0 = mulc(k.Rm[p], Ro);
+    const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
     const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
     const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
     const int jt = R::link_jtype[l], d = R::link_dof[l];
     if (jt == 0) {
-      const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, s.q[d]);
+      const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
       k.Rm[l + 1] = mul(R0, Rj);
-      k.x[l + 1] = x0 + mul(R0, anl - mul(Rj, anl));
-      if constexpr (AXES) { ja[d] = mul(R0, axl); jo[d] = x0 + mul(R0, anl); }
+      k.x[l + 1] = x0 + mul(R0, anl - mulc(Rj, anl));
+      if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0 + mulc(R0, anl); }
     } else if (jt == 1) {
       k.Rm[l + 1] = R0;
-      k.x[l + 1] = x0 + mul(R0, s.q[d] * axl);
-      if constexpr (AXES) { ja[d] = mul(R0, axl); jo[d] = x0; }
+      k.x[l + 1] = x0 + s.q[d] * mulc(R0, axl);
+      if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0; }
     } else {
       k.Rm[l + 1] = R0;
       k.x[l + 1] = x0;
     }
-    k.c[l + 1] = k.x[l + 1] + mul(k.Rm[l + 1], mk3((float)R::link_com[l][0], (float)R::link_com[l][1],
-                                                  (float)R::link_com[l][2]));
-  }
+    k.c[l + 1] = k.x[l + 1] + mulc(k.Rm[l + 1], (float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]);
+  });
 }
 
 // Opaque copy of the positional state: forces a recomputation instead of keeping values
@@ -412,13 +418,14 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   float cm[NB];
   f3 cp1[NB], cF[NB], cN[NB];
   s6 cJ[NB];
+  static_for<0, NB>([&](auto b_c) {
+    constexpr int b = decltype(b_c)::value;
+    if constexpr (D::is_owner(b)) {
+      cm[b] = 0.f; cp1[b] = mk3(0, 0, 0); cF[b] = mk3(0, 0, 0); cN[b] = mk3(0, 0, 0);
 #pragma unroll
-  for (int b = 0; b < NB; b++) {
-    if (!D::is_owner(b)) continue;
-    cm[b] = 0.f; cp1[b] = mk3(0, 0, 0); cF[b] = mk3(0, 0, 0); cN[b] = mk3(0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 6; i++) cJ[b].a[i] = 0.f;
-  }
+      for (int i = 0; i < 6; i++) cJ[b].a[i] = 0.f;
+    }
+  });
   f3 O = mk3(s.bp[0], s.bp[1], s.bp[2]);
   {
     Kin<R> k;
@@ -430,38 +437,36 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
     al[0] = mk3(0, 0, 0);
     ac[0] = mk3(0, 0, 0);
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
+    static_for<0, NB>([&](auto b_c) {
+      constexpr int b = decltype(b_c)::value;
       if (b > 0) {
         const int l = b - 1;
         const int p = R::link_parent[l] + 1;
         const int jt = R::link_jtype[l], d = R::link_dof[l];
-        const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
-                                 (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
-        const m3 R0 = mul(k.Rm[p], Ro);
-        const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
-                                                (float)R::link_offset_pos[l][2]));
+        const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+        const m3 R0 = mulc(k.Rm[p], Ro);
+        const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
         const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
         const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
         if (jt == 0) {
-          const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, s.q[d]);
+          const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
           k.Rm[b] = mul(R0, Rj);
-          k.x[b] = x0 + mul(R0, anl - mul(Rj, anl));
+          k.x[b] = x0 + mul(R0, anl - mulc(Rj, anl));
         } else if (jt == 1) {
           k.Rm[b] = R0;
-          k.x[b] = x0 + mul(R0, s.q[d] * axl);
+          k.x[b] = x0 + s.q[d] * mulc(R0, axl);
         } else {
           k.Rm[b] = R0;
           k.x[b] = x0;
         }
-        k.c[b] = k.x[b] + mul(k.Rm[b], mk3((float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]));
+        k.c[b] = k.x[b] + mulc(k.Rm[b], (float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]);
         const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
         const f3 c = k.c[b];
         if (jt == 0 || jt == 1) {
-          const f3 a = mul(R0, axl);
+          const f3 a = mulc(R0, axl);
           ja[d] = a;
           if (jt == 0) {
-            const f3 o = x0 + mul(R0, anl);
+            const f3 o = x0 + mulc(R0, anl);
             jo[d] = o;
             const f3 ro = o - cp;
             const f3 vo = vp + cross3(wp, ro);
@@ -490,9 +495,10 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         }
       }
       if (b == D::REF_BODY) O = k.c[b];
-      if (D::body_mass(b) > 0.0) {
+      if constexpr (D::body_mass(b) > 0.0) {
         const float m = (float)D::body_mass(b);
-        const s6 Iw = rotate_inertia(k.Rm[b], b == 0 ? R::base_inertia : R::link_inertia[b > 0 ? b - 1 : 0]);
+        constexpr typename D::Inertia6 I6 = D::template inertia<b>();
+        const s6 Iw = rotate_inertia(k.Rm[b], I6.v);
         const f3 r = k.c[b] - O;
         const float rr = dot3(r, r);
         s6 J;
@@ -508,19 +514,20 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         const f3 n = mul(Iw, al[b]) + cross3(w[b], Iww) +
                      ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
         const f3 pr = m * r, Nn = n + cross3(r, f);
+        static_for<0, NB>([&](auto a_c) {
+          constexpr int a = decltype(a_c)::value;
+          if constexpr (D::is_owner(a) && D::anc_or_self(a, b)) {
+            cm[a] += m;
+            cp1[a] += pr;
+            cF[a] += f;
+            cN[a] += Nn;
 #pragma unroll
-        for (int a = 0; a < NB; a++) {
-          if (!D::is_owner(a) || !D::anc_or_self(a, b)) continue;
-          cm[a] += m;
-          cp1[a] += pr;
-          cF[a] += f;
-          cN[a] += Nn;
-#pragma unroll
-          for (int i = 0; i < 6; i++) cJ[a].a[i] += J.a[i];
-        }
+            for (int i = 0; i < 6; i++) cJ[a].a[i] += J.a[i];
+          }
+        });
       }
       PBG_PHASE_BARRIER
-    }
+    });
   }
 
   STAMP(0)
@@ -676,8 +683,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   static_for<0, R::NS>([&](auto sl_c) {
     constexpr int sl = decltype(sl_c)::value;
     constexpr int b = R::slot_link[sl] + 1;
-    const f3 cc = k.x[b] + mul(k.Rm[b], mk3((float)R::slot_point[sl][0], (float)R::slot_point[sl][1],
-                                            (float)R::slot_point[sl][2]));
+    const f3 cc = k.x[b] + mulc(k.Rm[b], (float)R::slot_point[sl][0], (float)R::slot_point[sl][1], (float)R::slot_point[sl][2]);
     const float rad = (float)R::slot_radius[sl];
     const float dist = cc.z - rad;
     const bool act = dist < (float)PBG_CONTACT_THRESHOLD;
@@ -720,8 +726,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
     for (int gg = 0; gg < R::NG; gg++) {
       const int b = R::geom_link[gg] + 1;
-      G0[gg] = k.x[b] + mul(k.Rm[b], mk3((float)R::geom_p0[gg][0], (float)R::geom_p0[gg][1], (float)R::geom_p0[gg][2]));
-      G1[gg] = k.x[b] + mul(k.Rm[b], mk3((float)R::geom_p1[gg][0], (float)R::geom_p1[gg][1], (float)R::geom_p1[gg][2]));
+      G0[gg] = k.x[b] + mulc(k.Rm[b], (float)R::geom_p0[gg][0], (float)R::geom_p0[gg][1], (float)R::geom_p0[gg][2]);
+      G1[gg] = k.x[b] + mulc(k.Rm[b], (float)R::geom_p1[gg][0], (float)R::geom_p1[gg][1], (float)R::geom_p1[gg][2]);
     }
 #pragma unroll 1
     for (int pp = 0; pp < R::NPAIR; pp++) {
@@ -862,10 +868,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
     float ang = norm3(wv);
     if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    float sh, dw;
+    sincos_fast(0.5f * ang * dt, &sh, &dw);
     f3 ax;
     if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
-    else ax = (sinf(0.5f * ang * dt) / ang) * wv;
-    const float dw = cosf(0.5f * ang * dt);
+    else ax = (sh / ang) * wv;
     const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
     const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
     const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
@@ -1084,15 +1091,12 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
       const int p = R::link_parent[l] + 1, jt = R::link_jtype[l], d = R::link_dof[l];
       const f3 cp = k.c[p], c = k.c[l + 1];
       if (jt == 0 || jt == 1) {
-        const m3 Ro = quat_to_m3((float)R::link_offset_quat[l][0], (float)R::link_offset_quat[l][1],
-                                 (float)R::link_offset_quat[l][2], (float)R::link_offset_quat[l][3]);
-        const m3 R0 = mul(k.Rm[p], Ro);
-        const f3 a = mul(R0, mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]));
-        const f3 x0 = k.x[p] + mul(k.Rm[p], mk3((float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1],
-                                                (float)R::link_offset_pos[l][2]));
+        const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+        const m3 R0 = mulc(k.Rm[p], Ro);
+        const f3 a = mulc(R0, (float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
+        const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
         if (jt == 0) {
-          const f3 o = x0 + mul(R0, mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1],
-                                        (float)R::link_anchor[l][2]));
+          const f3 o = x0 + mulc(R0, (float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
           const f3 vo = v[p] + cross3(w[p], o - cp);
           w[l + 1] = w[p] + s.qd[d] * a;
           v[l + 1] = vo + cross3(w[l + 1], c - o);
