@@ -21,12 +21,20 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+METRIC = "env steps/sec (whole node) at N parallel envs, Ant + Humanoid, 1/2/4/8 MI355X"  # BASELINE.json
 ENV_ID = "AntPyBulletEnv-v0"
 ENVS_PER_GPU = 16384
-# Algorithmic HBM bytes per env-step: 4 * (2S + n + D + 2),
-# S = 35 state words, n = 8 actions, D = 28 obs, 2 = reward + done  ->  432 B.
-ALG_BYTES_PER_ENV_STEP = 4 * (2 * 35 + 8 + 28 + 2)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SHORT = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
+         "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
+         "HumanoidPyBulletEnv-v0": "humanoid"}
+
+
+def alg_bytes_per_env_step(info):
+    """Minimum HBM bytes per env-step (BASELINE.md section 4 / SURVEY.md 8d): 4 * (2S + n + D + 2),
+    S = 13 (floating base) + 2 * joint dofs + 6 per-env scalars; Ant: S = 35 -> 432 B."""
+    S = 13 * int(info.floating) + 2 * info.n_joints + 6
+    return 4 * (2 * S + info.action_dim + info.obs_dim + 2)
 
 
 def cpu_baseline(seconds=12.0):
@@ -53,16 +61,18 @@ def cpu_baseline(seconds=12.0):
                       f"{threads} OpenMP threads, {dt:.1f} s; no auto-reset"}
 
 
-def load_traffic():
-    """HBM bytes per launch of the step kernel from the latest committed PMC summary."""
-    path = os.path.join(REPO, "profiles", "pmc_step_ant.json")
-    if not os.path.exists(path):
-        return None
+def load_pmc(env_id, n):
+    """PMC summary of the step kernel (profiles/pmc_step_<robot>.json, written by
+    tools/pmc_summary.py from the committed rocprofv3 --pmc passes), if it was taken at
+    this env count."""
+    path = os.path.join(REPO, "profiles", f"pmc_step_{SHORT.get(env_id, env_id)}.json")
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except Exception:
+            d = json.load(f)
+    except (OSError, ValueError):
         return None
+    d["_path"] = path
+    return d if d.get("envs") == n else None
 
 
 def main():
@@ -139,10 +149,12 @@ def main():
     if rank == 0:
         steps_total = world * n * args.steps
         value = steps_total / elapsed
-        achieved = ALG_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
-        traffic = load_traffic()
+        alg = alg_bytes_per_env_step(env.info)
+        achieved = alg * n / (kernel_ms * 1e-3) / 1e9
+        pmc = load_pmc(args.env, n)
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
         out = {
-            "metric": "env steps/sec (whole node) at N parallel envs, AntPyBulletEnv-v0 random-action rollout",
+            "metric": METRIC,
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -153,16 +165,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: U(-1,1) float32 actions pre-generated in HBM; MJCF-compiled Ant model",
+            "data": "synthetic: U(-1,1) float32 actions pre-generated in HBM; robot compiled from the reference MJCF",
             "config": {"workload": f"{args.env} random-action rollout, auto-reset (TimeLimit 1000)",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps": env.info.substeps,
                        "solver_iterations": 5, "parallelism": f"env-sharded x{world}, no per-step collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"pbg::step_kernel<{args.env}>", "kernel_ms": kernel_ms,
-                         "alg_bytes_per_env_step": ALG_BYTES_PER_ENV_STEP},
+                         "alg_bytes_per_env_step": alg},
             "obs_finite": finite,
         }
+        if pmc and pmc.get("valu_insts_per_launch"):
+            # VALU issue roofline (the binding one): wave64 VALU instructions per
+            # launch (PMC SQ_INSTS_VALU) / the kernel's HIP-event time, against the chip's
+            # issue peak: 256 CUs x 4 SIMDs x one wave64 VALU op per 2 cycles at 2.4 GHz.
+            peak = 256 * 4 * 2.4e9 / 2 / 1e12
+            ach = pmc["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e12
+            out["valu_roofline"] = {"achieved": ach, "peak": peak, "unit": "T wave-instr/s", "frac": ach / peak,
+                                    "valu_instr_per_env": pmc["valu_insts_per_launch"] * 64 / n,
+                                    "source": "profiles/" + os.path.basename(pmc.get("_path", "pmc"))}
         if gather_ms is not None:
             out["allgather_obs_ms"] = gather_ms
         if world == 1 and not args.no_cpu_baseline:

@@ -1,14 +1,19 @@
 #!/bin/bash
-# bench + rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE, WRITE_SIZE).
+# bench + rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE; WRITE_SIZE; SQ
+# instruction/cycle counters).  usage: tools/gpu_bench_prof.sh TAG [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
+shift || true
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
+timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
+B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- $B > $OUT/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- $B > $OUT/pmc_write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sq -o run -- $B > $OUT/pmc_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 --output-format csv -d $OUT/pmc_flops -o run -- $B > $OUT/pmc_flops.log 2>&1
 echo done

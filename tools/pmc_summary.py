@@ -1,0 +1,66 @@
+"""Summarise the rocprofv3 passes of tools/gpu_bench_prof.sh into profiles/ (dev tool).
+
+usage: python tools/pmc_summary.py gpurun_out/TAG ROUND ROBOT ENVS
+writes profiles/ROUND_{kernel_stats,pmc_*}_<robot><envs/1024>k.csv copies and
+profiles/pmc_step_<robot>.json (per-launch medians of the step kernel), which bench.py
+reads for roofline.traffic and valu_roofline.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+src, rnd, robot, envs = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(REPO, "profiles")
+tag = f"{robot}{envs // 1024}k"
+
+
+def counter_csv(d):
+    f = glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True)
+    return f[0] if f else None
+
+
+def medians(path):
+    per = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "step_kernel" not in r["Kernel_Name"]:
+                continue
+            per.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
+            per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: statistics.median(v.values()) for k, v in per.items()}
+
+
+out = {"kernel": "pbg::step_kernel", "robot": robot, "envs": envs, "round": rnd}
+for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops"):
+    p = counter_csv(d)
+    if not p:
+        continue
+    shutil.copy(p, os.path.join(prof, f"{rnd}_{d}_{tag}.csv"))
+    out.update({k + "_median": v for k, v in medians(p).items()})
+st = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+if st:
+    shutil.copy(st[0], os.path.join(prof, f"{rnd}_kernel_stats_{tag}.csv"))
+    with open(st[0]) as f:
+        for r in csv.DictReader(f):
+            if "step_kernel" in r["Name"]:
+                out["trace_avg_ns"] = float(r["AverageNs"])
+                out["trace_calls"] = int(r["Calls"])
+if "FETCH_SIZE_median" in out and "WRITE_SIZE_median" in out:
+    out["hbm_bytes_per_launch"] = (2 * out["FETCH_SIZE_median"] + out["WRITE_SIZE_median"]) * 1024
+    out["correction"] = "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); kB = 1024 B"
+if "SQ_INSTS_VALU_median" in out:
+    out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_median"]
+if "SQ_INSTS_VALU_FMA_F32_median" in out:
+    out["fp32_flops_per_launch_from_insts"] = 64 * (
+        2 * out["SQ_INSTS_VALU_FMA_F32_median"] + out.get("SQ_INSTS_VALU_ADD_F32_median", 0)
+        + out.get("SQ_INSTS_VALU_MUL_F32_median", 0) + out.get("SQ_INSTS_VALU_TRANS_F32_median", 0))
+out["source"] = ("rocprofv3 --kernel-trace --stats; separate --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_* | "
+                 "SQ_INSTS_VALU_* (tools/gpu_bench_prof.sh), python bench.py --steps 20 --warmup 2")
+with open(os.path.join(prof, f"pmc_step_{robot}.json"), "w") as f:
+    json.dump(out, f, indent=1)
+print(json.dumps(out, indent=1))
