@@ -2,6 +2,7 @@
 // dispatches to the per-robot launchers of pbg_robot.hip (one translation unit each).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -35,7 +36,7 @@ int env_robot_id(const char* env_id) {
 }
 
 struct Ops {
-  int (*plan)(int, int, pbg::Geometry*);
+  int (*plan)(int, int, int, pbg::Geometry*);
   int (*step)(const pbg::Buffers&, const pbg::StepIO&, float*, const pbg::Geometry&, hipStream_t);
   int (*reset)(const pbg::Buffers&, const pbg::ResetIO&, hipStream_t);
   int (*get_state)(const pbg::Buffers&, double*, double*, hipStream_t);
@@ -124,7 +125,13 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
   const size_t n = (size_t)n_envs;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  int e = hip_check(o->plan(n_envs, cus, &h->geo), "kernel attributes");
+  // PBG_TEAM=0 selects the one-lane-per-env kernel for robots that have a quad variant
+  const char* team_env = getenv("PBG_TEAM");
+  const int allow_team = !(team_env && team_env[0] == '0');
+  int e = hip_check(o->plan(n_envs, cus, allow_team, &h->geo), "kernel attributes");
+  // PBG_LDS_ROWS=k caps the LDS-resident contact rows (tests of the workspace path)
+  const char* rows_env = getenv("PBG_LDS_ROWS");
+  if (rows_env && atoi(rows_env) >= 0 && atoi(rows_env) < h->geo.lds_rows) h->geo.lds_rows = atoi(rows_env);
   e |= hip_check(hipMalloc(&B.st, sizeof(float) * n * h->info.state_words), "hipMalloc state");
   e |= hip_check(hipMalloc(&B.pot, sizeof(double) * n), "hipMalloc potential");
   e |= hip_check(hipMalloc(&B.z0, sizeof(float) * n), "hipMalloc z0");

@@ -94,7 +94,12 @@ PBG_DEV m3 axis_angle_m3(float ax, float ay, float az, float ang) {
 // ---- products with compile-time model constants.  After inlining/unrolling the
 // constant c is known, so a 0 / +-1 factor costs nothing: kmul returns -0 for c == 0 and
 // x + (-0) == x exactly, so whole terms fold away (no fast-math needed).
-PBG_DEV float kmul(float c, float x) { return c == 0.f ? -0.f : (c == 1.f ? x : (c == -1.f ? -x : c * x)); }
+// Only a compile-time c is inspected (__builtin_constant_p resolves after inlining); a
+// run-time c is a plain product (no selects).
+PBG_DEV float kmul(float c, float x) {
+  if (__builtin_constant_p(c)) return c == 0.f ? -0.f : (c == 1.f ? x : (c == -1.f ? -x : c * x));
+  return c * x;
+}
 // A * c for a constant vector c
 PBG_DEV f3 mulc(const m3& A, float cx, float cy, float cz) {
   return mk3(kmul(cx, A.m[0]) + kmul(cy, A.m[1]) + kmul(cz, A.m[2]), kmul(cx, A.m[3]) + kmul(cy, A.m[4]) + kmul(cz, A.m[5]),
@@ -139,10 +144,9 @@ PBG_DEV f3 mul(const s6& S, f3 v) {
   return mk3(S.a[0] * v.x + S.a[3] * v.y + S.a[4] * v.z, S.a[3] * v.x + S.a[1] * v.y + S.a[5] * v.z,
              S.a[4] * v.x + S.a[5] * v.y + S.a[2] * v.z);
 }
-// R I R^T for body-frame inertia I6 (double constants)
-PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
-  float I[9] = {(float)I6[0], (float)I6[3], (float)I6[4], (float)I6[3], (float)I6[1],
-                (float)I6[5], (float)I6[4], (float)I6[5], (float)I6[2]};
+// R I R^T for body-frame inertia I6 = (xx, yy, zz, xy, xz, yz)
+PBG_DEV s6 rotate_inertia(const m3& R, const float* I6) {
+  const float I[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
   float RI[9];
 #pragma unroll
   for (int i = 0; i < 3; i++)
@@ -157,6 +161,11 @@ PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
   W.a[4] = RI[0] * R.m[6] + RI[1] * R.m[7] + RI[2] * R.m[8];
   W.a[5] = RI[3] * R.m[6] + RI[4] * R.m[7] + RI[5] * R.m[8];
   return W;
+}
+
+PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
+  const float I[6] = {(float)I6[0], (float)I6[1], (float)I6[2], (float)I6[3], (float)I6[4], (float)I6[5]};
+  return rotate_inertia(R, I);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

@@ -4,6 +4,7 @@
 
 #include "pbg_launch.h"
 #include "pbg_step.hip"
+#include "pbg_team.hip"
 
 #ifndef PBG_ROBOT
 #error "compile with -DPBG_ROBOT=<robot struct name>"
@@ -21,7 +22,51 @@ static inline unsigned blocks(int n, int b) { return (unsigned)((n + b - 1) / b)
 // the workgroup shrinks to 32 or 16 active lanes so every CU gets a wave (the step is
 // issue/latency bound: a wave's time barely depends on its active lanes).  All resident
 // workgroups of a CU share the 160 KiB LDS for their constraint rows.
-int PBG_FN(plan_)(int n_envs, int cus, Geometry* g) {
+// Team geometry (pbg_team.hip): 4 lanes per env, 16 envs per one-wave workgroup; the
+// per-env LDS holds [mu | owner | contact rows], rows past the capacity spill to the
+// device workspace.
+template <class RR>
+static int plan_team(int n_envs, int cus, Geometry* g) {
+  if constexpr (Team<RR>::ok) {
+    using RW = TRows<RR, 16>;
+    constexpr int ES = 16;
+    const int wgs = (n_envs + ES - 1) / ES;
+    const int wpc = (wgs + cus - 1) / cus;
+    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
+    long words = (long)(budget / ((size_t)ES * sizeof(float))) - RW::HEAD;
+    int cap = (int)(words / RW::W);
+    if (cap > RW::MR) cap = RW::MR;
+    if (cap < 0) cap = 0;
+    size_t per_env = (size_t)RW::HEAD + (size_t)cap * RW::W;
+    if (per_env < (size_t)(2 * RR::NL + 2 * RR::NJ)) per_env = 2 * RR::NL + 2 * RR::NJ;  // pack staging
+    g->team = 4;
+    g->block = 64;
+    g->lds_rows = cap;
+    g->lds_bytes = (size_t)ES * sizeof(float) * per_env;
+    g->scratch_words_per_env = RW::WORDS;
+    return (int)hipFuncSetAttribute((const void*)team_step_kernel<RR, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)g->lds_bytes);
+  } else {
+    (void)n_envs; (void)cus; (void)g;
+    return (int)hipErrorInvalidValue;
+  }
+}
+template <class RR>
+static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if constexpr (Team<RR>::ok) {
+    if (g.team != 4) return false;
+    hipLaunchKernelGGL((team_step_kernel<RR, 16>), dim3(blocks(4 * B.n, 64)), dim3(64), g.lds_bytes, s, B, io, scratch,
+                       g.lds_rows);
+    return true;
+  } else {
+    (void)B; (void)io; (void)scratch; (void)g; (void)s;
+    return false;
+  }
+}
+
+int PBG_FN(plan_)(int n_envs, int cus, int allow_team, Geometry* g) {
+  if (Team<R>::ok && allow_team) return plan_team<R>(n_envs, cus, g);
+  g->team = 1;
   const int per_cu = (n_envs + cus - 1) / cus;
   int b = 16;
   while (b < per_cu && b < 64) b *= 2;
@@ -45,6 +90,7 @@ int PBG_FN(plan_)(int n_envs, int cus, Geometry* g) {
 }
 
 int PBG_FN(launch_step_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if (launch_team<R>(B, io, scratch, g, s)) return (int)hipGetLastError();
   const dim3 grid(blocks(B.n, g.block)), blk(g.block);
   if (g.block == 64) hipLaunchKernelGGL((step_kernel<R, 64>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
   else if (g.block == 32) hipLaunchKernelGGL((step_kernel<R, 32>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);

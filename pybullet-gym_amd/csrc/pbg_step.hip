@@ -270,19 +270,19 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, f3* ja = nullptr, f3* jo = nul
   k.c[0] = k.x[0];
   static_for<0, R::NL>([&](auto l_c) {
     constexpr int l = decltype(l_c)::value;
-    const int p = R::link_parent[l] + 1;
+    constexpr int p = R::link_parent[l] + 1;
     const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
     const m3 R0 = mulc(k.Rm[p], Ro);
     const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
     const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
     const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
-    const int jt = R::link_jtype[l], d = R::link_dof[l];
-    if (jt == 0) {
+    constexpr int jt = R::link_jtype[l], d = R::link_dof[l];
+    if constexpr (jt == 0) {
       const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
       k.Rm[l + 1] = mul(R0, Rj);
       k.x[l + 1] = x0 + mul(R0, anl - mulc(Rj, anl));
       if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0 + mulc(R0, anl); }
-    } else if (jt == 1) {
+    } else if constexpr (jt == 1) {
       k.Rm[l + 1] = R0;
       k.x[l + 1] = x0 + s.q[d] * mulc(R0, axl);
       if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0; }
@@ -439,20 +439,20 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     ac[0] = mk3(0, 0, 0);
     static_for<0, NB>([&](auto b_c) {
       constexpr int b = decltype(b_c)::value;
-      if (b > 0) {
-        const int l = b - 1;
-        const int p = R::link_parent[l] + 1;
-        const int jt = R::link_jtype[l], d = R::link_dof[l];
+      if constexpr (b > 0) {
+        constexpr int l = b - 1;
+        constexpr int p = R::link_parent[l] + 1;
+        constexpr int jt = R::link_jtype[l], d = R::link_dof[l];
         const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
         const m3 R0 = mulc(k.Rm[p], Ro);
         const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
         const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
         const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
-        if (jt == 0) {
+        if constexpr (jt == 0) {
           const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
           k.Rm[b] = mul(R0, Rj);
           k.x[b] = x0 + mul(R0, anl - mulc(Rj, anl));
-        } else if (jt == 1) {
+        } else if constexpr (jt == 1) {
           k.Rm[b] = R0;
           k.x[b] = x0 + s.q[d] * mulc(R0, axl);
         } else {
@@ -462,10 +462,10 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         k.c[b] = k.x[b] + mulc(k.Rm[b], (float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]);
         const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
         const f3 c = k.c[b];
-        if (jt == 0 || jt == 1) {
+        if constexpr (jt == 0 || jt == 1) {
           const f3 a = mulc(R0, axl);
           ja[d] = a;
-          if (jt == 0) {
+          if constexpr (jt == 0) {
             const f3 o = x0 + mulc(R0, anl);
             jo[d] = o;
             const f3 ro = o - cp;

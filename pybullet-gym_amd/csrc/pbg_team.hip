@@ -1,0 +1,1182 @@
+// pbg_team.hip -- quad-per-env step kernel for a floating base carrying 4 isomorphic
+// branches (AntPyBulletEnv-v0: torso + 4 legs).  Included by pbg_robot.hip after
+// pbg_step.hip; selected by plan_* when Team<R>::ok.
+//
+// Same physics, constraint-row order and numpy-exact pack as step_kernel (one lane per
+// env, pbg_step.hip), which remains the kernel for the other robots.  Here an env's work
+// is split over the 4 lanes of a quad: lane k owns branch k -- its links' kinematics and
+// composite inertias, its block of the mass matrix and those Cholesky columns, its
+// joint-limit rows and the contact rows of its slots.  Base quantities (pose, velocity,
+// the 6x6 Schur complement and its factor, u_base) are replicated in all four lanes and
+// stay bitwise identical: every cross-lane sum is a quad butterfly (DPP quad_perm) whose
+// result is the same in each lane.  PGS stays sequential in Bullet's row order
+// (scene_bases.py:65 numSolverIterations=5 -> limits, normals, frictions); per row the
+// owner's branch dot product reaches the quad by DPP and the base part is replicated.
+//
+// Why: 16,384 Ant envs are 256 waves -- one per CU, one of its four SIMDs -- in the lane
+// kernel; as quads they are 1,024 waves, one per SIMD, and each lane carries a quarter of
+// the per-env register state (no scratch spills).
+//
+// Generalized order per lane: [branch dofs leaf-first (NDB) | base lin 0..2 | base ang 0..2],
+// i.e. the lane kernel's order (pbg_step.hip Dims::gj) restricted to one branch + base.
+
+namespace pbg {
+
+// ------------------------------------------------------------------ quad (DPP) helpers
+template <int CTRL>
+PBG_DEV float qperm(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+PBG_DEV int qperm_i(int x) {
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+// sum over the quad; identical bits in all four lanes ((x0+x1)+(x2+x3), addition commutes)
+PBG_DEV float quad_sum(float x) {
+  x = x + qperm<0xB1>(x);  // quad_perm [1,0,3,2]
+  return x + qperm<0x4E>(x);  // quad_perm [2,3,0,1]
+}
+PBG_DEV int quad_sum_i(int x) {
+  x = x + qperm_i<0xB1>(x);
+  return x + qperm_i<0x4E>(x);
+}
+template <int K>
+PBG_DEV float quad_bcast(float x) { return qperm<K | (K << 2) | (K << 4) | (K << 6)>(x); }
+template <int K>
+PBG_DEV int quad_bcast_i(int x) { return qperm_i<K | (K << 2) | (K << 4) | (K << 6)>(x); }
+// LDS written by one lane and read by another lane of the same wave: a compiler fence
+// (the wave's LDS operations execute in order).
+#define PBG_QUAD_SYNC                                    \
+  {                                                      \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                     \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+  }
+
+// ------------------------------------------------------------------ branch decomposition
+template <int N>
+struct BTab {  // per-branch constant: v[entry][branch]
+  float v[N > 0 ? N : 1][4];
+};
+template <int N>
+struct BTabI {
+  int v[N > 0 ? N : 1][4];
+};
+
+template <class R>
+struct Team {
+  static constexpr int NL = R::NL, NJ = R::NJ;
+  static constexpr int roots() {
+    int c = 0;
+    for (int l = 0; l < NL; l++) c += R::link_parent[l] == -1;
+    return c;
+  }
+  static constexpr int B = roots();
+  static constexpr int NLB = B > 0 ? NL / B : 1;
+  static constexpr int NDB = B > 0 ? NJ / B : 1;
+  static constexpr int base_slots() {
+    int c = 0;
+    for (int s = 0; s < R::NS; s++) c += R::slot_link[s] == -1;
+    return c;
+  }
+  static constexpr int NS0 = base_slots();
+  static constexpr int NSB = B > 0 ? (R::NS - NS0) / B : 0;
+  static constexpr int NC = R::NS;      // contact capacity
+  static constexpr int W = NDB + 9;     // contact row: y_b | y_base(6) | meff | target | lambda
+  static constexpr int check() {
+    if (!R::floating || R::kind != 0 || R::NPAIR != 0 || R::robot_body != -1 || B != 4) return false;
+    if (NL % B || NJ % B || (R::NS - NS0) % B || NDB < 1 || NDB > 8) return false;
+    for (int s = 0; s < NS0; s++)
+      if (R::slot_link[s] != -1) return false;
+    for (int k = 0; k < B; k++) {
+      for (int i = 0; i < NLB; i++) {
+        const int l = k * NLB + i, p = R::link_parent[l];
+        if (i == 0 ? p != -1 : p != k * NLB + R::link_parent[i]) return false;
+        if (R::link_jtype[l] != R::link_jtype[i]) return false;
+        const int d0 = R::link_dof[i], d = R::link_dof[l];
+        if (d0 < 0 ? d != -1 : d != k * NDB + d0) return false;
+        if ((R::link_mass[l] > 0.0) != (R::link_mass[i] > 0.0)) return false;
+      }
+      for (int j = 0; j < NDB; j++)
+        if (R::dof_limited[k * NDB + j] != R::dof_limited[j] || R::dof_jtype[k * NDB + j] != R::dof_jtype[j]) return false;
+      for (int s = 0; s < NSB; s++)
+        if (R::slot_link[NS0 + k * NSB + s] != k * NLB + R::slot_link[NS0 + s]) return false;
+    }
+    for (int f = 0; f < R::NF; f++)
+      if (R::foot_link[f] < 0) return false;
+    for (int i = 0; i < R::NA; i++)
+      if (R::act_dof[i] < 0 || R::act_dof[i] >= NJ) return false;
+    return true;
+  }
+  static constexpr bool ok = check();
+
+  // local structure (branch 0 is the template); gen index a <-> local dof NDB-1-a
+  static constexpr int dof_of(int a) { return NDB - 1 - a; }
+  static constexpr int lg(int j) { return NDB - 1 - j; }
+  static constexpr bool moves(int j, int i) { return i >= 0 && ((R::link_chain_mask[i] >> j) & 1u); }
+  static constexpr bool coupled(int a, int b) {
+    const int da = dof_of(a), db = dof_of(b);
+    return moves(da, R::dof_link[db]) || moves(db, R::dof_link[da]);
+  }
+  static constexpr bool anc(int a, int i) { return a == i || ((R::link_anc_mask[i] >> a) & 1u); }
+  static constexpr bool owner(int i) { return R::link_dof[i] >= 0; }
+  static constexpr bool in_chain(int a, int i) { return moves(dof_of(a), i); }  // gen a moves link i
+
+  // per-branch constants
+  static constexpr BTab<NLB * 3> vec3(const double (*t)[3]) {
+    BTab<NLB * 3> r{};
+    for (int i = 0; i < NLB; i++)
+      for (int c = 0; c < 3; c++)
+        for (int k = 0; k < B; k++) r.v[i * 3 + c][k] = (float)t[k * NLB + i][c];
+    return r;
+  }
+  static constexpr BTab<NLB * 9> make_rot() {
+    BTab<NLB * 9> r{};
+    for (int i = 0; i < NLB; i++)
+      for (int k = 0; k < B; k++) {
+        const double* q = R::link_offset_quat[k * NLB + i];
+        const double x = q[0], y = q[1], z = q[2], w = q[3];
+        const double m[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                             2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                             2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+        for (int c = 0; c < 9; c++) r.v[i * 9 + c][k] = (float)m[c];
+      }
+    return r;
+  }
+  static constexpr BTab<NLB> make_mass() {
+    BTab<NLB> r{};
+    for (int i = 0; i < NLB; i++)
+      for (int k = 0; k < B; k++) r.v[i][k] = (float)R::link_mass[k * NLB + i];
+    return r;
+  }
+  static constexpr BTab<NLB * 6> make_iner() {
+    BTab<NLB * 6> r{};
+    for (int i = 0; i < NLB; i++)
+      for (int c = 0; c < 6; c++)
+        for (int k = 0; k < B; k++) r.v[i * 6 + c][k] = (float)R::link_inertia[k * NLB + i][c];
+    return r;
+  }
+  static constexpr BTab<NDB> dofs(const double* t) {
+    BTab<NDB> r{};
+    for (int j = 0; j < NDB; j++)
+      for (int k = 0; k < B; k++) r.v[j][k] = (float)t[k * NDB + j];
+    return r;
+  }
+  static constexpr BTab<NDB> make_gain() {  // tau = gain * clip(a) of the actuator driving the dof
+    BTab<NDB> r{};
+    for (int i = 0; i < R::NA; i++) r.v[R::act_dof[i] % NDB][R::act_dof[i] / NDB] = (float)R::act_gain[i];
+    return r;
+  }
+  static constexpr BTabI<NDB> make_acti() {
+    BTabI<NDB> r{};
+    for (int j = 0; j < NDB; j++)
+      for (int k = 0; k < B; k++) r.v[j][k] = -1;
+    for (int i = 0; i < R::NA; i++) r.v[R::act_dof[i] % NDB][R::act_dof[i] / NDB] = i;
+    return r;
+  }
+  static constexpr BTabI<NDB> make_rst() {
+    BTabI<NDB> r{};
+    for (int j = 0; j < NDB; j++)
+      for (int k = 0; k < B; k++) r.v[j][k] = -1;
+    for (int q = 0; q < R::NR; q++) r.v[R::reset_dof[q] % NDB][R::reset_dof[q] / NDB] = q;
+    return r;
+  }
+  static constexpr BTabI<NLB> make_foot() {
+    BTabI<NLB> r{};
+    for (int i = 0; i < NLB; i++)
+      for (int k = 0; k < B; k++) r.v[i][k] = -1;
+    for (int f = 0; f < R::NF; f++) r.v[R::foot_link[f] % NLB][R::foot_link[f] / NLB] = f;
+    return r;
+  }
+  static constexpr BTab<NSB * 3> make_spt() {
+    BTab<NSB * 3> r{};
+    for (int s = 0; s < NSB; s++)
+      for (int c = 0; c < 3; c++)
+        for (int k = 0; k < B; k++) r.v[s * 3 + c][k] = (float)R::slot_point[NS0 + k * NSB + s][c];
+    return r;
+  }
+  static constexpr BTab<NSB> slots(const double* t) {
+    BTab<NSB> r{};
+    for (int s = 0; s < NSB; s++)
+      for (int k = 0; k < B; k++) r.v[s][k] = (float)t[NS0 + k * NSB + s];
+    return r;
+  }
+  static constexpr BTab<NLB * 3> OFFP = vec3(R::link_offset_pos);
+  static constexpr BTab<NLB * 3> AXIS = vec3(R::link_axis);
+  static constexpr BTab<NLB * 3> ANCH = vec3(R::link_anchor);
+  static constexpr BTab<NLB * 3> COM = vec3(R::link_com);
+  static constexpr BTab<NLB * 9> ROT = make_rot();
+  static constexpr BTab<NLB> MASS = make_mass();
+  static constexpr BTab<NLB * 6> INER = make_iner();
+  static constexpr BTab<NDB> DLO = dofs(R::dof_lower);
+  static constexpr BTab<NDB> DHI = dofs(R::dof_upper);
+  static constexpr BTab<NDB> DAMP = dofs(R::dof_damping);
+  static constexpr BTab<NDB> ARM = dofs(R::dof_armature);
+  static constexpr BTab<NDB> GAIN = make_gain();
+  static constexpr BTabI<NDB> ACTI = make_acti();
+  static constexpr BTabI<NDB> RST = make_rst();
+  static constexpr BTabI<NLB> FOOT = make_foot();
+  static constexpr BTab<NSB * 3> SPT = make_spt();
+  static constexpr BTab<NSB> SRAD = slots(R::slot_radius);
+  static constexpr BTab<NSB> SMU = slots(R::slot_mu);
+};
+
+// The lane's branch and its one-hot weights, for picking per-branch constants.
+struct Lane {
+  int k;
+  bool odd, hi, mid;
+  float e0, e1, e2, e3;
+};
+PBG_DEV Lane make_lane(int k) {
+  Lane L;
+  L.k = k;
+  L.odd = k & 1;
+  L.hi = k >= 2;
+  L.mid = k == 1 || k == 2;
+  L.e0 = k == 0; L.e1 = k == 1; L.e2 = k == 2; L.e3 = k == 3;
+  return L;
+}
+// per-branch constant of entry I of table T for this lane (a constant when all branches agree)
+template <const auto& T, int I>
+PBG_DEV float pk(const Lane& L) {
+  constexpr float a0 = T.v[I][0], a1 = T.v[I][1], a2 = T.v[I][2], a3 = T.v[I][3];
+  if constexpr (a0 == a1 && a0 == a2 && a0 == a3) return a0;
+  else if constexpr (a0 == a2 && a1 == a3) return L.odd ? a1 : a0;
+  else if constexpr (a0 == a1 && a2 == a3) return L.hi ? a2 : a0;
+  else if constexpr (a0 == a3 && a1 == a2) return L.mid ? a1 : a0;
+  else return a0 * L.e0 + a1 * L.e1 + a2 * L.e2 + a3 * L.e3;
+}
+template <const auto& T, int I>
+PBG_DEV int pki(const Lane& L) {
+  constexpr int a0 = T.v[I][0], a1 = T.v[I][1], a2 = T.v[I][2], a3 = T.v[I][3];
+  if constexpr (a1 - a0 == a2 - a1 && a2 - a1 == a3 - a2) return a0 + (a1 - a0) * L.k;
+  else return L.k == 0 ? a0 : (L.k == 1 ? a1 : (L.k == 2 ? a2 : a3));
+}
+template <const auto& T, int I>
+PBG_DEV f3 pk3(const Lane& L) {
+  return mk3(pk<T, 3 * I>(L), pk<T, 3 * I + 1>(L), pk<T, 3 * I + 2>(L));
+}
+
+// ------------------------------------------------------------------ per-lane state
+template <class R>
+struct TState {
+  static constexpr int NDB = Team<R>::NDB;
+  float bp[3], bq[4], bv[3], bw[3];  // replicated
+  float q[NDB], qd[NDB];             // this lane's branch dofs (local order)
+};
+
+template <class R>
+struct TKin {  // this lane's branch links
+  static constexpr int NLB = Team<R>::NLB;
+  m3 Rm[NLB];
+  f3 x[NLB], c[NLB];
+};
+
+// branch forward kinematics (positions); joint axes / anchors of the branch dofs on request
+template <class R, bool AXES = false>
+PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k, f3* ja = nullptr, f3* jo = nullptr) {
+  using T = Team<R>;
+  const f3 xb = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  static_for<0, T::NLB>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
+    constexpr int p = R::link_parent[i], jt = R::link_jtype[i], d = R::link_dof[i];
+    const m3& Rp = p < 0 ? Rb : k.Rm[p < 0 ? 0 : p];
+    const f3 xp = p < 0 ? xb : k.x[p < 0 ? 0 : p];
+    m3 Ro;
+#pragma unroll
+    for (int c = 0; c < 9; c++) Ro.m[c] = 0.f;
+    static_for<0, 9>([&](auto c_c) { Ro.m[decltype(c_c)::value] = pk<T::ROT, 9 * i + decltype(c_c)::value>(L); });
+    const m3 R0 = mulc(Rp, Ro);
+    const f3 x0 = xp + mulc(Rp, pk3<T::OFFP, i>(L));
+    if constexpr (jt == 0) {
+      const f3 axl = pk3<T::AXIS, i>(L), anl = pk3<T::ANCH, i>(L);
+      const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
+      k.Rm[i] = mul(R0, Rj);
+      k.x[i] = x0 + mul(R0, anl - mulc(Rj, anl));
+      if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0 + mulc(R0, anl); }
+    } else if constexpr (jt == 1) {
+      const f3 axl = pk3<T::AXIS, i>(L);
+      k.Rm[i] = R0;
+      k.x[i] = x0 + s.q[d] * mulc(R0, axl);
+      if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0; }
+    } else {
+      k.Rm[i] = R0;
+      k.x[i] = x0;
+    }
+    k.c[i] = k.x[i] + mulc(k.Rm[i], pk3<T::COM, i>(L));
+  });
+}
+
+// ------------------------------------------------------------------ contact rows
+// Per env (shared by its quad): [mu (NC) | owner lane (NC) | rows], LDS [word][env] with
+// stride = envs per workgroup; rows beyond the LDS capacity in a device workspace
+// [word][env].  Row: y_branch (NDB, the owner's branch) | y_base (6) | meff | target | lambda.
+template <class R, int ES>
+struct TRows {
+  using T = Team<R>;
+  static constexpr int NDB = T::NDB, W = T::W, NC = T::NC, MR = 3 * T::NC;
+  static constexpr int HEAD = 2 * NC;
+  static constexpr int WORDS = MR * W;  // device workspace words per env
+  lds_float* lds;  // LDS base + env slot
+  float* gbl;      // workspace base + env
+  int n;
+  int cap;         // rows resident in LDS
+  PBG_DEV lds_float& mu(int c) const { return lds[(size_t)c * ES]; }
+  PBG_DEV lds_float& own(int c) const { return lds[(size_t)(NC + c) * ES]; }
+  PBG_DEV lds_float& stage(int w) const { return lds[(size_t)w * ES]; }
+  template <class P>
+  static PBG_DEV void put_at(P p, size_t st, const float* yb, const float* yB, float meff, float target) {
+#pragma unroll
+    for (int i = 0; i < NDB; i++) p[i * st] = yb[i];
+#pragma unroll
+    for (int g = 0; g < 6; g++) p[(NDB + g) * st] = yB[g];
+    p[(NDB + 6) * st] = meff;
+    p[(NDB + 7) * st] = target;
+    p[(NDB + 8) * st] = 0.f;
+  }
+  template <class P>
+  static PBG_DEV void solve_at(P p, size_t st, float* ub, float* uB, bool mine, float lo, float hi) {
+    float yb[NDB], yB[6];
+#pragma unroll
+    for (int i = 0; i < NDB; i++) yb[i] = p[i * st];
+#pragma unroll
+    for (int g = 0; g < 6; g++) yB[g] = p[(NDB + g) * st];
+    const float meff = p[(NDB + 6) * st], tgt = p[(NDB + 7) * st], lam0 = p[(NDB + 8) * st];
+    float pb = 0.f;
+#pragma unroll
+    for (int i = 0; i < NDB; i++) pb += yb[i] * ub[i];
+    const float yub = quad_sum(mine ? pb : 0.f);
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 6; g += 2) { a0 += yB[g] * uB[g]; a1 += yB[g + 1] * uB[g + 1]; }
+    const float yu = yub + (a0 + a1);
+    const float nl = fminf(fmaxf(lam0 + meff * (tgt - yu), lo), hi);
+    const float dl = nl - lam0;
+    p[(NDB + 8) * st] = nl;
+#pragma unroll
+    for (int g = 0; g < 6; g++) uB[g] += yB[g] * dl;
+    const float dlb = mine ? dl : 0.f;
+#pragma unroll
+    for (int i = 0; i < NDB; i++) ub[i] += yb[i] * dlb;
+  }
+  PBG_DEV void put(int r, const float* yb, const float* yB, float meff, float target) const {
+    if (r < cap) put_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, yb, yB, meff, target);
+    else put_at(gbl + (size_t)r * W * n, (size_t)n, yb, yB, meff, target);
+  }
+  PBG_DEV float lam(int r) const {
+    if (r < cap) return lds[(size_t)(HEAD + r * W + NDB + 8) * ES];
+    return gbl[((size_t)r * W + NDB + 8) * n];
+  }
+  PBG_DEV void solve(int r, float* ub, float* uB, bool mine, float lo, float hi) const {
+    if (r < cap) solve_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, ub, uB, mine, lo, hi);
+    else solve_at(gbl + (size_t)r * W * n, (size_t)n, ub, uB, mine, lo, hi);
+  }
+};
+
+// y_base = Lbb^-1 t (6x6 lower, reciprocal diagonal)
+PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
+  static_for<0, 6>([&](auto g_c) {
+    constexpr int g = decltype(g_c)::value;
+    float v = t[g];
+    static_for<0, g>([&](auto h_c) { v -= Lbb[g][decltype(h_c)::value] * t[decltype(h_c)::value]; });
+    t[g] = v * Ldb[g];
+  });
+}
+
+// ------------------------------------------------------------------ one physics sub-step
+template <class R, int ES>
+PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t& slot_bits, uint32_t& base_bits,
+                         const TRows<R, ES>& rw SUB_STAMP_ARGS) {
+  using T = Team<R>;
+  constexpr int NDB = T::NDB, NLB = T::NLB;
+  constexpr float dt = (float)R::dt_sub;
+  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
+  constexpr float g = (float)PBG_GRAVITY;
+  const int kb = L.k;
+
+  // --- phase A: branch kinematics, velocities, bias accelerations; composites of the
+  // branch's dof-owning links and the branch total (all about O = base COM)
+  const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+  const f3 O = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  const f3 w0 = mk3(s.bw[0], s.bw[1], s.bw[2]), v0 = mk3(s.bv[0], s.bv[1], s.bv[2]);
+  TKin<R> k;
+  f3 ja[NDB], jo[NDB];
+  float cmass[NLB];
+  f3 cp1[NLB], cF[NLB], cN[NLB];
+  s6 cJ[NLB];
+  float tm = 0.f;
+  f3 tp1 = mk3(0, 0, 0), tF = mk3(0, 0, 0), tN = mk3(0, 0, 0);
+  s6 tJ;
+#pragma unroll
+  for (int i = 0; i < 6; i++) tJ.a[i] = 0.f;
+  static_for<0, NLB>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (T::owner(i)) {
+      cmass[i] = 0.f; cp1[i] = mk3(0, 0, 0); cF[i] = mk3(0, 0, 0); cN[i] = mk3(0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < 6; c++) cJ[i].a[c] = 0.f;
+    }
+  });
+  {
+    f3 w[NLB], v[NLB], al[NLB], ac[NLB];
+    static_for<0, NLB>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      constexpr int p = R::link_parent[i], jt = R::link_jtype[i], d = R::link_dof[i];
+      const m3& Rp = p < 0 ? Rb : k.Rm[p < 0 ? 0 : p];
+      const f3 xp = p < 0 ? O : k.x[p < 0 ? 0 : p];
+      const f3 cp = p < 0 ? O : k.c[p < 0 ? 0 : p];
+      const f3 wp = p < 0 ? w0 : w[p < 0 ? 0 : p], vp = p < 0 ? v0 : v[p < 0 ? 0 : p];
+      const f3 alp = p < 0 ? mk3(0, 0, 0) : al[p < 0 ? 0 : p], acp = p < 0 ? mk3(0, 0, 0) : ac[p < 0 ? 0 : p];
+      m3 Ro;
+      static_for<0, 9>([&](auto c_c) { Ro.m[decltype(c_c)::value] = pk<T::ROT, 9 * i + decltype(c_c)::value>(L); });
+      const m3 R0 = mulc(Rp, Ro);
+      const f3 x0 = xp + mulc(Rp, pk3<T::OFFP, i>(L));
+      if constexpr (jt == 0) {
+        const f3 axl = pk3<T::AXIS, i>(L), anl = pk3<T::ANCH, i>(L);
+        const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
+        k.Rm[i] = mul(R0, Rj);
+        k.x[i] = x0 + mul(R0, anl - mulc(Rj, anl));
+        k.c[i] = k.x[i] + mulc(k.Rm[i], pk3<T::COM, i>(L));
+        const f3 a = mulc(R0, axl);
+        const f3 o = x0 + mulc(R0, anl);
+        ja[d] = a;
+        jo[d] = o;
+        const f3 ro = o - cp;
+        const f3 vo = vp + cross3(wp, ro);
+        const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+        const f3 wl = wp + s.qd[d] * a;
+        const f3 all = alp + s.qd[d] * cross3(wp, a);
+        const f3 rc = k.c[i] - o;
+        w[i] = wl;
+        al[i] = all;
+        v[i] = vo + cross3(wl, rc);
+        ac[i] = ao + cross3(all, rc) + cross3(wl, cross3(wl, rc));
+      } else if constexpr (jt == 1) {
+        const f3 axl = pk3<T::AXIS, i>(L);
+        k.Rm[i] = R0;
+        const f3 a = mulc(R0, axl);
+        k.x[i] = x0 + s.q[d] * a;
+        k.c[i] = k.x[i] + mulc(k.Rm[i], pk3<T::COM, i>(L));
+        ja[d] = a;
+        jo[d] = x0;
+        const f3 r = k.c[i] - cp;
+        w[i] = wp;
+        al[i] = alp;
+        v[i] = vp + cross3(wp, r) + s.qd[d] * a;
+        ac[i] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * s.qd[d]) * cross3(wp, a);
+      } else {
+        k.Rm[i] = R0;
+        k.x[i] = x0;
+        k.c[i] = k.x[i] + mulc(k.Rm[i], pk3<T::COM, i>(L));
+        const f3 r = k.c[i] - cp;
+        w[i] = wp;
+        al[i] = alp;
+        v[i] = vp + cross3(wp, r);
+        ac[i] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
+      }
+      if constexpr (R::link_mass[i] > 0.0) {
+        const float m = pk<T::MASS, i>(L);
+        float I6[6];
+        static_for<0, 6>([&](auto c_c) { I6[decltype(c_c)::value] = pk<T::INER, 6 * i + decltype(c_c)::value>(L); });
+        const s6 Iw = rotate_inertia(k.Rm[i], I6);
+        const f3 r = k.c[i] - O;
+        const float rr = dot3(r, r);
+        s6 J;
+        J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
+        J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
+        J.a[2] = Iw.a[2] + m * (rr - r.z * r.z);
+        J.a[3] = Iw.a[3] - m * r.x * r.y;
+        J.a[4] = Iw.a[4] - m * r.x * r.z;
+        J.a[5] = Iw.a[5] - m * r.y * r.z;
+        const f3 Iww = mul(Iw, w[i]);
+        const f3 f = m * (ac[i] - mk3(0, 0, -g)) +
+                     (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[i]))) * v[i];
+        const f3 n = mul(Iw, al[i]) + cross3(w[i], Iww) +
+                     ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[i])) * Iww;
+        const f3 pr = m * r, Nn = n + cross3(r, f);
+        static_for<0, NLB>([&](auto a_c) {
+          constexpr int a = decltype(a_c)::value;
+          if constexpr (T::owner(a) && T::anc(a, i)) {
+            cmass[a] += m; cp1[a] += pr; cF[a] += f; cN[a] += Nn;
+#pragma unroll
+            for (int c = 0; c < 6; c++) cJ[a].a[c] += J.a[c];
+          }
+        });
+        tm += m; tp1 += pr; tF += f; tN += Nn;
+#pragma unroll
+        for (int c = 0; c < 6; c++) tJ.a[c] += J.a[c];
+      }
+      PBG_PHASE_BARRIER
+    });
+  }
+  // whole-robot composite = sum of the branch totals + the base body (at O: r = 0)
+  {
+    tm = quad_sum(tm);
+    tp1 = mk3(quad_sum(tp1.x), quad_sum(tp1.y), quad_sum(tp1.z));
+    tF = mk3(quad_sum(tF.x), quad_sum(tF.y), quad_sum(tF.z));
+    tN = mk3(quad_sum(tN.x), quad_sum(tN.y), quad_sum(tN.z));
+#pragma unroll
+    for (int c = 0; c < 6; c++) tJ.a[c] = quad_sum(tJ.a[c]);
+    const float m = (float)R::base_mass;
+    const s6 Iw = rotate_inertia(Rb, R::base_inertia);
+    const f3 Iww = mul(Iw, w0);
+    const f3 f = m * (mk3(0, 0, g)) + (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v0))) * v0;
+    const f3 n = cross3(w0, Iww) + ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w0)) * Iww;
+    tm += m; tF += f; tN += n;
+#pragma unroll
+    for (int c = 0; c < 6; c++) tJ.a[c] += Iw.a[c];
+  }
+
+  STAMP(0)
+  // --- mass matrix: branch block Lbr, base-branch block Lgb, base block Mbb; bias -------
+  float Lbr[NDB][NDB], Lgb[6][NDB], Mbb[6][6];
+  float rb[NDB], rB[6];
+  f3 sw[NDB], sv[NDB];
+  static_for<0, NDB>([&](auto a_c) {
+    constexpr int a = decltype(a_c)::value;
+    constexpr int d = T::dof_of(a);
+    if constexpr (R::dof_jtype[d] == 0) { sw[a] = ja[d]; sv[a] = cross3(jo[d] - O, ja[d]); }
+    else { sw[a] = mk3(0, 0, 0); sv[a] = ja[d]; }
+  });
+  static_for<0, NDB>([&](auto a_c) {
+    constexpr int a = decltype(a_c)::value;
+    constexpr int ia = R::dof_link[T::dof_of(a)];
+    rb[a] = -(dot3(sw[a], cN[ia]) + dot3(sv[a], cF[ia]));
+    static_for<0, a + 1>([&](auto b_c) {
+      constexpr int b = decltype(b_c)::value;
+      if constexpr (T::coupled(a, b)) {
+        constexpr int ibk = R::dof_link[T::dof_of(b)];
+        const f3 Jw_ = mul(cJ[ibk], sw[b]) + cross3(cp1[ibk], sv[b]);
+        const f3 Fv = cmass[ibk] * sv[b] - cross3(cp1[ibk], sw[b]);
+        Lbr[a][b] = dot3(sw[a], Jw_) + dot3(sv[a], Fv);
+      }
+    });
+    // base rows g against this dof (the dof's composite): lin g -> Fv_g, ang g -> Jw_g
+    const f3 Jw_ = mul(cJ[ia], sw[a]) + cross3(cp1[ia], sv[a]);
+    const f3 Fv = cmass[ia] * sv[a] - cross3(cp1[ia], sw[a]);
+    Lgb[0][a] = Fv.x; Lgb[1][a] = Fv.y; Lgb[2][a] = Fv.z;
+    Lgb[3][a] = Jw_.x; Lgb[4][a] = Jw_.y; Lgb[5][a] = Jw_.z;
+  });
+  // base block (lower): lin-lin m I; ang-lin p1 x e_h; ang-ang J
+  Mbb[0][0] = tm; Mbb[1][1] = tm; Mbb[2][2] = tm;
+  Mbb[1][0] = 0.f; Mbb[2][0] = 0.f; Mbb[2][1] = 0.f;
+  Mbb[3][0] = 0.f;      Mbb[4][0] = tp1.z;  Mbb[5][0] = -tp1.y;  // p1 x e_x = (0, p1z, -p1y)
+  Mbb[3][1] = -tp1.z;   Mbb[4][1] = 0.f;    Mbb[5][1] = tp1.x;   // p1 x e_y = (-p1z, 0, p1x)
+  Mbb[3][2] = tp1.y;    Mbb[4][2] = -tp1.x; Mbb[5][2] = 0.f;     // p1 x e_z = (p1y, -p1x, 0)
+  Mbb[3][3] = tJ.a[0]; Mbb[4][4] = tJ.a[1]; Mbb[5][5] = tJ.a[2];
+  Mbb[4][3] = tJ.a[3]; Mbb[5][3] = tJ.a[4]; Mbb[5][4] = tJ.a[5];
+  rB[0] = -tF.x; rB[1] = -tF.y; rB[2] = -tF.z;
+  rB[3] = -tN.x; rB[4] = -tN.y; rB[5] = -tN.z;
+  static_for<0, NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    constexpr int a = T::lg(j);
+    Lbr[a][a] += pk<T::ARM, j>(L);
+    rb[a] += tau[j] - pk<T::DAMP, j>(L) * s.qd[j];
+  });
+
+  STAMP(1)
+  // --- Cholesky: branch columns (lane), Schur complement of the base (quad sum), 6x6 ----
+  float Ld[NDB];
+  static_for<0, NDB>([&](auto b_c) {
+    constexpr int b = decltype(b_c)::value;
+    float sbb = Lbr[b][b];
+    static_for<0, b>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      if constexpr (T::coupled(b, kk)) sbb -= Lbr[b][kk] * Lbr[b][kk];
+    });
+    const float lbb = fast_sqrt(sbb);
+    const float inv = fast_rcp(lbb);
+    Ld[b] = inv;
+    Lbr[b][b] = lbb;
+    static_for<b + 1, NDB>([&](auto a_c) {
+      constexpr int a = decltype(a_c)::value;
+      if constexpr (T::coupled(a, b)) {
+        float t = Lbr[a][b];
+        static_for<0, b>([&](auto k_c) {
+          constexpr int kk = decltype(k_c)::value;
+          if constexpr (T::coupled(a, kk) && T::coupled(b, kk)) t -= Lbr[a][kk] * Lbr[b][kk];
+        });
+        Lbr[a][b] = t * inv;
+      }
+    });
+#pragma unroll
+    for (int gg = 0; gg < 6; gg++) {
+      float t = Lgb[gg][b];
+      static_for<0, b>([&](auto k_c) {
+        constexpr int kk = decltype(k_c)::value;
+        if constexpr (T::coupled(b, kk)) t -= Lgb[gg][kk] * Lbr[b][kk];
+      });
+      Lgb[gg][b] = t * inv;
+    }
+  });
+  float Lbb[6][6], Ldb[6];
+  static_for<0, 6>([&](auto g_c) {
+    constexpr int gg = decltype(g_c)::value;
+    static_for<0, gg + 1>([&](auto h_c) {
+      constexpr int h = decltype(h_c)::value;
+      float c = 0.f;
+#pragma unroll
+      for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * Lgb[h][b];
+      Lbb[gg][h] = Mbb[gg][h] - quad_sum(c);
+    });
+  });
+  static_for<0, 6>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    float sjj = Lbb[j][j];
+    static_for<0, j>([&](auto k_c) { sjj -= Lbb[j][decltype(k_c)::value] * Lbb[j][decltype(k_c)::value]; });
+    const float ljj = fast_sqrt(sjj);
+    const float inv = fast_rcp(ljj);
+    Ldb[j] = inv;
+    Lbb[j][j] = ljj;
+    static_for<j + 1, 6>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      float t = Lbb[i][j];
+      static_for<0, j>([&](auto k_c) { t -= Lbb[i][decltype(k_c)::value] * Lbb[j][decltype(k_c)::value]; });
+      Lbb[i][j] = t * inv;
+    });
+  });
+
+  // --- unconstrained velocity nu_pred = nu + dt M^-1 (tau - C); u = L^T nu_pred --------
+  float yb[NDB], yB[6];
+  static_for<0, NDB>([&](auto a_c) {
+    constexpr int a = decltype(a_c)::value;
+    float t = rb[a];
+    static_for<0, a>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      if constexpr (T::coupled(a, kk)) t -= Lbr[a][kk] * yb[kk];
+    });
+    yb[a] = t * Ld[a];
+  });
+#pragma unroll
+  for (int gg = 0; gg < 6; gg++) {
+    float c = 0.f;
+#pragma unroll
+    for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * yb[b];
+    yB[gg] = rB[gg] - quad_sum(c);
+  }
+  fwd6(Lbb, Ldb, yB);
+  float xB[6], xb[NDB];
+  static_for<0, 6>([&](auto r_c) {
+    constexpr int gg = 5 - decltype(r_c)::value;
+    float t = yB[gg];
+    static_for<gg + 1, 6>([&](auto h_c) { t -= Lbb[decltype(h_c)::value][gg] * xB[decltype(h_c)::value]; });
+    xB[gg] = t * Ldb[gg];
+  });
+  static_for<0, NDB>([&](auto r_c) {
+    constexpr int a = NDB - 1 - decltype(r_c)::value;
+    float t = yb[a];
+    static_for<a + 1, NDB>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      if constexpr (T::coupled(kk, a)) t -= Lbr[kk][a] * xb[kk];
+    });
+#pragma unroll
+    for (int gg = 0; gg < 6; gg++) t -= Lgb[gg][a] * xB[gg];
+    xb[a] = t * Ld[a];
+  });
+  float nb[NDB], nB[6];
+  static_for<0, NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    constexpr int a = T::lg(j);
+    nb[a] = fminf(fmaxf(s.qd[j] + dt * xb[a], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+  });
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    nB[i] = fminf(fmaxf(s.bv[i] + dt * xB[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    nB[3 + i] = fminf(fmaxf(s.bw[i] + dt * xB[3 + i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+  }
+  float ub[NDB], uB[6];
+  static_for<0, NDB>([&](auto a_c) {
+    constexpr int a = decltype(a_c)::value;
+    float t = 0.f;
+    static_for<a, NDB>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      if constexpr (T::coupled(kk, a)) t += Lbr[kk][a] * nb[kk];
+    });
+#pragma unroll
+    for (int gg = 0; gg < 6; gg++) t += Lgb[gg][a] * nB[gg];
+    ub[a] = t;
+  });
+  static_for<0, 6>([&](auto g_c) {
+    constexpr int gg = decltype(g_c)::value;
+    float t = 0.f;
+    static_for<gg, 6>([&](auto h_c) { t += Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
+    uB[gg] = t;
+  });
+
+  STAMP(2)
+  // --- joint-limit rows (lane: its branch dofs), in registers; base part broadcast ------
+  constexpr int NLIMB = [] {
+    int c = 0;
+    for (int j = 0; j < NDB; j++) c += R::dof_limited[j];
+    return c;
+  }();
+  constexpr int NLB_ = NLIMB > 0 ? NLIMB : 1;
+  float Lyb[NLB_][NDB], Lm[NLB_], Ltl[NLB_], Lth[NLB_], LyB[NLB_][6];
+  static_for<0, NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    if constexpr (R::dof_limited[j]) {
+      constexpr int li = [] {
+        int c = 0;
+        for (int jj = 0; jj < j; jj++) c += R::dof_limited[jj];
+        return c;
+      }();
+      constexpr int gd = T::lg(j);
+      float y[NDB];
+      static_for<0, NDB>([&](auto a_c) {
+        constexpr int a = decltype(a_c)::value;
+        if constexpr (a < gd || !T::coupled(a, gd)) {
+          y[a] = 0.f;
+        } else {
+          float t = a == gd ? 1.f : 0.f;
+          static_for<gd, a>([&](auto k_c) {
+            constexpr int kk = decltype(k_c)::value;
+            if constexpr (T::coupled(a, kk) && T::coupled(kk, gd)) t -= Lbr[a][kk] * y[kk];
+          });
+          y[a] = t * Ld[a];
+        }
+      });
+      float t6[6];
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) {
+        float c = 0.f;
+#pragma unroll
+        for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * y[b];
+        t6[gg] = -c;
+      }
+      fwd6(Lbb, Ldb, t6);
+      float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; vJ += y[a] * ub[a]; }
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; vJ += t6[gg] * uB[gg]; }
+      const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
+      const float plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
+      Ltl[li] = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
+      Lth[li] = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
+      Lm[li] = meff;
+#pragma unroll
+      for (int a = 0; a < NDB; a++) Lyb[li][a] = y[a];
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) LyB[li][gg] = t6[gg];
+    }
+  });
+  // every lane needs each branch's base part, m_eff and targets (replicated PGS math)
+  float BY[4][NLB_][6], Bm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
+  static_for<0, 4>([&](auto k_c) {
+    constexpr int kk = decltype(k_c)::value;
+    static_for<0, NLIMB>([&](auto l_c) {
+      constexpr int li = decltype(l_c)::value;
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) BY[kk][li][gg] = quad_bcast<kk>(LyB[li][gg]);
+      Bm[kk][li] = quad_bcast<kk>(Lm[li]);
+      Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
+      Bth[kk][li] = quad_bcast<kk>(Lth[li]);
+      Blo[kk][li] = 0.f;
+      Bhi[kk][li] = 0.f;
+    });
+  });
+
+  STAMP(3)
+  // --- contact rows: base slots (replicated), then each branch's slots (owner lane) ------
+  int n0 = 0;
+  base_bits = 0;
+  static_for<0, T::NS0>([&](auto sl_c) {
+    constexpr int sl = decltype(sl_c)::value;
+    const f3 cc = O + mulc(Rb, (float)R::slot_point[sl][0], (float)R::slot_point[sl][1], (float)R::slot_point[sl][2]);
+    const float rad = (float)R::slot_radius[sl];
+    const float dist = cc.z - rad;
+    if (!(dist < (float)PBG_CONTACT_THRESHOLD)) return;
+    base_bits |= 1u << sl;
+    const f3 rP = mk3(cc.x, cc.y, cc.z - rad) - O;
+#pragma unroll
+    for (int dir = 0; dir < 3; dir++) {
+      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 mm = cross3(rP, nd);
+      float y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+      fwd6(Lbb, Ldb, y6);
+      float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; vJ += y6[gg] * uB[gg]; }
+      float z[NDB];
+#pragma unroll
+      for (int a = 0; a < NDB; a++) z[a] = 0.f;
+      rw.put(3 * n0 + dir, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+    }
+    rw.mu(n0) = (float)R::slot_mu[sl];
+    rw.own(n0) = -1.f;
+    n0++;
+  });
+  // this branch's active slots, then their contact indices (exclusive quad prefix)
+  uint32_t act = 0;
+  float sdist[T::NSB > 0 ? T::NSB : 1];
+  f3 sP[T::NSB > 0 ? T::NSB : 1];
+  static_for<0, T::NSB>([&](auto sl_c) {
+    constexpr int sl = decltype(sl_c)::value;
+    constexpr int li = R::slot_link[T::NS0 + sl];
+    const f3 cc = k.x[li] + mulc(k.Rm[li], pk3<T::SPT, sl>(L));
+    const float rad = pk<T::SRAD, sl>(L);
+    sdist[sl] = cc.z - rad;
+    sP[sl] = mk3(cc.x, cc.y, cc.z - rad);
+    act |= (sdist[sl] < (float)PBG_CONTACT_THRESHOLD ? 1u : 0u) << sl;
+  });
+  const int cnt = __builtin_popcount(act);
+  const int c0 = quad_bcast_i<0>(cnt), c1 = quad_bcast_i<1>(cnt), c2 = quad_bcast_i<2>(cnt), c3 = quad_bcast_i<3>(cnt);
+  int ci = n0 + (kb > 0 ? c0 : 0) + (kb > 1 ? c1 : 0) + (kb > 2 ? c2 : 0);
+  const int nc = n0 + c0 + c1 + c2 + c3;
+  slot_bits = act;
+  static_for<0, T::NSB>([&](auto sl_c) {
+    constexpr int sl = decltype(sl_c)::value;
+    if (!((act >> sl) & 1u)) return;
+    constexpr int li = R::slot_link[T::NS0 + sl];
+    const float dist = sdist[sl];
+    const f3 rP = sP[sl] - O;
+#pragma unroll
+    for (int dir = 0; dir < 3; dir++) {
+      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 mm = cross3(rP, nd);
+      float y[NDB];
+      static_for<0, NDB>([&](auto a_c) {
+        constexpr int a = decltype(a_c)::value;
+        if constexpr (!T::in_chain(a, li)) {
+          y[a] = 0.f;
+        } else {
+          float t = dot3(nd, sv[a]) + dot3(mm, sw[a]);
+          static_for<0, a>([&](auto k_c) {
+            constexpr int kk = decltype(k_c)::value;
+            if constexpr (T::coupled(a, kk) && T::in_chain(kk, li)) t -= Lbr[a][kk] * y[kk];
+          });
+          y[a] = t * Ld[a];
+        }
+      });
+      float y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) {
+#pragma unroll
+        for (int b = 0; b < NDB; b++) y6[gg] -= Lgb[gg][b] * y[b];
+      }
+      fwd6(Lbb, Ldb, y6);
+      float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; vJ += y[a] * ub[a]; }
+#pragma unroll
+      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; vJ += y6[gg] * uB[gg]; }
+      rw.put(3 * ci + dir, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+    }
+    rw.mu(ci) = pk<T::SMU, sl>(L);
+    rw.own(ci) = (float)kb;
+    ci++;
+  });
+  if (3 * nc > rw.cap) {  // rows in the device workspace: same-CU visibility
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  PBG_QUAD_SYNC
+
+  STAMP(4)
+  // --- PGS, 5 sweeps, Bullet order: joint limits (dof order), normals, frictions ------
+  for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+    static_for<0, 4>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      static_for<0, NLIMB>([&](auto l_c) {
+        constexpr int li = decltype(l_c)::value;
+        float pb = 0.f;
+#pragma unroll
+        for (int a = 0; a < NDB; a++) pb += Lyb[li][a] * ub[a];
+        const float yub = quad_bcast<kk>(pb);
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int gg = 0; gg < 6; gg += 2) { a0 += BY[kk][li][gg] * uB[gg]; a1 += BY[kk][li][gg + 1] * uB[gg + 1]; }
+        const float yu = yub + (a0 + a1);
+        const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
+        const float nlo = fminf(fmaxf(llo + meff * (Btl[kk][li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float dlo = nlo - llo;
+        // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
+        const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
+        const float nhi = fminf(fmaxf(lhi + meff * (Bth[kk][li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float dhi = nhi - lhi;
+        Blo[kk][li] = nlo;
+        Bhi[kk][li] = nhi;
+        const float dl = dlo - dhi;
+#pragma unroll
+        for (int gg = 0; gg < 6; gg++) uB[gg] += BY[kk][li][gg] * dl;
+        const float dlb = kb == kk ? dl : 0.f;
+#pragma unroll
+        for (int a = 0; a < NDB; a++) ub[a] += Lyb[li][a] * dlb;
+      });
+    });
+    for (int c = 0; c < nc; c++) rw.solve(3 * c, ub, uB, (int)rw.own(c) == kb, 0.f, 3.0e38f);
+    for (int c = 0; c < nc; c++) {
+      const float ln = rw.lam(3 * c);
+      if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
+      const float lim = rw.mu(c) * ln;
+      const bool mine = (int)rw.own(c) == kb;
+      rw.solve(3 * c + 1, ub, uB, mine, -lim, lim);
+      rw.solve(3 * c + 2, ub, uB, mine, -lim, lim);
+    }
+  }
+
+  STAMP(5)
+  // --- nu = L^-T u (base first, replicated; then the branch); clamp; integrate ---------
+  static_for<0, 6>([&](auto r_c) {
+    constexpr int gg = 5 - decltype(r_c)::value;
+    float t = uB[gg];
+    static_for<gg + 1, 6>([&](auto h_c) { t -= Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
+    nB[gg] = fminf(fmaxf(t * Ldb[gg], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+  });
+  static_for<0, NDB>([&](auto r_c) {
+    constexpr int a = NDB - 1 - decltype(r_c)::value;
+    float t = ub[a];
+    static_for<a + 1, NDB>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      if constexpr (T::coupled(kk, a)) t -= Lbr[kk][a] * nb[kk];
+    });
+#pragma unroll
+    for (int gg = 0; gg < 6; gg++) t -= Lgb[gg][a] * nB[gg];
+    nb[a] = t * Ld[a];
+  });
+  static_for<0, NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    s.qd[j] = fminf(fmaxf(nb[T::lg(j)], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    s.q[j] += dt * s.qd[j];
+  });
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    s.bv[i] = nB[i];
+    s.bw[i] = nB[3 + i];
+    s.bp[i] += dt * s.bv[i];
+  }
+  {
+    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
+    float ang = norm3(wv);
+    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    float sh, dw;
+    sincos_fast(0.5f * ang * dt, &sh, &dw);
+    f3 ax;
+    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
+    else ax = (sh / ang) * wv;
+    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
+    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+    s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
+  }
+  STAMP(6)
+  return nc;
+}
+
+// ------------------------------------------------------------------ calc_state (pack)
+// Part COMs and joint states of all branches meet in the env's LDS staging area; every
+// lane of the quad then runs the (numpy-exact, float64) pack on identical inputs.
+template <class R, int ES>
+PBG_DEV void team_gather(const TState<R>& s, const Lane& L, const TRows<R, ES>& rw, bool has_floor, PackIn<R>& in) {
+  using T = Team<R>;
+  constexpr int NL = R::NL, NJ = R::NJ, NDB = T::NDB, NLB = T::NLB;
+  const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+  TKin<R> k;
+  team_fk<R>(s, L, Rb, k);
+  PBG_QUAD_SYNC  // staging may still be read by the previous pack
+#pragma unroll
+  for (int i = 0; i < NLB; i++) {
+    rw.stage(L.k * NLB + i) = k.c[i].x;
+    rw.stage(NL + L.k * NLB + i) = k.c[i].y;
+  }
+#pragma unroll
+  for (int j = 0; j < NDB; j++) {
+    rw.stage(2 * NL + L.k * NDB + j) = s.q[j];
+    rw.stage(2 * NL + NJ + L.k * NDB + j) = s.qd[j];
+  }
+  PBG_QUAD_SYNC
+  int np = 0;
+#pragma unroll
+  for (int p = 0; p < R::NP; p++) {
+    const int l = R::part_link[p];
+    in.part_x[np] = l < 0 ? (double)s.bp[0] : (double)rw.stage(l);
+    in.part_y[np] = l < 0 ? (double)s.bp[1] : (double)rw.stage(NL + l);
+    np++;
+  }
+  if (R::floor && has_floor) { in.part_x[np] = 0.0; in.part_y[np] = 0.0; np++; }
+  in.n_parts = np;
+  m3_to_quat_d(Rb, in.quat);
+#pragma unroll
+  for (int i = 0; i < 3; i++) { in.pos[i] = s.bp[i]; in.vel[i] = s.bv[i]; }
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) {
+    in.jq[i] = rw.stage(2 * NL + R::obs_dof[i]);
+    in.jqd[i] = rw.stage(2 * NL + NJ + R::obs_dof[i]);
+  }
+}
+
+// snapshot + Philox reset noise (pbg_step.hip reset_env); returns the reset pack
+template <class R, int ES>
+PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, const TRows<R, ES>& rw, float* obs,
+                        bool& has_floor, double& pot, float& z0) {
+  using T = Team<R>;
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bp[i] = (float)R::base_pos[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.bq[i] = (float)R::base_quat[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) { s.bv[i] = 0.f; s.bw[i] = 0.f; }
+  const uint32_t epi = B.episode[e];
+  const uint32_t gid = (uint32_t)(B.env_offset + e);
+  float noise[R::NR > 0 ? R::NR : 1];
+#pragma unroll
+  for (int blk = 0; blk < (R::NR + 3) / 4; blk++) {
+    u4 ctr = {gid, epi, (uint32_t)blk, 0x5EEDu};
+    const u4 rnd = philox4x32_10(ctr, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
+    const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+      if (4 * blk + t < R::NR) noise[4 * blk + t] = fmaf(0.2f, u01(rr[t]), -0.1f);
+  }
+  static_for<0, T::NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    const int r = pki<T::RST, j>(L);
+    float q = 0.f;
+#pragma unroll
+    for (int t = 0; t < R::NR; t++) q = r == t ? noise[t] : q;
+    s.q[j] = q;
+    s.qd[j] = 0.f;
+  });
+  PackIn<R> in;
+  team_gather<R, ES>(s, L, rw, has_floor, in);
+#pragma unroll
+  for (int f = 0; f < R::NF; f++) in.feet_prev[f] = 0.f;
+  in.feet_new = 0;
+  in.potential_old = 0.0;
+  in.initial_z = R::initial_z_fixed;
+  PackOut po;
+  walker_pack<R>(in, nullptr, obs, po);
+  pot = po.potential;
+  z0 = (float)po.initial_z;
+  has_floor = true;
+  if (L.k == 0) B.episode[e] = epi + 1;
+}
+
+template <class R, int ES>
+__global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int lds_rows) {
+  using T = Team<R>;
+  constexpr int NDB = T::NDB, SB = PBG_BASE_WORDS;
+  extern __shared__ float lds_dyn[];
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = tid >> 2;
+  if (e >= B.n) return;
+  const Lane L = make_lane(tid & 3);
+  const int kb = L.k;
+  STAMP_DECL
+  TState<R> s;
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bp[i] = B.st[(size_t)i * B.n + e];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.bq[i] = B.st[(size_t)(3 + i) * B.n + e];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bv[i] = B.st[(size_t)(7 + i) * B.n + e];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.bw[i] = B.st[(size_t)(10 + i) * B.n + e];
+#pragma unroll
+  for (int j = 0; j < NDB; j++) {
+    s.q[j] = B.st[(size_t)(SB + kb * NDB + j) * B.n + e];
+    s.qd[j] = B.st[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e];
+  }
+  float act[R::NA];
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
+  // apply_action (robot_locomotors.py:26-29): this branch's motors
+  float tau[NDB];
+  static_for<0, NDB>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    const int ai = pki<T::ACTI, j>(L);
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < R::NA; i++) a = ai == i ? act[i] : a;
+    tau[j] = ai < 0 ? 0.f : (float)((double)pk<T::GAIN, j>(L) * (double)fminf(fmaxf(a, -1.f), 1.f));
+  });
+  TRows<R, ES> rw;
+  rw.lds = (lds_float*)lds_dyn + (threadIdx.x >> 2);
+  rw.gbl = scratch + e;
+  rw.n = B.n;
+  rw.cap = lds_rows;
+  uint32_t slot_bits = 0, base_bits = 0;
+  int nc = 0;
+  STAMP(7)
+  for (int sub = 0; sub < R::substeps; sub++) nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw SUB_STAMP_PASS);
+  if (io.ncontact && kb == 0) io.ncontact[e] = nc;
+  // feet contact flags of the last sub-step: this branch's feet, OR-ed over the quad
+  uint32_t fb = 0;
+  static_for<0, T::NSB>([&](auto sl_c) {
+    constexpr int sl = decltype(sl_c)::value;
+    constexpr int li = R::slot_link[T::NS0 + sl];
+    const int f = pki<T::FOOT, li>(L);
+    if (f >= 0 && ((slot_bits >> sl) & 1u)) fb |= 1u << f;
+  });
+  const uint32_t fnew = (uint32_t)quad_sum_i((int)fb);  // disjoint bits: sum == or
+  const int el = B.elapsed[e] + 1;
+  uint32_t flags = B.flags[e];
+  float obs[R::OBS];
+  PackOut po;
+  {
+    PackIn<R> in;
+    team_gather<R, ES>(s, L, rw, flags & 1u, in);
+#pragma unroll
+    for (int f = 0; f < R::NF; f++) in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
+    in.feet_new = fnew;
+    in.potential_old = B.pot[e];
+    in.initial_z = B.z0[e];
+    walker_pack<R>(in, act, obs, po);
+    flags = (flags & 0xFFu) | (po.feet_out << 8);
+  }
+  STAMP(8)
+  const bool term = po.done;
+  const bool trunc = el >= R::max_episode_steps;
+  if (kb == 0) {
+    io.rew[e] = (float)po.reward;
+    if (io.rew64) io.rew64[e] = po.reward;
+    io.done[e] = term || trunc;
+    if (io.trunc) io.trunc[e] = trunc && !term;
+  }
+  if (io.autoreset && (term || trunc)) {
+    if (io.term_obs && kb == 0) {
+#pragma unroll
+      for (int i = 0; i < R::OBS; i++) io.term_obs[(size_t)e * R::OBS + i] = obs[i];
+    }
+    bool has_floor = flags & 1u;
+    double pot;
+    float z0;
+    team_reset<R, ES>(B, e, L, s, rw, obs, has_floor, pot, z0);
+    if (kb == 0) {
+      B.pot[e] = pot;
+      B.z0[e] = z0;
+      B.elapsed[e] = 0;
+      B.flags[e] = has_floor ? 1u : 0u;
+    }
+  } else if (kb == 0) {
+    B.pot[e] = po.potential;
+    B.elapsed[e] = el;
+    B.flags[e] = flags;
+  }
+  if (kb == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) B.st[(size_t)i * B.n + e] = s.bp[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) B.st[(size_t)(3 + i) * B.n + e] = s.bq[i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) B.st[(size_t)(7 + i) * B.n + e] = s.bv[i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) B.st[(size_t)(10 + i) * B.n + e] = s.bw[i];
+#pragma unroll
+    for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+  }
+#pragma unroll
+  for (int j = 0; j < NDB; j++) {
+    B.st[(size_t)(SB + kb * NDB + j) * B.n + e] = s.q[j];
+    B.st[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e] = s.qd[j];
+  }
+  STAMP(9)
+  STAMP_FLUSH
+}
+
+}  // namespace pbg
