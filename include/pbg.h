@@ -48,6 +48,7 @@ typedef struct {
   int max_episode_steps; /* gym TimeLimit (envs/__init__.py) */
   int reset_dofs;        /* joints randomised by reset (robot_locomotors.py:18-19) */
   int floating;
+  int lanes_per_env;     /* step kernel geometry: 1 (lane per env) or 4 (quad per env) */
 } pbg_info_t;
 
 typedef struct {

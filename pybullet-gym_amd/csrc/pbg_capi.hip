@@ -168,6 +168,7 @@ void pbg_destroy(pbg_handle* h) {
 int pbg_info(const pbg_handle* h, pbg_info_t* out) {
   if (!h || !out) return fail(PBG_E_ARG, "pbg_info: NULL argument%s%ld");
   *out = h->info;
+  out->lanes_per_env = h->geo.team;
   return PBG_OK;
 }
 

@@ -904,22 +904,27 @@ PBG_DEV double np_sum_f64(const double* a, int n) {
   for (; i < n; i++) res += a[i];
   return 0.0 + res;
 }
-PBG_DEV float np_sum_f32(const float* a, int n) {
-  if (n < 8) {
-    float res = 0.0f;
-    for (int i = 0; i < n; i++) res += a[i];
-    return 0.0f + res;
+// The same sums for a compile-time length (register-resident operands, no scratch).
+template <int N, class F>
+PBG_DEV F np_sum_n(const F* a) {
+  if constexpr (N < 8) {
+    F res = F(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) res += a[i];
+    return F(0) + res;
+  } else {
+    F r[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+#pragma unroll
+    for (int i = 8; i < N - (N % 8); i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    F res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int i = N - (N % 8); i < N; i++) res += a[i];
+    return F(0) + res;
   }
-  float r[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) r[j] = a[j];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8)
-#pragma unroll
-    for (int j = 0; j < 8; j++) r[j] += a[i + j];
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; i++) res += a[i];
-  return 0.0f + res;
 }
 PBG_DEV float clip5(float v) { return v < -5.0f ? -5.0f : (v > 5.0f ? 5.0f : v); }
 
@@ -941,7 +946,8 @@ struct PackOut {
 };
 
 // robot_locomotors.py:31-64 calc_state + gym_locomotion_envs.py:59-114 reward/done.
-template <class R>
+// GEN: any part count (golden-vector pack_kernel); otherwise the step's NP or NP + 1 parts.
+template <class R, bool GEN = false>
 PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, PackOut& out) {
   float j[2 * (R::NO > 0 ? R::NO : 1)];
 #pragma unroll
@@ -959,8 +965,17 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   int at_limit = 0;
 #pragma unroll
   for (int i = 0; i < R::NO; i++) at_limit += fabsf(j[2 * i]) > PBG_JOINT_AT_LIMIT;
-  const double bx = np_sum_f64(in.part_x, in.n_parts) / (double)in.n_parts;
-  const double by = np_sum_f64(in.part_y, in.n_parts) / (double)in.n_parts;
+  double bx, by;
+  if constexpr (GEN) {
+    bx = np_sum_f64(in.part_x, in.n_parts) / (double)in.n_parts;
+    by = np_sum_f64(in.part_y, in.n_parts) / (double)in.n_parts;
+  } else if (in.n_parts == R::NP + 1) {
+    bx = np_sum_n<R::NP + 1>(in.part_x) / (double)(R::NP + 1);
+    by = np_sum_n<R::NP + 1>(in.part_y) / (double)(R::NP + 1);
+  } else {
+    bx = np_sum_n<R::NP>(in.part_x) / (double)R::NP;
+    by = np_sum_n<R::NP>(in.part_y) / (double)R::NP;
+  }
   const double bz = in.pos[2];
   const double* q = in.quat;
   const double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
@@ -1015,10 +1030,10 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   float tmp[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) tmp[i] = fabsf(act[i] * j[2 * i + 1]);
-  const float mean_e = np_sum_f32(tmp, R::NA) / (float)R::NA;
+  const float mean_e = np_sum_n<R::NA>(tmp) / (float)R::NA;
 #pragma unroll
   for (int i = 0; i < R::NA; i++) tmp[i] = act[i] * act[i];
-  const float mean_s = np_sum_f32(tmp, R::NA) / (float)R::NA;
+  const float mean_s = np_sum_n<R::NA>(tmp) / (float)R::NA;
   double elec = R::electricity_cost * (double)mean_e;
   elec += R::stall_torque_cost * (double)mean_s;
   const double jal = R::joints_at_limit_cost * (double)at_limit;
@@ -1306,7 +1321,7 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
     in.feet_new = fn;
     in.potential_old = r[o_pot];
     in.initial_z = r[o_pot + 1];
-    walker_pack<R>(in, is_step ? act : nullptr, obs, po);
+    walker_pack<R, true>(in, is_step ? act : nullptr, obs, po);
   }
   if (!is_step) { po.reward = 0.0; po.done = false; }
 #pragma unroll

@@ -334,42 +334,58 @@ struct TRows {
     p[(NDB + 7) * st] = target;
     p[(NDB + 8) * st] = 0.f;
   }
+  // one row in registers (loaded ahead of its update: PGS software pipelining)
+  struct Row {
+    float yb[NDB], yB[6], meff, tgt, lam;
+  };
   template <class P>
-  static PBG_DEV void solve_at(P p, size_t st, float* ub, float* uB, bool mine, float lo, float hi) {
-    float yb[NDB], yB[6];
+  static PBG_DEV void load_at(P p, size_t st, Row& r) {
 #pragma unroll
-    for (int i = 0; i < NDB; i++) yb[i] = p[i * st];
+    for (int i = 0; i < NDB; i++) r.yb[i] = p[i * st];
 #pragma unroll
-    for (int g = 0; g < 6; g++) yB[g] = p[(NDB + g) * st];
-    const float meff = p[(NDB + 6) * st], tgt = p[(NDB + 7) * st], lam0 = p[(NDB + 8) * st];
+    for (int g = 0; g < 6; g++) r.yB[g] = p[(NDB + g) * st];
+    r.meff = p[(NDB + 6) * st];
+    r.tgt = p[(NDB + 7) * st];
+    r.lam = p[(NDB + 8) * st];
+  }
+  // LDS: every row of the wave is resident (the common case, no workspace branches)
+  template <bool LDS>
+  PBG_DEV void load(int r, Row& row) const {
+    if (LDS || r < cap) load_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, row);
+    else load_at(gbl + (size_t)r * W * n, (size_t)n, row);
+  }
+  template <bool LDS>
+  PBG_DEV void set_lam(int r, float v) const {
+    if (LDS || r < cap) lds[(size_t)(HEAD + r * W + NDB + 8) * ES] = v;
+    else gbl[((size_t)r * W + NDB + 8) * n] = v;
+  }
+  template <bool LDS>
+  PBG_DEV float get_lam(int r) const {
+    if (LDS || r < cap) return lds[(size_t)(HEAD + r * W + NDB + 8) * ES];
+    return gbl[((size_t)r * W + NDB + 8) * n];
+  }
+  // projected Gauss-Seidel update of a loaded row; returns the new impulse
+  static PBG_DEV float update(const Row& r, float* ub, float* uB, bool mine, float lo, float hi) {
     float pb = 0.f;
 #pragma unroll
-    for (int i = 0; i < NDB; i++) pb += yb[i] * ub[i];
+    for (int i = 0; i < NDB; i++) pb += r.yb[i] * ub[i];
     const float yub = quad_sum(mine ? pb : 0.f);
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int g = 0; g < 6; g += 2) { a0 += yB[g] * uB[g]; a1 += yB[g + 1] * uB[g + 1]; }
+    for (int g = 0; g < 6; g += 2) { a0 += r.yB[g] * uB[g]; a1 += r.yB[g + 1] * uB[g + 1]; }
     const float yu = yub + (a0 + a1);
-    const float nl = fminf(fmaxf(lam0 + meff * (tgt - yu), lo), hi);
-    const float dl = nl - lam0;
-    p[(NDB + 8) * st] = nl;
+    const float nl = fminf(fmaxf(r.lam + r.meff * (r.tgt - yu), lo), hi);
+    const float dl = nl - r.lam;
 #pragma unroll
-    for (int g = 0; g < 6; g++) uB[g] += yB[g] * dl;
+    for (int g = 0; g < 6; g++) uB[g] += r.yB[g] * dl;
     const float dlb = mine ? dl : 0.f;
 #pragma unroll
-    for (int i = 0; i < NDB; i++) ub[i] += yb[i] * dlb;
+    for (int i = 0; i < NDB; i++) ub[i] += r.yb[i] * dlb;
+    return nl;
   }
   PBG_DEV void put(int r, const float* yb, const float* yB, float meff, float target) const {
     if (r < cap) put_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, yb, yB, meff, target);
     else put_at(gbl + (size_t)r * W * n, (size_t)n, yb, yB, meff, target);
-  }
-  PBG_DEV float lam(int r) const {
-    if (r < cap) return lds[(size_t)(HEAD + r * W + NDB + 8) * ES];
-    return gbl[((size_t)r * W + NDB + 8) * n];
-  }
-  PBG_DEV void solve(int r, float* ub, float* uB, bool mine, float lo, float hi) const {
-    if (r < cap) solve_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, ub, uB, mine, lo, hi);
-    else solve_at(gbl + (size_t)r * W * n, (size_t)n, ub, uB, mine, lo, hi);
   }
 };
 
@@ -381,6 +397,42 @@ PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
     static_for<0, g>([&](auto h_c) { v -= Lbb[g][decltype(h_c)::value] * t[decltype(h_c)::value]; });
     t[g] = v * Ldb[g];
   });
+}
+
+// One PGS sweep over the contact rows in Bullet's order: all normals, then the two
+// friction rows of each contact whose normal impulse is positive, box-clamped at mu*lambda_n.
+// The next normal row is loaded before the current one is updated: two register buffers
+// alternate, so LDS latency overlaps the update arithmetic.
+template <bool LDS, class RW>
+PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
+  using Row = typename RW::Row;
+  const float kf = (float)kb;
+  if (nc <= 0) return;
+  {
+    Row A, B;
+    rw.template load<LDS>(0, A);
+    float oA = rw.own(0), oB = 0.f;
+    int c = 0;
+    while (true) {
+      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), B); oB = rw.own(c + 1); }
+      rw.template set_lam<LDS>(3 * c, RW::update(A, ub, uB, oA == kf, 0.f, 3.0e38f));
+      if (++c >= nc) break;
+      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), A); oA = rw.own(c + 1); }
+      rw.template set_lam<LDS>(3 * c, RW::update(B, ub, uB, oB == kf, 0.f, 3.0e38f));
+      if (++c >= nc) break;
+    }
+  }
+  for (int c = 0; c < nc; c++) {
+    const float ln = rw.template get_lam<LDS>(3 * c);
+    if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
+    Row r1, r2;
+    rw.template load<LDS>(3 * c + 1, r1);
+    rw.template load<LDS>(3 * c + 2, r2);
+    const float lim = rw.mu(c) * ln;
+    const bool mine = rw.own(c) == kf;
+    rw.template set_lam<LDS>(3 * c + 1, RW::update(r1, ub, uB, mine, -lim, lim));
+    rw.template set_lam<LDS>(3 * c + 2, RW::update(r2, ub, uB, mine, -lim, lim));
+  }
 }
 
 // ------------------------------------------------------------------ one physics sub-step
@@ -873,6 +925,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   PBG_QUAD_SYNC
+  // wave-uniform: do all rows of the wave's envs live in LDS?
+  const bool all_lds = __builtin_amdgcn_ballot_w64(3 * nc > rw.cap) == 0;
 
   STAMP(4)
   // --- PGS, 5 sweeps, Bullet order: joint limits (dof order), normals, frictions ------
@@ -906,15 +960,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         for (int a = 0; a < NDB; a++) ub[a] += Lyb[li][a] * dlb;
       });
     });
-    for (int c = 0; c < nc; c++) rw.solve(3 * c, ub, uB, (int)rw.own(c) == kb, 0.f, 3.0e38f);
-    for (int c = 0; c < nc; c++) {
-      const float ln = rw.lam(3 * c);
-      if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
-      const float lim = rw.mu(c) * ln;
-      const bool mine = (int)rw.own(c) == kb;
-      rw.solve(3 * c + 1, ub, uB, mine, -lim, lim);
-      rw.solve(3 * c + 2, ub, uB, mine, -lim, lim);
-    }
+    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uB);
+    else contact_sweep<false>(rw, nc, kb, ub, uB);
   }
 
   STAMP(5)

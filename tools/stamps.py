@@ -23,7 +23,8 @@ for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] o
     for i in range(steps): env.step(acts[10 + i])
     torch.cuda.synchronize()
     L.pbg_debug_stamps(rid, buf)
-    waves = (n + env.block - 1) // env.block if hasattr(env, 'block') else (n + 63) // 64
+    lanes = n * max(1, env.info.lanes_per_env)
+    waves = (lanes + 63) // 64
     tot = sum(buf[i] for i in range(10))
     print(f"{env_id} n={n}: cycles per wave per env-step = {tot / waves / steps:.0f}")
     for i in range(10):
