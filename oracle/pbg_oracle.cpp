@@ -89,10 +89,10 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[5] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[6] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                         view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
-                        view<pbg_models::Humanoid>()};
-  if (robot < 0 || robot > 4) return nullptr;
+                        view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>()};
+  if (robot < 0 || robot > 5) return nullptr;
   return &views[robot];
 }
 

@@ -207,7 +207,7 @@ def _arr2(name, ctype, rows, w):
 
 def emit_struct(t: Dict) -> str:
     cls = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah",
-           "ant": "Ant", "humanoid": "Humanoid"}[t["key"]]
+           "ant": "Ant", "humanoid": "Humanoid", "walker2d": "Walker2D"}[t["key"]]
     L = [f"// {t['env_id']}: generated by pybulletgym_amd.codegen from the reference MJCF asset",
          f"struct {cls} {{",
          f"  static constexpr int robot_id = {ROBOT_IDS[t['key']]};",
@@ -262,7 +262,7 @@ def emit_struct(t: Dict) -> str:
     return "\n".join(L)
 
 
-ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4}
+ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -25,12 +25,13 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[5][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[6][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
-                                  {"HumanoidPyBulletEnv-v0", "humanoid"}};
-  for (int i = 0; i < 5; i++)
+                                  {"HumanoidPyBulletEnv-v0", "humanoid"},
+                                  {"Walker2DPyBulletEnv-v0", "walker2d"}};
+  for (int i = 0; i < 6; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -62,9 +63,9 @@ pbg_info_t info_of(int rid) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
 
 const Ops* ops(int rid) {
-  static const Ops table[5] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
-                               PBG_OPS(Humanoid, 4)};
-  return (rid >= 0 && rid < 5) ? &table[rid] : nullptr;
+  static const Ops table[6] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+                               PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5)};
+  return (rid >= 0 && rid < 6) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {
@@ -226,6 +227,7 @@ int pbg_debug_stamps(int rid, unsigned long long* host_out) {
     case 2: return pbg::debug_stamps_HalfCheetah(host_out);
     case 3: return pbg::debug_stamps_Ant(host_out);
     case 4: return pbg::debug_stamps_Humanoid(host_out);
+    case 5: return pbg::debug_stamps_Walker2D(host_out);
   }
   return PBG_E_ENV;
 }

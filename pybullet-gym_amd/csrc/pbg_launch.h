@@ -33,4 +33,5 @@ PBG_DECLARE_ROBOT(Hopper)
 PBG_DECLARE_ROBOT(HalfCheetah)
 PBG_DECLARE_ROBOT(Ant)
 PBG_DECLARE_ROBOT(Humanoid)
+PBG_DECLARE_ROBOT(Walker2D)
 }  // namespace pbg

@@ -103,6 +103,7 @@ def _robot_class(key, base_cls):
 
 
 Hopper = _robot_class("hopper", "Hopper")                    # robot_locomotors.py:82-90
+Walker2D = _robot_class("walker2d", "Walker2D")              # :93-106
 HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
 Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
@@ -122,6 +123,7 @@ def _alive_bonus_humanoid(self, z, pitch):
 
 
 Hopper.alive_bonus = _alive_bonus_hopper
+Walker2D.alive_bonus = _alive_bonus_hopper  # robot_locomotors.py:100-101 (same rule as Hopper)
 Ant.alive_bonus = _alive_bonus_ant
 Humanoid.alive_bonus = _alive_bonus_humanoid
 
@@ -229,6 +231,14 @@ class HopperBulletEnv(WalkerBaseBulletEnv):
         WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
 
 
+class Walker2DBulletEnv(WalkerBaseBulletEnv):
+    env_id = "Walker2DPyBulletEnv-v0"  # gym_locomotion_envs.py:128-131
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = Walker2D()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+
+
 class HalfCheetahBulletEnv(WalkerBaseBulletEnv):
     env_id = "HalfCheetahPyBulletEnv-v0"
 
@@ -277,6 +287,7 @@ class InvertedPendulumBulletEnv(BaseBulletEnv):
 ENV_CLASSES = {
     "InvertedPendulumPyBulletEnv-v0": InvertedPendulumBulletEnv,
     "HopperPyBulletEnv-v0": HopperBulletEnv,
+    "Walker2DPyBulletEnv-v0": Walker2DBulletEnv,
     "HalfCheetahPyBulletEnv-v0": HalfCheetahBulletEnv,
     "AntPyBulletEnv-v0": AntBulletEnv,
     "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
@@ -284,6 +295,7 @@ ENV_CLASSES = {
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
 REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
+                    "Walker2DPyBulletEnv-v0": 2500.0,
                     "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
 
 

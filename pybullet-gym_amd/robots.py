@@ -72,6 +72,11 @@ _add(RobotSpec("AntPyBulletEnv-v0", "ant", "ant.xml", "torso", action_dim=8, obs
                kind=KIND_WALKER, power=2.5,
                foot_list=["front_left_foot", "front_right_foot", "left_back_foot", "right_back_foot"],
                alive=ALIVE_ANT))
+# Walker2D: robot_locomotors.py:93-106 (foot power_coef 30 set in robot_specific_reset),
+# gym_locomotion_envs.py:128-131, envs/__init__.py:53-58
+_add(RobotSpec("Walker2DPyBulletEnv-v0", "walker2d", "walker2d.xml", "torso", action_dim=6, obs_dim=22,
+               kind=KIND_WALKER, power=0.40, foot_list=["foot", "foot_left"], alive=ALIVE_HOPPER,
+               power_coef={"foot_joint": 30.0, "foot_left_joint": 30.0}))
 # Humanoid: robot_locomotors.py:141-192, gym_locomotion_envs.py:146-151, envs/__init__.py:80-84
 _add(RobotSpec("HumanoidPyBulletEnv-v0", "humanoid", "humanoid_symmetric.xml", "torso", action_dim=17,
                obs_dim=44, kind=KIND_WALKER, power=0.41, foot_list=["right_foot", "left_foot"],

@@ -43,6 +43,7 @@ ROBOTS = {
     "halfcheetah": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HalfCheetahBulletEnv"),
     "ant": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "AntBulletEnv"),
     "humanoid": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidBulletEnv"),
+    "walker2d": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "Walker2DBulletEnv"),
 }
 
 

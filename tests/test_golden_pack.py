@@ -8,7 +8,7 @@ import pytest
 import oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-WALKERS = ["hopper", "halfcheetah", "ant", "humanoid"]
+WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d"]
 
 
 def load(key):

@@ -25,7 +25,7 @@ from pybulletgym_amd.vec_env import VecEnv, pack, pack_record_sizes
 pytestmark = pytest.mark.gpu
 
 ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
-        "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"]
+        "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 

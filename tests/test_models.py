@@ -69,3 +69,13 @@ def test_humanoid_dummies_and_pairs():
                 out.append(i)
             return out
         assert a not in anc(b) and b not in anc(a), (names[a], names[b])
+
+
+def test_walker2d_topology_and_gains():
+    """robot_locomotors.py:93-106: power 0.40, foot joints power_coef 30 (robot_specific_reset)."""
+    t = codegen.load_tables("walker2d")
+    assert t["floating"] == 0 and t["NJ"] == 9 and t["NA"] == 6 and t["OBS"] == 22
+    assert t["act_joint_names"] == ["thigh_joint", "leg_joint", "foot_joint",
+                                    "thigh_left_joint", "leg_left_joint", "foot_left_joint"]
+    assert t["act_gain"] == pytest.approx([40.0, 40.0, 12.0, 40.0, 40.0, 12.0])
+    assert [t["link_name"][l] for l in t["foot_link"]] == ["foot", "foot_left"]

@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 
-KEYS = ["hopper", "halfcheetah", "ant", "humanoid"]
+KEYS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d"]
 MODELS = os.path.join(os.path.dirname(__file__), "..", "pybullet-gym_amd", "models")
 
 
