@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--gather", action="store_true", help="also time the RCCL obs all-gather (separately)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
     args = ap.parse_args()
 
     import torch
@@ -113,22 +114,47 @@ def main():
     for i in range(args.warmup):
         env.step(acts[i % pool])
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # timed region: the K steps as HIP-graph replays of G captured steps (G divides K)
+    G = 1
+    if not args.no_graph:
+        G = max(d for d in range(1, min(64, args.steps) + 1) if args.steps % d == 0)
+        graph = env.capture([acts[j % pool] for j in range(G)])
+    # per-launch kernel time (roofline.kernel_ms), HIP events on the launch stream: around
+    # graph replays (back-to-back kernels) or, with --no-graph, around single launches
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n_ev = 0
+    if args.no_graph:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(100)]
+        for i in range(100):
+            ev[i][0].record(stream)
+            env.step(acts[(args.warmup + i) % pool])
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / 100
+    else:
+        reps = max(1, 200 // G)
+        e0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        kernel_ms = e0.elapsed_time(e1) / (reps * G)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        env.step(acts[(args.warmup + i) % pool])
-        ev[i][1].record(stream)
+    if args.no_graph:
+        for i in range(args.steps):
+            env.step(acts[(args.warmup + i) % pool])
+    else:
+        for _ in range(args.steps // G):
+            graph.replay()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -168,10 +194,13 @@ def main():
             "data": "synthetic: U(-1,1) float32 actions pre-generated in HBM; robot compiled from the reference MJCF",
             "config": {"workload": f"{args.env} random-action rollout, auto-reset (TimeLimit 1000)",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps": env.info.substeps,
-                       "solver_iterations": 5, "parallelism": f"env-sharded x{world}, no per-step collective"},
+                       "solver_iterations": 5, "parallelism": f"env-sharded x{world}, no per-step collective",
+                       "launch": "host loop" if args.no_graph else f"hipGraph replay of {G} captured steps",
+                       "lanes_per_env": env.info.lanes_per_env},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"pbg::step_kernel<{args.env}>", "kernel_ms": kernel_ms,
+                         "kernel": ("pbg::team_step_kernel" if env.info.lanes_per_env == 4 else "pbg::step_kernel")
+                                   + f"<{args.env}>", "kernel_ms": kernel_ms,
                          "alg_bytes_per_env_step": alg},
             "obs_finite": finite,
         }

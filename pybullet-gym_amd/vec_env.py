@@ -115,6 +115,22 @@ class VecEnv:
         _native.check(_native.lib().pbg_step_ex(self._h, ctypes.byref(io), _stream(self.device)), "pbg_step")
         return StepResult(self.obs, self.reward, self.done, self.truncated, self.terminal_obs)
 
+    def capture(self, actions) -> "torch.cuda.CUDAGraph":
+        """Record ``len(actions)`` consecutive steps (one action batch each, device tensors
+        that stay alive) into a HIP graph; ``graph.replay()`` then runs them with a single
+        launch from the host.  The step has no host synchronisation or allocation, so it
+        captures as is; outputs land in the usual ``obs``/``reward``/``done`` buffers."""
+        self.step(actions[0])  # first-step lazy buffers outside the capture
+        dev = self.device
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for a in actions:
+                self.step(a)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        return g
+
     # ---------------------------------------------------------------- state records
     def get_state(self):
         phys = torch.zeros((self.num_envs, self.info.state_words), dtype=torch.float64, device=self.device)
