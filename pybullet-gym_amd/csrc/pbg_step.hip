@@ -56,6 +56,10 @@ struct BoolTab {
   bool v[A][B];
 };
 template <int A, int B>
+struct FloatTab {
+  float v[A][B];
+};
+template <int A, int B>
 struct IntTab {
   int v[A][B];
 };
@@ -152,6 +156,24 @@ struct Dims {
     for (int i = 0; i < 6; i++) I.v[i] = b == 0 ? R::base_inertia[i] : R::link_inertia[b > 0 ? b - 1 : 0][i];
     return I;
   }
+  // squared (2 x bounding distance) per self-collision pair, for the broad phase
+  static constexpr FloatTab<(R::NPAIR > 0 ? R::NPAIR : 1), 1> make_pair_bound() {
+    FloatTab<(R::NPAIR > 0 ? R::NPAIR : 1), 1> t{};
+    for (int pp = 0; pp < R::NPAIR; pp++) {
+      const int ga = R::pair_ga[pp], gb = R::pair_gb[pp];
+      double ha = 0, hb = 0;
+      for (int c = 0; c < 3; c++) {
+        ha += (R::geom_p1[ga][c] - R::geom_p0[ga][c]) * (R::geom_p1[ga][c] - R::geom_p0[ga][c]);
+        hb += (R::geom_p1[gb][c] - R::geom_p0[gb][c]) * (R::geom_p1[gb][c] - R::geom_p0[gb][c]);
+      }
+      // sqrt by Newton (constexpr); generous margin keeps the cull conservative in float32
+      auto csqrt = [](double x) { double r = x > 1 ? x : 1; for (int i = 0; i < 60; i++) r = 0.5 * (r + x / r); return x > 0 ? r : 0.0; };
+      const double bound = 0.5 * csqrt(ha) + 0.5 * csqrt(hb) + R::geom_r[ga] + R::geom_r[gb] + PBG_CONTACT_THRESHOLD + 0.01;
+      t.v[pp][0] = (float)(4.0 * bound * bound);
+    }
+    return t;
+  }
+  static constexpr FloatTab<(R::NPAIR > 0 ? R::NPAIR : 1), 1> PAIR_BOUND2 = make_pair_bound();
   static constexpr bool is_owner(int b) { return b == 0 ? R::floating : R::link_dof[b - 1] >= 0; }
   // every body with mass comes after the reference body in DFS order (O is set first)
   static constexpr bool ref_first() {
@@ -733,6 +755,10 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     for (int pp = 0; pp < R::NPAIR; pp++) {
       const int ga = R::pair_ga[pp], gb = R::pair_gb[pp];
       const f3 a0 = G0[ga], a1 = G1[ga], b0 = G0[gb], b1 = G1[gb];
+      // broad phase: capsules whose bounding spheres are beyond the contact threshold
+      // cannot touch (bound = half lengths + radii + threshold, compile-time per pair)
+      const f3 dc = (a0 + a1) - (b0 + b1);  // twice the centre distance
+      if (dot3(dc, dc) > D::PAIR_BOUND2.v[pp][0]) continue;
       const f3 d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
       const float aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
       float ss, tt;
@@ -1090,7 +1116,12 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
   if (R::floor && has_floor) { in.part_x[np] = 0.0; in.part_y[np] = 0.0; np++; }
   in.n_parts = np;
   constexpr int b = R::robot_body + 1;
-  m3_to_quat_d(k.Rm[b], in.quat);
+  if constexpr (b == 0) {  // getBasePositionAndOrientation: the state's own quaternion
+#pragma unroll
+    for (int i = 0; i < 4; i++) in.quat[i] = s.bq[i];
+  } else {
+    m3_to_quat_d(k.Rm[b], in.quat);
+  }
   in.pos[0] = k.c[b].x; in.pos[1] = k.c[b].y; in.pos[2] = k.c[b].z;
   // robot_body COM velocity
   f3 vel;
@@ -1308,7 +1339,8 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
   } else {
     PackIn<R> in;
     in.n_parts = (int)r[o_np];
-    for (int p = 0; p < in.n_parts && p < R::NP + 1; p++) { in.part_x[p] = r[3 * p]; in.part_y[p] = r[3 * p + 1]; }
+#pragma unroll
+    for (int p = 0; p < R::NP + 1; p++) { in.part_x[p] = r[3 * p]; in.part_y[p] = r[3 * p + 1]; }
 #pragma unroll
     for (int i = 0; i < 4; i++) in.quat[i] = r[o_q + i];
 #pragma unroll
@@ -1321,7 +1353,9 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
     in.feet_new = fn;
     in.potential_old = r[o_pot];
     in.initial_z = r[o_pot + 1];
-    walker_pack<R, true>(in, is_step ? act : nullptr, obs, po);
+    // the step's part counts take the kernels' compile-time path (what this test pins)
+    if (in.n_parts == R::NP || in.n_parts == R::NP + 1) walker_pack<R>(in, is_step ? act : nullptr, obs, po);
+    else walker_pack<R, true>(in, is_step ? act : nullptr, obs, po);
   }
   if (!is_step) { po.reward = 0.0; po.done = false; }
 #pragma unroll

@@ -1047,7 +1047,8 @@ PBG_DEV void team_gather(const TState<R>& s, const Lane& L, const TRows<R, ES>& 
   }
   if (R::floor && has_floor) { in.part_x[np] = 0.0; in.part_y[np] = 0.0; np++; }
   in.n_parts = np;
-  m3_to_quat_d(Rb, in.quat);
+#pragma unroll
+  for (int i = 0; i < 4; i++) in.quat[i] = s.bq[i];
 #pragma unroll
   for (int i = 0; i < 3; i++) { in.pos[i] = s.bp[i]; in.vel[i] = s.bv[i]; }
 #pragma unroll
