@@ -66,7 +66,8 @@ typedef struct {
 /* gym.make(env_id) for n envs (envs/__init__.py:4-103 registry entries; the env's
  * physics client is created here instead of lazily in BaseBulletEnv._reset,
  * env_bases.py:46-56).  env_id: "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0",
- * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "InvertedPendulumPyBulletEnv-v0". */
+ * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "InvertedPendulumPyBulletEnv-v0",
+ * "Walker2DPyBulletEnv-v0". */
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out);
 /* BaseBulletEnv._close (env_bases.py:103-107) */
 void pbg_destroy(pbg_handle* h);
