@@ -126,10 +126,11 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
   const size_t n = (size_t)n_envs;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  // PBG_TEAM=0 selects the one-lane-per-env kernel for robots that have a quad variant
+  // PBG_TEAM=0 selects the one-lane-per-env kernel for every robot, PBG_TEAM=2 the gang
+  // kernel for every walker (Ant included); default: quad for Ant, gang for the others
   const char* team_env = getenv("PBG_TEAM");
-  const int allow_team = !(team_env && team_env[0] == '0');
-  int e = hip_check(o->plan(n_envs, cus, allow_team, &h->geo), "kernel attributes");
+  const int mode = (team_env && team_env[0] == '0') ? 0 : ((team_env && team_env[0] == '2') ? 2 : 1);
+  int e = hip_check(o->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
   // PBG_LDS_ROWS=k caps the LDS-resident contact rows (tests of the workspace path)
   const char* rows_env = getenv("PBG_LDS_ROWS");
   if (rows_env && atoi(rows_env) >= 0 && atoi(rows_env) < h->geo.lds_rows) h->geo.lds_rows = atoi(rows_env);

@@ -1,0 +1,596 @@
+// pbg_gang.hip -- gang-per-env step kernel: T = 16 lanes (one DPP row) per env, four
+// envs per wave.  Included by pbg_robot.hip after pbg_step.hip / pbg_team.hip; selected
+// by plan_* for the robots without a quad decomposition (Humanoid, Hopper, HalfCheetah,
+// Walker2D) when the env count leaves SIMDs idle in the lane kernel.
+//
+// Same physics, Bullet row order and numpy-exact pack as step_kernel (pbg_step.hip).
+// What changes is who does the work:
+//  * replicated -- every lane of the gang runs the unconstrained dynamics (dynamics():
+//    composites, mass matrix, Cholesky, u = L^T nu), integration and the pack on identical
+//    inputs, so the results are bitwise identical across the gang;
+//  * distributed -- collision candidates (floor slots, self-collision pairs), constraint
+//    rows (joint limits + 3 rows per contact: y = L^-1 J^T, m_eff, target) and the PGS
+//    vector work.  Candidates and rows are dealt round-robin to the lanes and run through
+//    ONE generic code path (runtime link / slot / pair index, model constants from a
+//    __constant__ table) instead of the lane kernel's fully unrolled per-slot code: the
+//    whole contact phase is a few hundred instructions per lane instead of tens of
+//    thousands, and the contact count per lane is nc / 16.
+//  * PGS keeps Bullet's sequential row order; the generalized velocity in Cholesky space
+//    u is sliced over the gang (lane t owns u[t], u[t+16], ...), each row is a slice dot
+//    product + a 16-lane DPP all-reduce (quad_perm, row_half_mirror, row_mirror: the same
+//    bits in every lane) + a replicated impulse update.
+// Contacts are compacted in candidate order with a wave ballot (rank = popcount of the
+// gang's lower lanes), which reproduces the lane kernel's contact order: floor slots in
+// slot order, then pairs in pair order.
+//
+// Why: at the BASELINE env counts (Humanoid 4,096 / GPU, Hopper and Walker2D 4,096,
+// HalfCheetah 8,192) the lane kernel runs 64-256 waves of 16-32 active lanes -- one SIMD
+// in four busy, three lanes in four idle, every instruction's latency exposed.  The gang
+// kernel runs n/4 full waves (1,024 at 4,096 envs: one per SIMD).
+//
+// Per-env LDS region (words), [gang-shared]:
+//   L (NNZ) | Ld (N) | u (YS) | sw (3N) | sv (3N) | body frames (12 NB) | limit pos (2 NLIM)
+//   | limit rows NLIM x (YS + 5) | contacts 0..cap-1 x PERC
+// contact c: descriptor (DW) | mu | 3 rows x (y (YS) | m_eff | target | lambda); contacts
+// at c >= cap live at the same offsets in the env's device workspace.
+namespace pbg {
+
+template <int CTRL>
+PBG_DEV float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// all-reduce over the T (4, 8 or 16) lanes of a DPP row segment; identical bits in every
+// lane (each step adds a value and its mirror image: a + b == b + a)
+template <int T>
+PBG_DEV float gang_sum(float x) {
+  x = x + dpp_f<0xB1>(x);  // quad_perm [1,0,3,2]
+  x = x + dpp_f<0x4E>(x);  // quad_perm [2,3,0,1]
+  if constexpr (T >= 8) x = x + dpp_f<0x141>(x);   // row_half_mirror
+  if constexpr (T >= 16) x = x + dpp_f<0x140>(x);  // row_mirror
+  return x;
+}
+PBG_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+// ------------------------------------------------------------------ constant tables
+template <class R>
+struct GangTab {
+  static constexpr int NS1 = R::NS > 0 ? R::NS : 1, NP1 = R::NPAIR > 0 ? R::NPAIR : 1;
+  static constexpr int NG1 = R::NG > 0 ? R::NG : 1, NB = R::NL + 1;
+  static constexpr int NL1 = Dims<R>::NLIM > 0 ? Dims<R>::NLIM : 1;
+  float slot[NS1][4];  // point (link frame) | radius
+  float slot_mu[NS1];
+  int slot_body[NS1];
+  float gp0[NG1][4];   // capsule end 0 | radius
+  float gp1[NG1][4];   // capsule end 1
+  int geom_body[NG1];
+  int pga[NP1], pgb[NP1];
+  float pmu[NP1], pbound2[NP1];
+  uint32_t chain[NB];  // joint dofs moving body b (0: the base)
+  int lim_g[NL1];      // generalized index of limit row li
+};
+template <class R>
+constexpr GangTab<R> make_gang_tab() {
+  using D = Dims<R>;
+  GangTab<R> t{};
+  for (int s = 0; s < R::NS; s++) {
+    for (int c = 0; c < 3; c++) t.slot[s][c] = (float)R::slot_point[s][c];
+    t.slot[s][3] = (float)R::slot_radius[s];
+    t.slot_mu[s] = (float)R::slot_mu[s];
+    t.slot_body[s] = R::slot_link[s] + 1;
+  }
+  for (int g = 0; g < R::NG; g++) {
+    for (int c = 0; c < 3; c++) { t.gp0[g][c] = (float)R::geom_p0[g][c]; t.gp1[g][c] = (float)R::geom_p1[g][c]; }
+    t.gp0[g][3] = (float)R::geom_r[g];
+    t.geom_body[g] = R::geom_link[g] + 1;
+  }
+  for (int p = 0; p < R::NPAIR; p++) {
+    t.pga[p] = R::pair_ga[p];
+    t.pgb[p] = R::pair_gb[p];
+    t.pmu[p] = (float)R::pair_mu[p];
+    t.pbound2[p] = D::PAIR_BOUND2.v[p][0];
+  }
+  t.chain[0] = 0;
+  for (int l = 0; l < R::NL; l++) t.chain[l + 1] = R::link_chain_mask[l];
+  for (int li = 0; li < D::NLIM; li++) t.lim_g[li] = D::gj(D::LIM.v[li][0]);
+  return t;
+}
+template <class R>
+__constant__ GangTab<R> g_gang_tab = make_gang_tab<R>();
+
+// ------------------------------------------------------------------ layout
+template <class R, int T>
+struct Gang {
+  using D = Dims<R>;
+  static constexpr int N = R::NDOF, NNZ = D::NNZ, NB = D::NB, NLIM = D::NLIM;
+  static constexpr int NSL = (N + T - 1) / T;  // u entries per lane
+  static constexpr int YS = NSL * T;           // padded row length
+  static constexpr int MAXC = R::NS + R::NPAIR;
+  static constexpr int DW = 16;                // descriptor: rA 3 | rB 3 | n 3 | dist | fA | fB | mA | mB | floor | pad
+  static constexpr int CRW = YS + 3;           // y | m_eff | target | lambda
+  static constexpr int LRW = YS + 5;           // y | m_eff | t_lo | t_hi | pad 2
+  static constexpr int PERC = DW + 1 + 3 * CRW;
+  static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_SW = O_U + YS, O_SV = O_SW + 3 * N;
+  static constexpr int O_FR = O_SV + 3 * N, O_LP = O_FR + 12 * NB, O_LR = O_LP + 2 * NLIM;
+  static constexpr int FIXED = O_LR + NLIM * LRW;
+  static constexpr int GWORDS = (MAXC > 0 ? MAXC : 1) * PERC;  // device workspace per env
+  static constexpr int ROUNDS_S = (R::NS + T - 1) / T;
+};
+
+// per-lane view of the env's LDS region and device workspace
+struct GangCtx {
+  lds_float* l;  // env LDS region
+  float* g;      // env device workspace
+  int cap;       // contacts resident in LDS
+  int t;         // lane in the gang
+  int le;        // gang in the wave
+};
+#define PBG_GANG_SYNC                                    \
+  {                                                      \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                     \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+  }
+
+// contact c, word w: LDS if resident, else the device workspace
+template <class R, int T>
+PBG_DEV void cput(const GangCtx& X, int c, int w, float v) {
+  using G = Gang<R, T>;
+  if (c < X.cap) X.l[G::FIXED + c * G::PERC + w] = v;
+  else X.g[(size_t)c * G::PERC + w] = v;
+}
+template <class R, int T>
+PBG_DEV float cget(const GangCtx& X, int c, int w) {
+  using G = Gang<R, T>;
+  if (c < X.cap) return X.l[G::FIXED + c * G::PERC + w];
+  return X.g[(size_t)c * G::PERC + w];
+}
+
+// one PGS update of contact row (c, dir) with u sliced over the gang: returns the new
+// impulse (same bits in every lane) and updates this lane's slice.
+template <class R, int T>
+PBG_DEV float gang_row(const GangCtx& X, int c, int dir, float* us, float lo, float hi, float* lam_out) {
+  using G = Gang<R, T>;
+  constexpr int NSL = G::NSL;
+  const int w0 = G::DW + 1 + dir * G::CRW;
+  float y[NSL], meff, tgt, lam;
+  if (c < X.cap) {
+    const lds_float* p = X.l + G::FIXED + c * G::PERC + w0;
+#pragma unroll
+    for (int m = 0; m < NSL; m++) y[m] = p[X.t + m * T];
+    meff = p[G::YS]; tgt = p[G::YS + 1]; lam = p[G::YS + 2];
+  } else {
+    const float* p = X.g + (size_t)c * G::PERC + w0;
+#pragma unroll
+    for (int m = 0; m < NSL; m++) y[m] = p[X.t + m * T];
+    meff = p[G::YS]; tgt = p[G::YS + 1]; lam = p[G::YS + 2];
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int m = 0; m < NSL; m++) part += y[m] * us[m];
+  const float yu = gang_sum<T>(part);
+  const float nl = fminf(fmaxf(lam + meff * (tgt - yu), lo), hi);
+  const float dl = nl - lam;
+#pragma unroll
+  for (int m = 0; m < NSL; m++) us[m] += y[m] * dl;
+  *lam_out = lam;
+  return nl;
+}
+
+template <class R, int T>
+PBG_DEV void set_row_lam(const GangCtx& X, int c, int dir, float v) {
+  using G = Gang<R, T>;
+  if (X.t == 0) cput<R, T>(X, c, G::DW + 1 + dir * G::CRW + G::YS + 2, v);
+}
+
+// ------------------------------------------------------------------ one physics sub-step
+template <class R, int T>
+PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits SUB_STAMP_ARGS) {
+  using D = Dims<R>;
+  using G = Gang<R, T>;
+  const GangTab<R>& TB = g_gang_tab<R>;
+  constexpr int N = R::NDOF, NB = D::NB, NLIM = D::NLIM, NSL = G::NSL, YS = G::YS;
+  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
+  const bool w0 = X.t == 0;  // the gang's writer for replicated values
+  f3 O;
+  // --- replicated: unconstrained dynamics, staged into the gang's LDS -------------------
+  {
+    float L[D::NNZ], Ld[N], nu[N], u[N];
+    dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
+    STAMP(3)
+    if (w0) {
+#pragma unroll
+      for (int i = 0; i < D::NNZ; i++) X.l[G::O_L + i] = L[i];
+#pragma unroll
+      for (int i = 0; i < N; i++) { X.l[G::O_LD + i] = Ld[i]; X.l[G::O_U + i] = u[i]; }
+#pragma unroll
+      for (int i = N; i < YS; i++) X.l[G::O_U + i] = 0.f;
+    }
+  }
+  {
+    Kin<R> k;
+    f3 sw[N], sv[N];
+    kin_motion<R>(s, k, sw, sv, O);
+    if (w0) {
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        X.l[G::O_SW + 3 * i] = sw[i].x; X.l[G::O_SW + 3 * i + 1] = sw[i].y; X.l[G::O_SW + 3 * i + 2] = sw[i].z;
+        X.l[G::O_SV + 3 * i] = sv[i].x; X.l[G::O_SV + 3 * i + 1] = sv[i].y; X.l[G::O_SV + 3 * i + 2] = sv[i].z;
+      }
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) X.l[G::O_FR + 12 * b + i] = k.Rm[b].m[i];
+        X.l[G::O_FR + 12 * b + 9] = k.x[b].x; X.l[G::O_FR + 12 * b + 10] = k.x[b].y; X.l[G::O_FR + 12 * b + 11] = k.x[b].z;
+      }
+      static_for<0, NLIM>([&](auto li_c) {
+        constexpr int li = decltype(li_c)::value;
+        constexpr int d = D::LIM.v[li][0];
+        X.l[G::O_LP + 2 * li] = s.q[d] - (float)R::dof_lower[d];
+        X.l[G::O_LP + 2 * li + 1] = (float)R::dof_upper[d] - s.q[d];
+      });
+    }
+  }
+  PBG_GANG_SYNC
+  STAMP(10)
+  auto frame = [&](int b, m3& Rm, f3& x) {
+    const lds_float* p = X.l + G::O_FR + 12 * b;
+#pragma unroll
+    for (int i = 0; i < 9; i++) Rm.m[i] = p[i];
+    x = mk3(p[9], p[10], p[11]);
+  };
+  auto put_desc = [&](int c, f3 rA, f3 rB, f3 n, float dist, float fB, uint32_t mA, uint32_t mB, float floor_, float mu) {
+    const float v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, 1.f, fB,
+                            __builtin_bit_cast(float, mA), __builtin_bit_cast(float, mB), floor_, 0.f};
+#pragma unroll
+    for (int w = 0; w < G::DW; w++) cput<R, T>(X, c, w, v[w]);
+    cput<R, T>(X, c, G::DW, mu);
+  };
+  const uint64_t gang_mask = ((T == 64) ? ~0ull : ((1ull << T) - 1ull)) << (X.le * T);
+  const uint64_t below = (1ull << (X.le * T + X.t)) - 1ull;
+  int nc = 0;
+  // --- distributed: floor slots (slot order) ---------------------------------------------
+  uint64_t sb = 0;
+  static_for<0, G::ROUNDS_S>([&](auto r_c) {
+    constexpr int r = decltype(r_c)::value;
+    const int sl = r * T + X.t;
+    bool act = false;
+    f3 cc;
+    float rad = 0.f;
+    if (sl < R::NS) {
+      m3 Rm; f3 x;
+      frame(TB.slot_body[sl], Rm, x);
+      cc = x + mul(Rm, mk3(TB.slot[sl][0], TB.slot[sl][1], TB.slot[sl][2]));
+      rad = TB.slot[sl][3];
+      act = cc.z - rad < (float)PBG_CONTACT_THRESHOLD;
+    }
+    const uint64_t bal = __ballot(act);
+    const uint64_t mine = bal & gang_mask;
+    sb |= (mine >> (X.le * T)) << (r * T);
+    if (act) {
+      const int c = nc + __popcll(bal & gang_mask & below);
+      const f3 P = mk3(cc.x, cc.y, cc.z - rad);
+      put_desc(c, P - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[TB.slot_body[sl]], 0u, 1.f, TB.slot_mu[sl]);
+    }
+    nc += __popcll(mine);
+  });
+  slot_bits = sb;
+  // --- distributed: self-collision pairs (pair order) ------------------------------------
+  if constexpr (R::NPAIR > 0) {
+#pragma unroll 1
+    for (int r = 0; r < (R::NPAIR + T - 1) / T; r++) {
+      const int pp = r * T + X.t;
+      bool act = false;
+      f3 PA, PB, nrm;
+      float dist = 0.f;
+      int ga = 0, gb = 0;
+      if (pp < R::NPAIR) {
+        ga = TB.pga[pp]; gb = TB.pgb[pp];
+        m3 Ra; f3 xa, xb; m3 Rb;
+        frame(TB.geom_body[ga], Ra, xa);
+        frame(TB.geom_body[gb], Rb, xb);
+        const f3 a0 = xa + mul(Ra, mk3(TB.gp0[ga][0], TB.gp0[ga][1], TB.gp0[ga][2]));
+        const f3 a1 = xa + mul(Ra, mk3(TB.gp1[ga][0], TB.gp1[ga][1], TB.gp1[ga][2]));
+        const f3 b0 = xb + mul(Rb, mk3(TB.gp0[gb][0], TB.gp0[gb][1], TB.gp0[gb][2]));
+        const f3 b1 = xb + mul(Rb, mk3(TB.gp1[gb][0], TB.gp1[gb][1], TB.gp1[gb][2]));
+        const f3 dc = (a0 + a1) - (b0 + b1);
+        if (dot3(dc, dc) <= TB.pbound2[pp]) {
+          // closest points of two segments (same branch structure as the lane kernel)
+          const f3 d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
+          const float aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
+          float ss, tt;
+          const float eps = 1e-12f;
+          if (aa <= eps && ee <= eps) { ss = tt = 0.f; }
+          else if (aa <= eps) { ss = 0.f; tt = fminf(fmaxf(ff / ee, 0.f), 1.f); }
+          else {
+            const float cc2 = dot3(d1, r0);
+            if (ee <= eps) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+            else {
+              const float bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
+              ss = den > eps ? fminf(fmaxf((bb2 * ff - cc2 * ee) / den, 0.f), 1.f) : 0.f;
+              tt = (bb2 * ss + ff) / ee;
+              if (tt < 0.f) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+              else if (tt > 1.f) { tt = 1.f; ss = fminf(fmaxf((bb2 - cc2) / aa, 0.f), 1.f); }
+            }
+          }
+          const f3 ca = a0 + ss * d1, cb = b0 + tt * d2;
+          const f3 dv = ca - cb;
+          const float dd = norm3(dv);
+          const float ra = TB.gp0[ga][3], rb = TB.gp0[gb][3];
+          dist = dd - ra - rb;
+          act = dist < (float)PBG_CONTACT_THRESHOLD;
+          nrm = dd > 1e-9f ? fast_rcp(dd) * dv : mk3(0, 0, 1);
+          PA = ca - ra * nrm;
+          PB = cb + rb * nrm;
+        }
+      }
+      const uint64_t bal = __ballot(act);
+      if (act) {
+        const int c = nc + __popcll(bal & gang_mask & below);
+        put_desc(c, PA - O, PB - O, nrm, dist, 1.f, TB.chain[TB.geom_body[ga]], TB.chain[TB.geom_body[gb]], 0.f, TB.pmu[pp]);
+      }
+      nc += __popcll(bal & gang_mask);
+    }
+  }
+  PBG_GANG_SYNC
+  STAMP(4)
+  // --- distributed: constraint rows (limits first, then 3 rows per contact) --------------
+  const int njobs = NLIM + 3 * nc;
+#pragma unroll 1
+  for (int j = X.t; wave_any(j < njobs); j += T) {
+    if (j >= njobs) continue;
+    float J[N];
+    const bool is_lim = j < NLIM;
+    int c = 0, dir = 0;
+    float dist = 0.f;
+    if (is_lim) {
+      const int g = TB.lim_g[j];
+#pragma unroll
+      for (int i = 0; i < N; i++) J[i] = i == g ? 1.f : 0.f;
+    } else {
+      c = (j - NLIM) / 3;
+      dir = (j - NLIM) - 3 * c;
+      float v[G::DW];
+#pragma unroll
+      for (int w = 0; w < G::DW; w++) v[w] = cget<R, T>(X, c, w);
+      const f3 rA = mk3(v[0], v[1], v[2]), rB = mk3(v[3], v[4], v[5]), nrm = mk3(v[6], v[7], v[8]);
+      dist = v[9];
+      const float fB = v[11];
+      const uint32_t mA = __builtin_bit_cast(uint32_t, v[12]), mB = __builtin_bit_cast(uint32_t, v[13]);
+      f3 t1, t2;  // btPlaneSpace1(nrm); the floor's (+z) gives (0,-1,0), (1,0,0)
+      if (v[14] != 0.f) { t1 = mk3(0, -1, 0); t2 = mk3(1, 0, 0); }
+      else if (fabsf(nrm.z) > 0.7071067811865476f) {
+        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
+        t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
+        t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+      } else {
+        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
+        t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
+        t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+      }
+      const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
+      const f3 mmA = cross3(rA, nd), mmB = cross3(rB, nd);
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int di = D::dof_of(i);
+        const bool inA = di < 0 || ((mA >> di) & 1u), inB = di < 0 ? fB != 0.f : ((mB >> di) & 1u) != 0u;
+        const f3 sw = mk3(X.l[G::O_SW + 3 * i], X.l[G::O_SW + 3 * i + 1], X.l[G::O_SW + 3 * i + 2]);
+        const f3 sv = mk3(X.l[G::O_SV + 3 * i], X.l[G::O_SV + 3 * i + 1], X.l[G::O_SV + 3 * i + 2]);
+        float tj = 0.f;
+        if (inA) tj += dot3(nd, sv) + dot3(mmA, sw);
+        if (inB) tj -= dot3(nd, sv) + dot3(mmB, sw);
+        J[i] = tj;
+      }
+    }
+    // y = L^-1 J (forward substitution over the compile-time pattern of L)
+    float y[N];
+    float D2 = 0.f, vJ = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      float tt = J[i];
+#pragma unroll
+      for (int kk = 0; kk < i; kk++)
+        if (D::coupled(i, kk)) tt -= X.l[G::O_L + D::lidx(i, kk)] * y[kk];
+      y[i] = tt * X.l[G::O_LD + i];
+      D2 += y[i] * y[i];
+      vJ += y[i] * X.l[G::O_U + i];
+    }
+    const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
+    if (is_lim) {
+      lds_float* p = X.l + G::O_LR + j * G::LRW;
+#pragma unroll
+      for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
+      const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
+      p[YS] = meff;
+      p[YS + 1] = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
+      p[YS + 2] = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
+    } else {
+      const int w0r = G::DW + 1 + dir * G::CRW;
+#pragma unroll
+      for (int i = 0; i < YS; i++) cput<R, T>(X, c, w0r + i, i < N ? y[i] : 0.f);
+      cput<R, T>(X, c, w0r + YS, meff);
+      cput<R, T>(X, c, w0r + YS + 1,
+                 dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+      cput<R, T>(X, c, w0r + YS + 2, 0.f);
+    }
+  }
+  PBG_GANG_SYNC
+  STAMP(11)
+  // --- PGS: 5 sweeps, Bullet order (scene_bases.py:65 numSolverIterations=5) -------------
+  float us[NSL];
+#pragma unroll
+  for (int m = 0; m < NSL; m++) us[m] = X.l[G::O_U + X.t + m * T];
+  {
+    // joint-limit rows stay in registers for the whole solve
+    constexpr int NL1 = NLIM > 0 ? NLIM : 1;
+    float ly[NL1][NSL], lm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
+#pragma unroll
+    for (int li = 0; li < NLIM; li++) {
+      const lds_float* p = X.l + G::O_LR + li * G::LRW;
+#pragma unroll
+      for (int m = 0; m < NSL; m++) ly[li][m] = p[X.t + m * T];
+      lm[li] = p[YS]; ltl[li] = p[YS + 1]; lth[li] = p[YS + 2];
+      llo[li] = 0.f; lhi[li] = 0.f;
+    }
+    for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+#pragma unroll
+      for (int li = 0; li < NLIM; li++) {
+        float part = 0.f;
+#pragma unroll
+        for (int m = 0; m < NSL; m++) part += ly[li][m] * us[m];
+        const float yu = gang_sum<T>(part);
+        const float meff = lm[li];
+        const float nlo = fminf(fmaxf(llo[li] + meff * (ltl[li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float dlo = nlo - llo[li];
+        // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
+        const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
+        const float nhi = fminf(fmaxf(lhi[li] + meff * (lth[li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float dhi = nhi - lhi[li];
+        llo[li] = nlo;
+        lhi[li] = nhi;
+        const float dl = dlo - dhi;
+#pragma unroll
+        for (int m = 0; m < NSL; m++) us[m] += ly[li][m] * dl;
+      }
+#pragma unroll 1
+      for (int c = 0; wave_any(c < nc); c++) {  // contact normals
+        if (c >= nc) continue;
+        float lam;
+        const float nl = gang_row<R, T>(X, c, 0, us, 0.f, 3.0e38f, &lam);
+        set_row_lam<R, T>(X, c, 0, nl);
+      }
+#pragma unroll 1
+      for (int c = 0; wave_any(c < nc); c++) {  // frictions, only under a positive normal impulse [EXT]
+        if (c >= nc) continue;
+        const float ln = cget<R, T>(X, c, G::DW + 1 + G::YS + 2);
+        if (!(ln > 0.f)) continue;
+        const float lim = cget<R, T>(X, c, G::DW) * ln;
+        float lam;
+        float nl = gang_row<R, T>(X, c, 1, us, -lim, lim, &lam);
+        set_row_lam<R, T>(X, c, 1, nl);
+        nl = gang_row<R, T>(X, c, 2, us, -lim, lim, &lam);
+        set_row_lam<R, T>(X, c, 2, nl);
+      }
+    }
+  }
+  // --- replicated: gather u, back-substitute, integrate ----------------------------------
+  STAMP(5)
+#pragma unroll
+  for (int m = 0; m < NSL; m++) X.l[G::O_U + X.t + m * T] = us[m];
+  PBG_GANG_SYNC
+  {
+    float L[D::NNZ], Ld[N], u[N], nu[N];
+#pragma unroll
+    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+#pragma unroll
+    for (int i = 0; i < N; i++) { Ld[i] = X.l[G::O_LD + i]; u[i] = X.l[G::O_U + i]; }
+    integrate<R>(s, L, Ld, u, nu);
+  }
+  PBG_GANG_SYNC  // the next sub-step's staging overwrites this one's LDS
+  STAMP(6)
+  return nc;
+}
+
+template <class R, int T>
+__global__ __launch_bounds__(64) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
+                                                       int env_words) {
+  extern __shared__ float lds_dyn[];
+  using G = Gang<R, T>;
+  constexpr int EPW = 64 / T;
+  GangCtx X;
+  X.t = threadIdx.x % T;
+  X.le = threadIdx.x / T;
+  const int e = blockIdx.x * EPW + X.le;
+  if (e >= B.n) return;  // whole gangs only
+  X.l = (lds_float*)lds_dyn + X.le * env_words;
+  X.g = scratch + (size_t)e * G::GWORDS;
+  X.cap = cap;
+  const bool w0 = X.t == 0;
+  STAMP_DECL
+  State<R> s;
+  load_state<R>(s, B.st, B.n, e);
+  float act[R::NA];
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
+  // apply_action: tau = power * power_coef * clip(a, -1, 1)   (robot_locomotors.py:26-29)
+  float tau[R::NJ];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) tau[d] = 0.f;
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) {
+    const float c = fminf(fmaxf(act[i], -1.f), 1.f);
+    tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
+  }
+  uint64_t slot_bits = 0;
+  int nc = 0;
+  STAMP(7)
+  for (int sub = 0; sub < R::substeps; sub++) nc = gang_substep<R, T>(s, tau, X, slot_bits SUB_STAMP_PASS);
+  if (io.ncontact && w0) io.ncontact[e] = nc;
+  const int el = B.elapsed[e] + 1;
+  uint32_t flags = B.flags[e];
+  float obs[R::OBS];
+  PackOut po;
+  double pot_new = 0.0;
+  if constexpr (R::kind == 1) {
+    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+  } else {
+    PackIn<R> in;
+    gather<R>(s, flags & 1u, in);
+    uint32_t fnew = 0;
+#pragma unroll
+    for (int f = 0; f < R::NF; f++) {
+      uint64_t fm = 0;
+#pragma unroll
+      for (int sl = 0; sl < R::NS; sl++)
+        if (R::slot_link[sl] == R::foot_link[f]) fm |= 1ull << sl;
+      fnew |= ((slot_bits & fm) ? 1u : 0u) << f;
+      in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
+    }
+    in.feet_new = fnew;
+    in.potential_old = B.pot[e];
+    in.initial_z = B.z0[e];
+    walker_pack<R>(in, act, obs, po);
+    pot_new = po.potential;
+    flags = (flags & 0xFFu) | (po.feet_out << 8);
+  }
+  STAMP(8)
+  const bool term = po.done;
+  const bool trunc = el >= R::max_episode_steps;  // gym TimeLimit (envs/__init__.py max_episode_steps)
+  if (w0) {
+    io.rew[e] = (float)po.reward;
+    if (io.rew64) io.rew64[e] = po.reward;
+    io.done[e] = term || trunc;
+    if (io.trunc) io.trunc[e] = trunc && !term;
+  }
+  if (io.autoreset && (term || trunc)) {
+    if (io.term_obs && w0) {
+#pragma unroll
+      for (int i = 0; i < R::OBS; i++) io.term_obs[(size_t)e * R::OBS + i] = obs[i];
+    }
+    bool has_floor = flags & 1u;
+    double pot;
+    float z0;
+    // every lane reads the episode counter (one load instruction) before the writer bumps it
+    const uint32_t epi = B.episode[e];
+    if (w0) B.episode[e] = epi + 1;
+    reset_env_epi<R>(B, e, s, nullptr, obs, has_floor, pot, z0, epi);
+    if (w0) {
+      B.pot[e] = pot;
+      B.z0[e] = z0;
+      B.elapsed[e] = 0;
+      B.flags[e] = has_floor ? 1u : 0u;
+    }
+  } else if (w0) {
+    B.pot[e] = pot_new;
+    B.elapsed[e] = el;
+    B.flags[e] = flags;
+  }
+  if (w0) {
+    store_state<R>(s, B.st, B.n, e);
+#pragma unroll
+    for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+  }
+  STAMP(9)
+  STAMP_FLUSH
+}
+
+}  // namespace pbg

@@ -12,15 +12,17 @@ struct StepIO;
 struct ResetIO;
 
 struct Geometry {
-  int team;          // lanes per env: 1 (step_kernel) or 4 (team_step_kernel, pbg_team.hip)
+  int team;          // lanes per env: 1 (step_kernel), 4 (team_step_kernel, pbg_team.hip) or
+                     // 16 (gang_step_kernel, pbg_gang.hip)
   int block;         // lanes per step workgroup: 16, 32 or 64
-  int lds_rows;      // contact-constraint rows resident in LDS per env
+  int lds_rows;      // contact-constraint rows (gang: contacts) resident in LDS per env
+  int env_words;     // gang: LDS words per env
   size_t lds_bytes;  // dynamic LDS per step workgroup
   size_t scratch_words_per_env;
 };
 
 #define PBG_DECLARE_ROBOT(NAME)                                                                            \
-  int plan_##NAME(int n_envs, int cus, int allow_team, Geometry* g);                                                       \
+  int plan_##NAME(int n_envs, int cus, int mode, Geometry* g);                                                       \
   int launch_step_##NAME(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s); \
   int launch_reset_##NAME(const Buffers& B, const ResetIO& io, hipStream_t s);                             \
   int launch_get_state_##NAME(const Buffers& B, double* phys, double* aux, hipStream_t s);                 \

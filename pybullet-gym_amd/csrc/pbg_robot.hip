@@ -5,6 +5,7 @@
 #include "pbg_launch.h"
 #include "pbg_step.hip"
 #include "pbg_team.hip"
+#include "pbg_gang.hip"
 
 #ifndef PBG_ROBOT
 #error "compile with -DPBG_ROBOT=<robot struct name>"
@@ -40,6 +41,7 @@ static int plan_team(int n_envs, int cus, Geometry* g) {
     size_t per_env = (size_t)RW::HEAD + (size_t)cap * RW::W;
     if (per_env < (size_t)(2 * RR::NL + 2 * RR::NJ)) per_env = 2 * RR::NL + 2 * RR::NJ;  // pack staging
     g->team = 4;
+    g->env_words = 0;
     g->block = 64;
     g->lds_rows = cap;
     g->lds_bytes = (size_t)ES * sizeof(float) * per_env;
@@ -64,9 +66,54 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
   }
 }
 
-int PBG_FN(plan_)(int n_envs, int cus, int allow_team, Geometry* g) {
-  if (Team<R>::ok && allow_team) return plan_team<R>(n_envs, cus, g);
+// Gang geometry (pbg_gang.hip): 16 lanes per env, 4 envs per one-wave workgroup; the
+// per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
+// + 3 rows), contacts past the capacity spill to the device workspace.
+template <class RR>
+static int plan_gang(int n_envs, int cus, Geometry* g) {
+  if constexpr (RR::kind == 0) {
+    using G = Gang<RR, 16>;
+    constexpr int EPW = 4;
+    const int wgs = (n_envs + EPW - 1) / EPW;
+    const int wpc = (wgs + cus - 1) / cus;
+    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
+    long words = (long)(budget / ((size_t)EPW * sizeof(float))) - G::FIXED;
+    int cap = (int)(words / G::PERC);
+    if (cap > G::MAXC) cap = G::MAXC;
+    if (cap < 0) cap = 0;
+    g->team = 16;
+    g->block = 64;
+    g->lds_rows = cap;
+    g->env_words = G::FIXED + cap * G::PERC;
+    g->lds_bytes = (size_t)EPW * sizeof(float) * (size_t)g->env_words;
+    g->scratch_words_per_env = G::GWORDS;
+    return (int)hipFuncSetAttribute((const void*)gang_step_kernel<RR, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)g->lds_bytes);
+  } else {
+    (void)n_envs; (void)cus; (void)g;
+    return (int)hipErrorInvalidValue;
+  }
+}
+template <class RR>
+static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if constexpr (RR::kind == 0) {
+    if (g.team != 16) return false;
+    hipLaunchKernelGGL((gang_step_kernel<RR, 16>), dim3(blocks(B.n, 4)), dim3(64), g.lds_bytes, s, B, io, scratch,
+                       g.lds_rows, g.env_words);
+    return true;
+  } else {
+    (void)B; (void)io; (void)scratch; (void)g; (void)s;
+    return false;
+  }
+}
+
+// mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers);
+// 2 = gang for every walker (parity tests of the gang kernel on Ant)
+int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
+  if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
+  if (R::kind == 0 && mode >= 1) return plan_gang<R>(n_envs, cus, g);
   g->team = 1;
+  g->env_words = 0;
   const int per_cu = (n_envs + cus - 1) / cus;
   int b = 16;
   while (b < per_cu && b < 64) b *= 2;
@@ -91,6 +138,7 @@ int PBG_FN(plan_)(int n_envs, int cus, int allow_team, Geometry* g) {
 
 int PBG_FN(launch_step_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if (launch_team<R>(B, io, scratch, g, s)) return (int)hipGetLastError();
+  if (launch_gang<R>(B, io, scratch, g, s)) return (int)hipGetLastError();
   const dim3 grid(blocks(B.n, g.block)), blk(g.block);
   if (g.block == 64) hipLaunchKernelGGL((step_kernel<R, 64>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
   else if (g.block == 32) hipLaunchKernelGGL((step_kernel<R, 32>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);

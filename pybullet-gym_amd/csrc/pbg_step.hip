@@ -417,6 +417,19 @@ PBG_DEV void motion_vectors(const f3* ja, const f3* jo, f3 O, f3* sw, f3* sv) {
   }
 }
 
+// Link frames and dof motion vectors about the reference point O, recomputed from the
+// positions (cheaper than keeping phase A's copies live through the factorisation).
+template <class R>
+PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, f3* sw, f3* sv, f3& O) {
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ;
+  const State<R> sp = opaque_positions<R>(s);
+  f3 ja2[NJ > 0 ? NJ : 1], jo2[NJ > 0 ? NJ : 1];
+  fk_pos<R, true>(sp, k, ja2, jo2);
+  O = k.c[D::REF_BODY];
+  motion_vectors<R>(ja2, jo2, O, sw, sv);
+}
+
 #ifdef PBG_STAMPS
 #define SUB_STAMP_ARGS , unsigned long long& _st_t, unsigned long long* _st_acc
 #define SUB_STAMP_PASS , _st_t, _st_acc
@@ -424,12 +437,14 @@ PBG_DEV void motion_vectors(const f3* ja, const f3* jo, f3 O, f3* sw, f3* sv) {
 #define SUB_STAMP_ARGS
 #define SUB_STAMP_PASS
 #endif
-template <class R, int LS>
-PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw SUB_STAMP_ARGS) {
+// Unconstrained joint-space dynamics of one sub-step (phase A .. u): composites, mass
+// matrix and bias, its sparse Cholesky factor L (Ld = 1/diag), the predicted velocity
+// nu = clamp(nu + dt M^-1 (tau - C)) and u = L^T nu.  Shared by the lane and gang kernels.
+template <class R>
+PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
   constexpr float dt = (float)R::dt_sub;
-  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
   constexpr float g = (float)PBG_GRAVITY;
 
   // --- phase A: one forward pass over the bodies: kinematics, velocities, bias
@@ -554,7 +569,6 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 
   STAMP(0)
   // --- mass matrix (lower triangle, gi >= gk) and bias -----------------------------------
-  float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
   float rhs[N];
   {
   f3 sw[N], sv[N];
@@ -587,7 +601,6 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 
   STAMP(1)
   // --- Cholesky (no fill-in in leaf-first order); Ld = 1 / diag(L) ----------------------
-  float Ld[N];
 #pragma unroll
   for (int j = 0; j < N; j++) {
     float sjj = L[D::lidx(j, j)];
@@ -610,7 +623,6 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   }
 
   // --- unconstrained velocity: nu_pred = nu + dt * M^-1 (tau - C) ------------------------
-  float nu[N];
 #pragma unroll
   for (int d = 0; d < NJ; d++) nu[D::gj(d)] = s.qd[d];
   if (R::floating) {
@@ -635,7 +647,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * qdd[kk];
     qdd[i] = t * Ld[i];
   }
-  float u[N];  // u = L^T nu_pred
+  // u = L^T nu_pred
 #pragma unroll
   for (int i = 0; i < N; i++) {
     float t = nu[i] + dt * qdd[i];
@@ -649,7 +661,66 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       if (D::coupled(kk, i)) t += L[D::lidx(kk, i)] * nu[kk];
     u[i] = t;
   }
+}
 
+// nu = L^-T u, clamp, semi-implicit Euler (exponential-map base rotation).  nu: scratch.
+template <class R>
+PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float* u, float* nu) {
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ, N = R::NDOF;
+  constexpr float dt = (float)R::dt_sub;
+  // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    float t = u[i];
+#pragma unroll
+    for (int kk = i + 1; kk < N; kk++)
+      if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * nu[kk];
+    nu[i] = t * Ld[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) nu[i] = fminf(fmaxf(nu[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+#pragma unroll
+  for (int d = 0; d < NJ; d++) {
+    s.qd[d] = nu[D::gj(d)];
+    s.q[d] += dt * s.qd[d];
+  }
+  if (R::floating) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      s.bv[i] = nu[NJ + i];
+      s.bw[i] = nu[NJ + 3 + i];
+      s.bp[i] += dt * s.bv[i];
+    }
+    // exponential-map quaternion update with the world angular velocity  [EXT]
+    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
+    float ang = norm3(wv);
+    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    float sh, dw;
+    sincos_fast(0.5f * ang * dt, &sh, &dw);
+    f3 ax;
+    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
+    else ax = (sh / ang) * wv;
+    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
+    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+    s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
+  }
+}
+
+template <class R, int LS>
+PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw SUB_STAMP_ARGS) {
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ, N = R::NDOF;
+  constexpr float dt = (float)R::dt_sub;
+  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
+  float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
+  float Ld[N], nu[N], u[N];
+  dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
+  f3 O;
   STAMP(2)
   // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
   static_for<0, D::NLIM>([&](auto li_c) {
@@ -691,14 +762,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   // keeping phase A's copies live through the factorisation
   Kin<R> k;
   f3 sw[N], sv[N];
-  {
-    const State<R> sp = opaque_positions<R>(s);
-    f3 ja2[NJ > 0 ? NJ : 1], jo2[NJ > 0 ? NJ : 1];
-    fk_pos<R, true>(sp, k, ja2, jo2);
-    const f3 O2 = k.c[D::REF_BODY];
-    motion_vectors<R>(ja2, jo2, O2, sw, sv);
-    O = O2;
-  }
+  kin_motion<R>(s, k, sw, sv, O);
   // contact rows are staged: normals first (in contact order), frictions after.
   // Each contact stores its normal row now and its two friction rows at MAXROWS-space
   // offsets after all normals; friction rows are compacted once nc is known.
@@ -867,46 +931,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   }
 
   STAMP(5)
-  // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
-#pragma unroll
-  for (int i = N - 1; i >= 0; i--) {
-    float t = u[i];
-#pragma unroll
-    for (int kk = i + 1; kk < N; kk++)
-      if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * nu[kk];
-    nu[i] = t * Ld[i];
-  }
-#pragma unroll
-  for (int i = 0; i < N; i++) nu[i] = fminf(fmaxf(nu[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
-#pragma unroll
-  for (int d = 0; d < NJ; d++) {
-    s.qd[d] = nu[D::gj(d)];
-    s.q[d] += dt * s.qd[d];
-  }
-  if (R::floating) {
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      s.bv[i] = nu[NJ + i];
-      s.bw[i] = nu[NJ + 3 + i];
-      s.bp[i] += dt * s.bv[i];
-    }
-    // exponential-map quaternion update with the world angular velocity  [EXT]
-    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
-    float ang = norm3(wv);
-    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
-    float sh, dw;
-    sincos_fast(0.5f * ang * dt, &sh, &dw);
-    f3 ax;
-    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
-    else ax = (sh / ang) * wv;
-    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
-    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
-    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
-    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
-    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
-    s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
-  }
+  integrate<R>(s, L, Ld, u, nu);
   STAMP(6)
   return nc;
 }
@@ -1162,12 +1187,11 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
   for (int i = 0; i < R::NO; i++) { in.jq[i] = s.q[R::obs_dof[i]]; in.jqd[i] = s.qd[R::obs_dof[i]]; }
 }
 
+// epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e]
 template <class R>
-PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                       double& pot, float& z0) {
+PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
+                           double& pot, float& z0, uint32_t epi) {
   snapshot_state<R>(s);
-  const uint32_t epi = B.episode[e];
-  B.episode[e] = epi + 1;
   if (init_q) {
 #pragma unroll
     for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = init_q[(size_t)e * R::NR + r];
@@ -1204,6 +1228,14 @@ PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q
   z0 = (float)po.initial_z;
   has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
   }
+}
+
+template <class R>
+PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
+                       double& pot, float& z0) {
+  const uint32_t epi = B.episode[e];
+  B.episode[e] = epi + 1;
+  reset_env_epi<R>(B, e, s, init_q, obs, has_floor, pot, z0, epi);
 }
 
 template <class R>

@@ -10,6 +10,8 @@ from pybulletgym_amd.vec_env import VecEnv
 L = _native.lib()
 L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
 names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS", "integrate", "act+load", "pack", "store"]
+gang_names = {0: "phase A (kin, composites)", 1: "mass matrix", 3: "cholesky+solve", 10: "stage to LDS", 4: "detect",
+              11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 8: "pack", 9: "store"}
 for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]))]:
     env = VecEnv(env_id, n, seed=1, autoreset=True)
     env.reset()
@@ -23,9 +25,15 @@ for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] o
     for i in range(steps): env.step(acts[10 + i])
     torch.cuda.synchronize()
     L.pbg_debug_stamps(rid, buf)
-    lanes = n * max(1, env.info.lanes_per_env)
-    waves = (lanes + 63) // 64
-    tot = sum(buf[i] for i in range(10))
-    print(f"{env_id} n={n}: cycles per wave per env-step = {tot / waves / steps:.0f}")
-    for i in range(10):
-        print(f"   {names[i]:16s} {buf[i] / waves / steps:10.0f}  {100.0 * buf[i] / tot:5.1f}%")
+    lpe = max(1, env.info.lanes_per_env)
+    if lpe == 1:  # lane kernel: workgroups of 16/32/64 lanes, one wave each (plan_* in pbg_robot.hip)
+        per_cu, b = -(-n // 256), 16
+        while b < per_cu and b < 64: b *= 2
+        waves = -(-n // b)
+    else:
+        waves = -(-n * lpe // 64)
+    tot = sum(buf[i] for i in range(16))
+    print(f"{env_id} n={n} lanes/env={lpe}: cycles per wave per env-step = {tot / waves / steps:.0f}")
+    labels = gang_names if lpe == 16 else dict(enumerate(names))
+    for i in sorted(labels, key=lambda k: list(labels).index(k)):
+        print(f"   {labels[i]:26s} {buf[i] / waves / steps:10.0f}  {100.0 * buf[i] / tot:5.1f}%")
