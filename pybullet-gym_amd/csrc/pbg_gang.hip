@@ -35,6 +35,8 @@
 // at c >= cap live at the same offsets in the env's device workspace.
 namespace pbg {
 
+#define PBG_GANG_BLOCK 256  // lanes per gang workgroup (4 waves)
+
 template <int CTRL>
 PBG_DEV float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
@@ -97,6 +99,94 @@ constexpr GangTab<R> make_gang_tab() {
 template <class R>
 __constant__ GangTab<R> g_gang_tab = make_gang_tab<R>();
 
+// body tree for the distributed dynamics: body 0 = base, body l+1 = link l
+template <class R>
+struct GangDynTab {
+  static constexpr int NB = R::NL + 1, N = R::NDOF, NNZ = Dims<R>::NNZ, NJ1 = R::NJ > 0 ? R::NJ : 1;
+  int parent[NB], jt[NB], dof[NB];
+  int lev_start[NB + 2], lev_body[NB];  // bodies grouped by depth
+  int child_start[NB + 1], child[NB];
+  float ro[NB][9], opos[NB][3], axis[NB][3], anchor[NB][3], com[NB][3], mass[NB], inertia[NB][6];
+  int me_i[NNZ], me_k[NNZ], me_b[NNZ];  // packed lower-triangle entries of M: rows, cols, composite
+  float me_arm[NNZ];                     // armature on joint diagonals
+  int g_body[N], g_dof[N];               // composite owning generalized index i; its joint dof (-1: base)
+  float damping[NJ1];
+};
+template <class R>
+constexpr int body_depth(int b) {
+  int d = 0;
+  while (b > 0) { b = R::link_parent[b - 1] + 1; d++; }
+  return d;
+}
+template <class R>
+constexpr int gang_nlev() {
+  int m = 0;
+  for (int b = 0; b <= R::NL; b++) m = body_depth<R>(b) > m ? body_depth<R>(b) : m;
+  return m + 1;
+}
+template <class R>
+constexpr GangDynTab<R> make_gang_dyn_tab() {
+  using D = Dims<R>;
+  GangDynTab<R> t{};
+  constexpr int NB = R::NL + 1;
+  for (int b = 0; b < NB; b++) {
+    t.parent[b] = b == 0 ? -1 : R::link_parent[b - 1] + 1;
+    t.jt[b] = b == 0 ? 4 : R::link_jtype[b - 1];
+    t.dof[b] = b == 0 ? -1 : R::link_dof[b - 1];
+    t.mass[b] = (float)D::body_mass(b);
+    for (int i = 0; i < 6; i++) t.inertia[b][i] = (float)(b == 0 ? R::base_inertia[i] : R::link_inertia[b - 1][i]);
+    if (b > 0) {
+      const int l = b - 1;
+      const double x = R::link_offset_quat[l][0], y = R::link_offset_quat[l][1], z = R::link_offset_quat[l][2], w = R::link_offset_quat[l][3];
+      const double m[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                           2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                           2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+      for (int i = 0; i < 9; i++) t.ro[b][i] = (float)m[i];
+      for (int c = 0; c < 3; c++) {
+        t.opos[b][c] = (float)R::link_offset_pos[l][c];
+        t.axis[b][c] = (float)R::link_axis[l][c];
+        t.anchor[b][c] = (float)R::link_anchor[l][c];
+        t.com[b][c] = (float)R::link_com[l][c];
+      }
+    }
+  }
+  constexpr int NLEV = gang_nlev<R>();
+  int k = 0;
+  for (int lv = 0; lv < NLEV; lv++) {
+    t.lev_start[lv] = k;
+    for (int b = 0; b < NB; b++)
+      if (body_depth<R>(b) == lv) t.lev_body[k++] = b;
+  }
+  for (int lv = NLEV; lv < NB + 2; lv++) t.lev_start[lv] = k;
+  k = 0;
+  for (int b = 0; b < NB; b++) {
+    t.child_start[b] = k;
+    for (int c = 1; c < NB; c++)
+      if (R::link_parent[c - 1] + 1 == b) t.child[k++] = c;
+  }
+  t.child_start[NB] = k;
+  int e = 0;
+  for (int a = 0; a < R::NDOF; a++)
+    for (int b = 0; b <= a; b++)
+      if (D::coupled(a, b)) {
+        const int dk = D::dof_of(b), da = D::dof_of(a);
+        t.me_i[e] = a;
+        t.me_k[e] = b;
+        t.me_b[e] = dk >= 0 ? R::dof_link[dk] + 1 : 0;
+        t.me_arm[e] = (a == b && da >= 0) ? (float)R::dof_armature[da] : 0.f;
+        e++;
+      }
+  for (int i = 0; i < R::NDOF; i++) {
+    const int di = D::dof_of(i);
+    t.g_dof[i] = di;
+    t.g_body[i] = di >= 0 ? R::dof_link[di] + 1 : 0;
+  }
+  for (int d = 0; d < R::NJ; d++) t.damping[d] = (float)R::dof_damping[d];
+  return t;
+}
+template <class R>
+__constant__ GangDynTab<R> g_gang_dyn = make_gang_dyn_tab<R>();
+
 // ------------------------------------------------------------------ layout
 template <class R, int T>
 struct Gang {
@@ -109,20 +199,40 @@ struct Gang {
   static constexpr int CRW = YS + 3;           // y | m_eff | target | lambda
   static constexpr int LRW = YS + 5;           // y | m_eff | t_lo | t_hi | pad 2
   static constexpr int PERC = DW + 1 + 3 * CRW;
-  static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_SW = O_U + YS, O_SV = O_SW + 3 * N;
-  static constexpr int O_FR = O_SV + 3 * N, O_LP = O_FR + 12 * NB, O_LR = O_LP + 2 * NLIM;
-  static constexpr int FIXED = O_LR + NLIM * LRW;
+  static constexpr int NJ1 = R::NJ > 0 ? R::NJ : 1;
+  static constexpr int BW = 27;                // body record: Rm 9 | x 3 | c 3 | w 3 | v 3 | al 3 | ac 3
+  static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
+  static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
+  static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
+  static constexpr int O_FR = O_JO + 3 * NJ1, O_LP = O_FR + BW * NB, O_LR = O_LP + 2 * NLIM;
+  // the composites (dead once M is built) share their words with the limit rows
+  static constexpr int O_CP = O_LR;
+  static constexpr int LRSZ = NLIM * LRW > NB * CW ? NLIM * LRW : NB * CW;
+  static constexpr int FIXED = O_LR + LRSZ;
   static constexpr int GWORDS = (MAXC > 0 ? MAXC : 1) * PERC;  // device workspace per env
   static constexpr int ROUNDS_S = (R::NS + T - 1) / T;
 };
 
 // per-lane view of the env's LDS region and device workspace
 struct GangCtx {
+  lds_float* tabs;  // workgroup copy of GangTab<R> | GangDynTab<R>
   lds_float* l;  // env LDS region
   float* g;      // env device workspace
   int cap;       // contacts resident in LDS
   int t;         // lane in the gang
   int le;        // gang in the wave
+};
+// model tables, copied once per workgroup into LDS (vector-memory loads of a __constant__
+// table indexed by lane cost hundreds of cycles each; the level loops chain several)
+template <class R>
+struct GangTabs {
+  typedef __attribute__((address_space(3))) const GangTab<R> Tab;
+  typedef __attribute__((address_space(3))) const GangDynTab<R> Dyn;
+  static constexpr int TAB_WORDS = (int)((sizeof(GangTab<R>) + 15) / 16) * 4;
+  static constexpr int DYN_WORDS = (int)((sizeof(GangDynTab<R>) + 15) / 16) * 4;
+  static constexpr int WORDS = TAB_WORDS + DYN_WORDS;
+  static PBG_DEV Tab& tab(const lds_float* p) { return *(Tab*)p; }
+  static PBG_DEV Dyn& dyn(const lds_float* p) { return *(Dyn*)(p + TAB_WORDS); }
 };
 #define PBG_GANG_SYNC                                    \
   {                                                      \
@@ -182,21 +292,220 @@ PBG_DEV void set_row_lam(const GangCtx& X, int c, int dir, float v) {
   if (X.t == 0) cput<R, T>(X, c, G::DW + 1 + dir * G::CRW + G::YS + 2, v);
 }
 
-// ------------------------------------------------------------------ one physics sub-step
+// Distributed unconstrained dynamics of one sub-step (the gang counterpart of dyn_mass):
+// level-synchronous forward kinematics / velocities / bias accelerations (one body per
+// lane per tree level), per-body inertia + wrench about the reference point O, composites
+// by a leaf-to-root pass over the levels, then the packed lower triangle of M and the bias
+// dealt round-robin over the lanes.  Everything lands in the gang's LDS: body records
+// (frames for the collision pass), motion vectors sw / sv, M at O_L, the right-hand side
+// at O_RHS.  Same formulas as dyn_mass with run-time model constants.
 template <class R, int T>
+PBG_DEV f3 gang_O(const GangCtx& X) {
+  using G = Gang<R, T>;
+  constexpr int rb = Dims<R>::REF_BODY;
+  const lds_float* p = X.l + G::O_FR + G::BW * rb + 12;
+  return mk3(p[0], p[1], p[2]);
+}
+template <class R, int T>
+PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
+  using D = Dims<R>;
+  using G = Gang<R, T>;
+  auto& TD = GangTabs<R>::dyn(X.tabs);
+  constexpr int NB = D::NB, N = R::NDOF, NLEV = gang_nlev<R>();
+  constexpr float g = (float)PBG_GRAVITY;
+  const bool w0 = X.t == 0;
+  // base record and joint state (replicated registers -> LDS)
+  if (w0) {
+    const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+    lds_float* p = X.l + G::O_FR;
+    const float rec[G::BW] = {Rb.m[0], Rb.m[1], Rb.m[2], Rb.m[3], Rb.m[4], Rb.m[5], Rb.m[6], Rb.m[7], Rb.m[8],
+                              s.bp[0], s.bp[1], s.bp[2], s.bp[0], s.bp[1], s.bp[2],
+                              R::floating ? s.bw[0] : 0.f, R::floating ? s.bw[1] : 0.f, R::floating ? s.bw[2] : 0.f,
+                              R::floating ? s.bv[0] : 0.f, R::floating ? s.bv[1] : 0.f, R::floating ? s.bv[2] : 0.f,
+                              0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < G::BW; i++) p[i] = rec[i];
+#pragma unroll
+    for (int d = 0; d < R::NJ; d++) { X.l[G::O_Q + d] = s.q[d]; X.l[G::O_QD + d] = s.qd[d]; }
+  }
+  PBG_GANG_SYNC
+  // forward pass, one level at a time (a body's parent is one level up)
+  static_for<1, NLEV>([&](auto lv_c) {
+    constexpr int lv = decltype(lv_c)::value;
+#pragma unroll 1
+    for (int idx = TD.lev_start[lv] + X.t; idx < TD.lev_start[lv + 1]; idx += T) {
+      const int b = TD.lev_body[idx], p = TD.parent[b], jt = TD.jt[b], d = TD.dof[b];
+      const lds_float* P = X.l + G::O_FR + G::BW * p;
+      m3 Rp, Ro;
+#pragma unroll
+      for (int i = 0; i < 9; i++) { Rp.m[i] = P[i]; Ro.m[i] = TD.ro[b][i]; }
+      const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(P[12], P[13], P[14]), wp = mk3(P[15], P[16], P[17]);
+      const f3 vp = mk3(P[18], P[19], P[20]), alp = mk3(P[21], P[22], P[23]), acp = mk3(P[24], P[25], P[26]);
+      const m3 R0 = mul(Rp, Ro);
+      const f3 x0 = xp + mul(Rp, mk3(TD.opos[b][0], TD.opos[b][1], TD.opos[b][2]));
+      const f3 axl = mk3(TD.axis[b][0], TD.axis[b][1], TD.axis[b][2]);
+      const f3 anl = mk3(TD.anchor[b][0], TD.anchor[b][1], TD.anchor[b][2]);
+      const float q = d >= 0 ? X.l[G::O_Q + d] : 0.f, qd = d >= 0 ? X.l[G::O_QD + d] : 0.f;
+      m3 Rm = R0;
+      f3 x = x0;
+      if (jt == 0) {
+        const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, q);
+        Rm = mul(R0, Rj);
+        x = x0 + mul(R0, anl - mul(Rj, anl));
+      } else if (jt == 1) {
+        x = x0 + q * mul(R0, axl);
+      }
+      const f3 c = x + mul(Rm, mk3(TD.com[b][0], TD.com[b][1], TD.com[b][2]));
+      f3 w, v, al, ac;
+      if (jt == 0) {
+        const f3 a = mul(R0, axl);
+        const f3 o = x0 + mul(R0, anl);
+        const f3 ro = o - cp;
+        const f3 vo = vp + cross3(wp, ro);
+        const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+        w = wp + qd * a;
+        al = alp + qd * cross3(wp, a);
+        const f3 rc = c - o;
+        v = vo + cross3(w, rc);
+        ac = ao + cross3(al, rc) + cross3(w, cross3(w, rc));
+        X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
+        X.l[G::O_JO + 3 * d] = o.x; X.l[G::O_JO + 3 * d + 1] = o.y; X.l[G::O_JO + 3 * d + 2] = o.z;
+      } else if (jt == 1) {
+        const f3 a = mul(R0, axl);
+        const f3 r = c - cp;
+        w = wp;
+        al = alp;
+        v = vp + cross3(wp, r) + qd * a;
+        ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * qd) * cross3(wp, a);
+        X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
+        X.l[G::O_JO + 3 * d] = x0.x; X.l[G::O_JO + 3 * d + 1] = x0.y; X.l[G::O_JO + 3 * d + 2] = x0.z;
+      } else {
+        const f3 r = c - cp;
+        w = wp;
+        al = alp;
+        v = vp + cross3(wp, r);
+        ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
+      }
+      const float rec[G::BW] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
+                                x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z};
+      lds_float* Q = X.l + G::O_FR + G::BW * b;
+#pragma unroll
+      for (int i = 0; i < G::BW; i++) Q[i] = rec[i];
+    }
+    PBG_GANG_SYNC
+  });
+  const f3 O = gang_O<R, T>(X);
+  // per-body inertia and wrench about O; motion vectors about O
+#pragma unroll 1
+  for (int b = X.t; b < NB; b += T) {
+    const lds_float* P = X.l + G::O_FR + G::BW * b;
+    m3 Rm;
+#pragma unroll
+    for (int i = 0; i < 9; i++) Rm.m[i] = P[i];
+    const f3 c = mk3(P[12], P[13], P[14]), w = mk3(P[15], P[16], P[17]), v = mk3(P[18], P[19], P[20]);
+    const f3 al = mk3(P[21], P[22], P[23]), ac = mk3(P[24], P[25], P[26]);
+    const float m = TD.mass[b];
+    float I6[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) I6[i] = TD.inertia[b][i];
+    const s6 Iw = rotate_inertia(Rm, I6);
+    const f3 r = c - O;
+    const float rr = dot3(r, r);
+    const f3 Iww = mul(Iw, w);
+    const f3 f = m * (ac - mk3(0, 0, -g)) + (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v))) * v;
+    const f3 n = mul(Iw, al) + cross3(w, Iww) + ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w)) * Iww;
+    const f3 pr = m * r, Nn = n + cross3(r, f);
+    const float cmp[G::CW] = {Iw.a[0] + m * (rr - r.x * r.x), Iw.a[1] + m * (rr - r.y * r.y), Iw.a[2] + m * (rr - r.z * r.z),
+                              Iw.a[3] - m * r.x * r.y, Iw.a[4] - m * r.x * r.z, Iw.a[5] - m * r.y * r.z,
+                              pr.x, pr.y, pr.z, f.x, f.y, f.z, Nn.x, Nn.y, Nn.z, m};
+    lds_float* C = X.l + G::O_CP + G::CW * b;
+    const bool massive = m > 0.f;
+#pragma unroll
+    for (int i = 0; i < G::CW; i++) C[i] = massive ? cmp[i] : 0.f;
+  }
+#pragma unroll 1
+  for (int i = X.t; i < N; i += T) {
+    const int d = TD.g_dof[i];
+    f3 sw, sv;
+    if (d >= 0) {
+      const f3 a = mk3(X.l[G::O_JA + 3 * d], X.l[G::O_JA + 3 * d + 1], X.l[G::O_JA + 3 * d + 2]);
+      const f3 o = mk3(X.l[G::O_JO + 3 * d], X.l[G::O_JO + 3 * d + 1], X.l[G::O_JO + 3 * d + 2]);
+      const bool rev = TD.jt[TD.g_body[i]] == 0;
+      sw = rev ? a : mk3(0, 0, 0);
+      sv = rev ? cross3(o - O, a) : a;
+    } else {
+      const int kk = i - R::NJ;  // 0..2 linear, 3..5 angular
+      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
+      sw = kk < 3 ? mk3(0, 0, 0) : e;
+      sv = kk < 3 ? e : mk3(0, 0, 0);
+    }
+    X.l[G::O_SW + 3 * i] = sw.x; X.l[G::O_SW + 3 * i + 1] = sw.y; X.l[G::O_SW + 3 * i + 2] = sw.z;
+    X.l[G::O_SV + 3 * i] = sv.x; X.l[G::O_SV + 3 * i + 1] = sv.y; X.l[G::O_SV + 3 * i + 2] = sv.z;
+  }
+  PBG_GANG_SYNC
+  // composites: leaf-to-root over the levels (a body adds its children's sums)
+  static_for<0, NLEV - 1>([&](auto k_c) {
+    constexpr int lv = NLEV - 2 - decltype(k_c)::value;
+#pragma unroll 1
+    for (int idx = TD.lev_start[lv] + X.t; idx < TD.lev_start[lv + 1]; idx += T) {
+      const int b = TD.lev_body[idx];
+      lds_float* C = X.l + G::O_CP + G::CW * b;
+      float acc[G::CW];
+#pragma unroll
+      for (int i = 0; i < G::CW; i++) acc[i] = C[i];
+#pragma unroll 1
+      for (int j = TD.child_start[b]; j < TD.child_start[b + 1]; j++) {
+        const lds_float* K = X.l + G::O_CP + G::CW * TD.child[j];
+#pragma unroll
+        for (int i = 0; i < G::CW; i++) acc[i] += K[i];
+      }
+#pragma unroll
+      for (int i = 0; i < G::CW; i++) C[i] = acc[i];
+    }
+    PBG_GANG_SYNC
+  });
+  // packed lower triangle of M, then the bias (C_i = s_i . (N, F) of its composite)
+#pragma unroll 1
+  for (int j = X.t; j < D::NNZ + N; j += T) {
+    if (j < D::NNZ) {
+      const int gi = TD.me_i[j], gk = TD.me_k[j], bk = TD.me_b[j];
+      const lds_float* C = X.l + G::O_CP + G::CW * bk;
+      s6 J;
+#pragma unroll
+      for (int i = 0; i < 6; i++) J.a[i] = C[i];
+      const f3 p1 = mk3(C[6], C[7], C[8]);
+      const float cm = C[15];
+      const f3 swk = mk3(X.l[G::O_SW + 3 * gk], X.l[G::O_SW + 3 * gk + 1], X.l[G::O_SW + 3 * gk + 2]);
+      const f3 svk = mk3(X.l[G::O_SV + 3 * gk], X.l[G::O_SV + 3 * gk + 1], X.l[G::O_SV + 3 * gk + 2]);
+      const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
+      const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
+      const f3 Jw_ = mul(J, swk) + cross3(p1, svk);
+      const f3 Fv = cm * svk - cross3(p1, swk);
+      X.l[G::O_L + j] = (dot3(swi, Jw_) + dot3(svi, Fv)) + TD.me_arm[j];
+    } else {
+      const int gi = j - D::NNZ, bi = TD.g_body[gi], d = TD.g_dof[gi];
+      const lds_float* C = X.l + G::O_CP + G::CW * bi;
+      const f3 F = mk3(C[9], C[10], C[11]), Nn = mk3(C[12], C[13], C[14]);
+      const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
+      const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
+      float r = -(dot3(swi, Nn) + dot3(svi, F));
+      if (d >= 0) r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
+      X.l[G::O_RHS + gi] = r;
+    }
+  }
+  PBG_GANG_SYNC
+}
+
+// ------------------------------------------------------------------ one physics sub-step
+template <class R, int T, bool DIST>
 PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits SUB_STAMP_ARGS) {
   using D = Dims<R>;
   using G = Gang<R, T>;
-  const GangTab<R>& TB = g_gang_tab<R>;
+  auto& TB = GangTabs<R>::tab(X.tabs);
   constexpr int N = R::NDOF, NB = D::NB, NLIM = D::NLIM, NSL = G::NSL, YS = G::YS;
   constexpr float inv_dt = (float)(1.0 / R::dt_sub);
   const bool w0 = X.t == 0;  // the gang's writer for replicated values
-  f3 O;
-  // --- replicated: unconstrained dynamics, staged into the gang's LDS -------------------
-  {
-    float L[D::NNZ], Ld[N], nu[N], u[N];
-    dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
-    STAMP(3)
+  auto stage_solution = [&](const float* L, const float* Ld, const float* u) {
     if (w0) {
 #pragma unroll
       for (int i = 0; i < D::NNZ; i++) X.l[G::O_L + i] = L[i];
@@ -204,24 +513,6 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       for (int i = 0; i < N; i++) { X.l[G::O_LD + i] = Ld[i]; X.l[G::O_U + i] = u[i]; }
 #pragma unroll
       for (int i = N; i < YS; i++) X.l[G::O_U + i] = 0.f;
-    }
-  }
-  {
-    Kin<R> k;
-    f3 sw[N], sv[N];
-    kin_motion<R>(s, k, sw, sv, O);
-    if (w0) {
-#pragma unroll
-      for (int i = 0; i < N; i++) {
-        X.l[G::O_SW + 3 * i] = sw[i].x; X.l[G::O_SW + 3 * i + 1] = sw[i].y; X.l[G::O_SW + 3 * i + 2] = sw[i].z;
-        X.l[G::O_SV + 3 * i] = sv[i].x; X.l[G::O_SV + 3 * i + 1] = sv[i].y; X.l[G::O_SV + 3 * i + 2] = sv[i].z;
-      }
-#pragma unroll
-      for (int b = 0; b < NB; b++) {
-#pragma unroll
-        for (int i = 0; i < 9; i++) X.l[G::O_FR + 12 * b + i] = k.Rm[b].m[i];
-        X.l[G::O_FR + 12 * b + 9] = k.x[b].x; X.l[G::O_FR + 12 * b + 10] = k.x[b].y; X.l[G::O_FR + 12 * b + 11] = k.x[b].z;
-      }
       static_for<0, NLIM>([&](auto li_c) {
         constexpr int li = decltype(li_c)::value;
         constexpr int d = D::LIM.v[li][0];
@@ -229,11 +520,52 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         X.l[G::O_LP + 2 * li + 1] = (float)R::dof_upper[d] - s.q[d];
       });
     }
+  };
+  if constexpr (DIST) {
+    // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
+    gang_dyn_mass<R, T>(s, X);
+    STAMP(3)
+    // --- replicated: factorisation and the unconstrained velocity, staged for the rows ---
+    float L[D::NNZ], rhs[N], Ld[N], nu[N], u[N];
+#pragma unroll
+    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+#pragma unroll
+    for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
+    dyn_solve<R>(s, L, rhs, Ld, nu, u);
+    stage_solution(L, Ld, u);
+  } else {
+    // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
+    {
+      float L[D::NNZ], Ld[N], nu[N], u[N];
+      dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
+      STAMP(3)
+      stage_solution(L, Ld, u);
+    }
+    Kin<R> k;
+    f3 sw[N], sv[N], O0;
+    kin_motion<R>(s, k, sw, sv, O0);
+    if (w0) {
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        X.l[G::O_SW + 3 * i] = sw[i].x; X.l[G::O_SW + 3 * i + 1] = sw[i].y; X.l[G::O_SW + 3 * i + 2] = sw[i].z;
+        X.l[G::O_SV + 3 * i] = sv[i].x; X.l[G::O_SV + 3 * i + 1] = sv[i].y; X.l[G::O_SV + 3 * i + 2] = sv[i].z;
+      }
+#pragma unroll
+      for (int b = 0; b < D::NB; b++) {
+        lds_float* p = X.l + G::O_FR + G::BW * b;
+#pragma unroll
+        for (int i = 0; i < 9; i++) p[i] = k.Rm[b].m[i];
+        p[9] = k.x[b].x; p[10] = k.x[b].y; p[11] = k.x[b].z;
+        p[12] = k.c[b].x; p[13] = k.c[b].y; p[14] = k.c[b].z;
+      }
+    }
   }
+  PBG_GANG_SYNC
+  const f3 O = gang_O<R, T>(X);
   PBG_GANG_SYNC
   STAMP(10)
   auto frame = [&](int b, m3& Rm, f3& x) {
-    const lds_float* p = X.l + G::O_FR + 12 * b;
+    const lds_float* p = X.l + G::O_FR + G::BW * b;
 #pragma unroll
     for (int i = 0; i < 9; i++) Rm.m[i] = p[i];
     x = mk3(p[9], p[10], p[11]);
@@ -490,18 +822,30 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   return nc;
 }
 
-template <class R, int T>
-__global__ __launch_bounds__(64) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
+template <class R, int T, bool DIST>
+__global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
   extern __shared__ float lds_dyn[];
   using G = Gang<R, T>;
-  constexpr int EPW = 64 / T;
+  using TT = GangTabs<R>;
+  constexpr int EPB = PBG_GANG_BLOCK / T;  // envs per workgroup
+  lds_float* lds = (lds_float*)lds_dyn;
+  {
+    const uint32_t* src0 = (const uint32_t*)&g_gang_tab<R>;
+    const uint32_t* src1 = (const uint32_t*)&g_gang_dyn<R>;
+    __attribute__((address_space(3))) uint32_t* dst = (__attribute__((address_space(3))) uint32_t*)lds;
+    for (int i = threadIdx.x; i < (int)(sizeof(GangTab<R>) / 4); i += PBG_GANG_BLOCK) dst[i] = src0[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(GangDynTab<R>) / 4); i += PBG_GANG_BLOCK) dst[TT::TAB_WORDS + i] = src1[i];
+  }
+  __syncthreads();
   GangCtx X;
+  X.tabs = lds;
   X.t = threadIdx.x % T;
   X.le = threadIdx.x / T;
-  const int e = blockIdx.x * EPW + X.le;
-  if (e >= B.n) return;  // whole gangs only
-  X.l = (lds_float*)lds_dyn + X.le * env_words;
+  const int e = blockIdx.x * EPB + X.le;
+  if (e >= B.n) return;  // whole gangs only (no workgroup barrier below)
+  X.le &= 64 / T - 1;     // gang within the wave (ballot masks)
+  X.l = lds + TT::WORDS + (threadIdx.x / T) * env_words;
   X.g = scratch + (size_t)e * G::GWORDS;
   X.cap = cap;
   const bool w0 = X.t == 0;
@@ -520,10 +864,14 @@ __global__ __launch_bounds__(64) void gang_step_kernel(Buffers B, StepIO io, flo
     const float c = fminf(fmaxf(act[i], -1.f), 1.f);
     tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
   }
+  if (w0) {
+#pragma unroll
+    for (int d = 0; d < R::NJ; d++) X.l[G::O_TAU + d] = tau[d];
+  }
   uint64_t slot_bits = 0;
   int nc = 0;
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = gang_substep<R, T>(s, tau, X, slot_bits SUB_STAMP_PASS);
+  for (int sub = 0; sub < R::substeps; sub++) nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits SUB_STAMP_PASS);
   if (io.ncontact && w0) io.ncontact[e] = nc;
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];

@@ -17,6 +17,7 @@ struct Geometry {
   int block;         // lanes per step workgroup: 16, 32 or 64
   int lds_rows;      // contact-constraint rows (gang: contacts) resident in LDS per env
   int env_words;     // gang: LDS words per env
+  int gang_dist;     // gang: distributed (1) or replicated (0) unconstrained dynamics
   size_t lds_bytes;  // dynamic LDS per step workgroup
   size_t scratch_words_per_env;
 };

@@ -1,6 +1,7 @@
 // pbg_robot.hip -- per-robot kernel instantiations + launchers.  Compiled once per robot
 // with -DPBG_ROBOT=<Pendulum|Hopper|HalfCheetah|Ant|Humanoid>.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "pbg_launch.h"
 #include "pbg_step.hip"
@@ -73,22 +74,27 @@ template <class RR>
 static int plan_gang(int n_envs, int cus, Geometry* g) {
   if constexpr (RR::kind == 0) {
     using G = Gang<RR, 16>;
-    constexpr int EPW = 4;
-    const int wgs = (n_envs + EPW - 1) / EPW;
+    constexpr int EPB = PBG_GANG_BLOCK / 16;  // envs per workgroup
+    const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
-    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
-    long words = (long)(budget / ((size_t)EPW * sizeof(float))) - G::FIXED;
+    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1) - sizeof(float) * GangTabs<RR>::WORDS;
+    long words = (long)(budget / ((size_t)EPB * sizeof(float))) - G::FIXED;
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
+    // distributed dynamics for deep trees (Humanoid) or more than one wave per SIMD (its
+    // smaller register footprint lets two waves share a SIMD); replicated otherwise
+    g->gang_dist = RR::NDOF >= 16 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
+    const char* dist_env = getenv("PBG_GANG_DIST");  // tests: force either variant
+    if (dist_env && (dist_env[0] == '0' || dist_env[0] == '1')) g->gang_dist = dist_env[0] == '1';
     g->team = 16;
-    g->block = 64;
+    g->block = PBG_GANG_BLOCK;
     g->lds_rows = cap;
     g->env_words = G::FIXED + cap * G::PERC;
-    g->lds_bytes = (size_t)EPW * sizeof(float) * (size_t)g->env_words;
+    g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
     g->scratch_words_per_env = G::GWORDS;
-    return (int)hipFuncSetAttribute((const void*)gang_step_kernel<RR, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)g->lds_bytes);
+    const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;
+    return (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
   } else {
     (void)n_envs; (void)cus; (void)g;
     return (int)hipErrorInvalidValue;
@@ -98,8 +104,11 @@ template <class RR>
 static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if constexpr (RR::kind == 0) {
     if (g.team != 16) return false;
-    hipLaunchKernelGGL((gang_step_kernel<RR, 16>), dim3(blocks(B.n, 4)), dim3(64), g.lds_bytes, s, B, io, scratch,
-                       g.lds_rows, g.env_words);
+    const dim3 grid(blocks(B.n, PBG_GANG_BLOCK / 16)), blk(PBG_GANG_BLOCK);
+    if (g.gang_dist)
+      hipLaunchKernelGGL((gang_step_kernel<RR, 16, true>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
+    else
+      hipLaunchKernelGGL((gang_step_kernel<RR, 16, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
     return true;
   } else {
     (void)B; (void)io; (void)scratch; (void)g; (void)s;

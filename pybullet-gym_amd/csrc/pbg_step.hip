@@ -441,10 +441,9 @@ PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, f3* sw, f3* sv, f3& O) {
 // matrix and bias, its sparse Cholesky factor L (Ld = 1/diag), the predicted velocity
 // nu = clamp(nu + dt M^-1 (tau - C)) and u = L^T nu.  Shared by the lane and gang kernels.
 template <class R>
-PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u SUB_STAMP_ARGS) {
+PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
-  constexpr float dt = (float)R::dt_sub;
   constexpr float g = (float)PBG_GRAVITY;
 
   // --- phase A: one forward pass over the bodies: kinematics, velocities, bias
@@ -569,7 +568,6 @@ PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, 
 
   STAMP(0)
   // --- mass matrix (lower triangle, gi >= gk) and bias -----------------------------------
-  float rhs[N];
   {
   f3 sw[N], sv[N];
   motion_vectors<R>(ja, jo, O, sw, sv);
@@ -598,9 +596,16 @@ PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, 
     L[D::lidx(D::gj(d), D::gj(d))] += (float)R::dof_armature[d];
     rhs[D::gj(d)] += tau[d] - (float)R::dof_damping[d] * s.qd[d];
   }
-
   STAMP(1)
-  // --- Cholesky (no fill-in in leaf-first order); Ld = 1 / diag(L) ----------------------
+}
+
+// Cholesky of the mass matrix held in L (in place, no fill-in in leaf-first order; Ld =
+// 1 / diag(L)), nu = clamp(nu + dt M^-1 rhs), u = L^T nu.
+template <class R>
+PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld, float* nu, float* u) {
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ, N = R::NDOF;
+  constexpr float dt = (float)R::dt_sub;
 #pragma unroll
   for (int j = 0; j < N; j++) {
     float sjj = L[D::lidx(j, j)];
@@ -661,6 +666,13 @@ PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, 
       if (D::coupled(kk, i)) t += L[D::lidx(kk, i)] * nu[kk];
     u[i] = t;
   }
+}
+
+template <class R>
+PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u SUB_STAMP_ARGS) {
+  float rhs[R::NDOF];
+  dyn_mass<R>(s, tau, L, rhs SUB_STAMP_PASS);
+  dyn_solve<R>(s, L, rhs, Ld, nu, u);
 }
 
 // nu = L^-T u, clamp, semi-implicit Euler (exponential-map base rotation).  nu: scratch.

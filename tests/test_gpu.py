@@ -344,11 +344,14 @@ def _variant_vs_lane(monkeypatch, env_id, n, steps, variant_env, seed=3):
 
 @pytest.mark.parametrize("env_id,variant", [("HumanoidPyBulletEnv-v0", {}), ("HopperPyBulletEnv-v0", {}),
                                             ("HalfCheetahPyBulletEnv-v0", {}), ("Walker2DPyBulletEnv-v0", {}),
-                                            ("AntPyBulletEnv-v0", {"PBG_TEAM": "2"})])
+                                            ("AntPyBulletEnv-v0", {"PBG_TEAM": "2"}),
+                                            ("HumanoidPyBulletEnv-v0", {"PBG_GANG_DIST": "0"}),
+                                            ("Walker2DPyBulletEnv-v0", {"PBG_GANG_DIST": "1"})])
 def test_gang_kernel_matches_lane_kernel_teacher_forced(monkeypatch, env_id, variant):
-    """16-lanes-per-env gang kernel vs the one-lane-per-env kernel from the same states:
-    same physics and row order, different float32 summation order (DPP tree dots) and
-    constant-table transforms.  Tolerances as for the oracle comparison: done identical,
+    """16-lanes-per-env gang kernel (distributed or replicated dynamics) vs the
+    one-lane-per-env kernel from the same states: same physics and row order, different
+    float32 summation order (DPP tree dots, level-order composites) and constant-table
+    transforms.  Tolerances as for the oracle comparison: done identical,
     contacts identical in >= 99.9 %, median obs error <= 1e-4, 99th percentile <= 1e-2."""
     n, steps = 256, 30
     lanes, e, cmis = _variant_vs_lane(monkeypatch, env_id, n, steps, variant)
