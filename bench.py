@@ -27,7 +27,7 @@ ENVS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SHORT = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
          "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
-         "HumanoidPyBulletEnv-v0": "humanoid"}
+         "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d"}
 
 
 def alg_bytes_per_env_step(info):
@@ -75,6 +75,87 @@ def load_pmc(env_id, n):
     return d if d.get("envs") == n else None
 
 
+def valu_roofline(pmc, kernel_ms, n):
+    """VALU issue roofline (the binding one): wave64 VALU instructions per
+    launch (PMC SQ_INSTS_VALU) / the kernel's HIP-event time, against the chip's issue
+    peak: 256 CUs x 4 SIMDs x one wave64 VALU op per 2 cycles at 2.4 GHz."""
+    peak = 256 * 4 * 2.4e9 / 2 / 1e12
+    ach = pmc["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e12
+    return {"achieved": ach, "peak": peak, "unit": "T wave-instr/s", "frac": ach / peak,
+            "valu_instr_per_env": pmc["valu_insts_per_launch"] * 64 / n,
+            "source": "profiles/" + os.path.basename(pmc.get("_path", "pmc"))}
+
+
+def kernel_name(env):
+    lpe = env.info.lanes_per_env
+    k = {1: "pbg::step_kernel", 4: "pbg::team_step_kernel", 16: "pbg::gang_step_kernel"}.get(lpe, "pbg::step_kernel")
+    return f"{k}<{env.env_id}>"
+
+
+def timed_rollout(VecEnv, env_id, n, steps, warmup, dev, rank, world, no_graph):
+    """Random-action rollout of n envs on this GPU: warmup steps, per-launch kernel time
+    (HIP events on the launch stream), then exactly `steps` steps bracketed by a barrier +
+    device sync on both sides; returns (env, elapsed_s max over ranks, kernel_ms, G)."""
+    import torch
+    import torch.distributed as dist
+    env = VecEnv(env_id, n, device=dev, seed=0x5EED, env_offset=rank * n, autoreset=True)
+    env.reset()
+    na = env.info.action_dim
+    total = warmup + steps
+    pool = min(total, 256)  # distinct pre-generated action batches, cycled
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    acts = torch.rand((pool, n, na), device=dev, generator=g, dtype=torch.float32) * 2 - 1
+
+    for i in range(warmup):
+        env.step(acts[i % pool])
+    stream = torch.cuda.current_stream(dev)
+    # timed region: the K steps as HIP-graph replays of G captured steps (G divides K)
+    G = 1
+    if not no_graph:
+        G = max(d for d in range(1, min(64, steps) + 1) if steps % d == 0)
+        graph = env.capture([acts[j % pool] for j in range(G)])
+    # per-launch kernel time (roofline.kernel_ms), HIP events on the launch stream: around
+    # graph replays (back-to-back kernels) or, with --no-graph, around single launches
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if no_graph:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(100)]
+        for i in range(100):
+            ev[i][0].record(stream)
+            env.step(acts[(warmup + i) % pool])
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / 100
+    else:
+        reps = max(1, 200 // G)
+        e0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        kernel_ms = e0.elapsed_time(e1) / (reps * G)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if no_graph:
+        for i in range(steps):
+            env.step(acts[(warmup + i) % pool])
+    else:
+        for _ in range(steps // G):
+            graph.replay()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+    return env, elapsed, kernel_ms, G
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +166,8 @@ def main():
     ap.add_argument("--gather", action="store_true", help="also time the RCCL obs all-gather (separately)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
+    ap.add_argument("--second-env", default="HumanoidPyBulletEnv-v0", help="second workload of the metric ('none' = off)")
+    ap.add_argument("--second-envs-per-gpu", type=int, default=4096)
     args = ap.parse_args()
 
     import torch
@@ -103,62 +186,29 @@ def main():
     from pybulletgym_amd.vec_env import VecEnv
 
     n = args.envs_per_gpu
-    env = VecEnv(args.env, n, device=dev, seed=0x5EED, env_offset=rank * n, autoreset=True)
-    env.reset()
-    na = env.info.action_dim
-    total = args.warmup + args.steps
-    pool = min(total, 256)  # distinct pre-generated action batches, cycled (256 x 512 KB)
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    acts = torch.rand((pool, n, na), device=dev, generator=g, dtype=torch.float32) * 2 - 1
-
-    for i in range(args.warmup):
-        env.step(acts[i % pool])
-    stream = torch.cuda.current_stream(dev)
-    # timed region: the K steps as HIP-graph replays of G captured steps (G divides K)
-    G = 1
-    if not args.no_graph:
-        G = max(d for d in range(1, min(64, args.steps) + 1) if args.steps % d == 0)
-        graph = env.capture([acts[j % pool] for j in range(G)])
-    # per-launch kernel time (roofline.kernel_ms), HIP events on the launch stream: around
-    # graph replays (back-to-back kernels) or, with --no-graph, around single launches
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n_ev = 0
-    if args.no_graph:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(100)]
-        for i in range(100):
-            ev[i][0].record(stream)
-            env.step(acts[(args.warmup + i) % pool])
-            ev[i][1].record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / 100
-    else:
-        reps = max(1, 200 // G)
-        e0.record(stream)
-        for _ in range(reps):
-            graph.replay()
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = e0.elapsed_time(e1) / (reps * G)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if args.no_graph:
-        for i in range(args.steps):
-            env.step(acts[(args.warmup + i) % pool])
-    else:
-        for _ in range(args.steps // G):
-            graph.replay()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+    env, elapsed, kernel_ms, G = timed_rollout(VecEnv, args.env, n, args.steps, args.warmup, dev, rank, world,
+                                               args.no_graph)
+    second = None
+    if args.second_env not in ("", "none") and args.second_env != args.env:
+        # BASELINE metric names Ant + Humanoid: the Humanoid config (32,768 envs on 8 GPUs =
+        # 4,096 per GPU, BASELINE.json configs[4]) timed the same way, reported beside `value`
+        n2 = args.second_envs_per_gpu
+        steps2 = max(1, min(args.steps, 200))
+        env2, el2, km2, G2 = timed_rollout(VecEnv, args.second_env, n2, steps2, min(args.warmup, 20), dev, rank,
+                                           world, args.no_graph)
+        second = {"env": args.second_env, "envs_per_gpu": n2, "global_envs": world * n2, "steps": steps2,
+                  "value": world * n2 * steps2 / el2, "unit": "env-steps/s", "ms_per_step": el2 / steps2 * 1e3,
+                  "kernel": kernel_name(env2), "kernel_ms": km2, "lanes_per_env": env2.info.lanes_per_env,
+                  "obs_finite": bool(torch.isfinite(env2.obs).all())}
+        alg2 = alg_bytes_per_env_step(env2.info)
+        ach2 = alg2 * n2 / (km2 * 1e-3) / 1e9
+        pmc2 = load_pmc(args.second_env, n2)
+        second["roofline"] = {"bound": "hbm", "achieved": ach2, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": ach2 / HBM_PEAK_GBS, "traffic": pmc2.get("hbm_bytes_per_launch") if pmc2 else None,
+                              "alg_bytes_per_env_step": alg2}
+        if pmc2 and pmc2.get("valu_insts_per_launch"):
+            second["valu_roofline"] = valu_roofline(pmc2, km2, n2)
+        env2.close()
 
     gather_ms = None
     if args.gather and world > 1:
@@ -199,20 +249,14 @@ def main():
                        "lanes_per_env": env.info.lanes_per_env},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("pbg::team_step_kernel" if env.info.lanes_per_env == 4 else "pbg::step_kernel")
-                                   + f"<{args.env}>", "kernel_ms": kernel_ms,
+                         "kernel": kernel_name(env), "kernel_ms": kernel_ms,
                          "alg_bytes_per_env_step": alg},
             "obs_finite": finite,
         }
         if pmc and pmc.get("valu_insts_per_launch"):
-            # VALU issue roofline (the binding one): wave64 VALU instructions per
-            # launch (PMC SQ_INSTS_VALU) / the kernel's HIP-event time, against the chip's
-            # issue peak: 256 CUs x 4 SIMDs x one wave64 VALU op per 2 cycles at 2.4 GHz.
-            peak = 256 * 4 * 2.4e9 / 2 / 1e12
-            ach = pmc["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e12
-            out["valu_roofline"] = {"achieved": ach, "peak": peak, "unit": "T wave-instr/s", "frac": ach / peak,
-                                    "valu_instr_per_env": pmc["valu_insts_per_launch"] * 64 / n,
-                                    "source": "profiles/" + os.path.basename(pmc.get("_path", "pmc"))}
+            out["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)
+        if second is not None:
+            out["humanoid" if "Humanoid" in second["env"] else "second"] = second
         if gather_ms is not None:
             out["allgather_obs_ms"] = gather_ms
         if world == 1 and not args.no_cpu_baseline:

@@ -1,6 +1,7 @@
 #!/bin/bash
 # bench + rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE; WRITE_SIZE; SQ
-# instruction/cycle counters).  usage: tools/gpu_bench_prof.sh TAG [bench args...]
+# instruction/cycle counters; VALU op mix) for the two metric workloads (Ant 16,384 envs and
+# Humanoid 4,096 envs).  usage: tools/gpu_bench_prof.sh TAG [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
@@ -10,10 +11,13 @@ mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
-B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- $B > $OUT/pmc_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- $B > $OUT/pmc_write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sq -o run -- $B > $OUT/pmc_sq.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 --output-format csv -d $OUT/pmc_flops -o run -- $B > $OUT/pmc_flops.log 2>&1
+for W in ant humanoid; do
+  if [ $W = ant ]; then A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384"; else A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096"; fi
+  B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline --second-env none $A"
+  timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$W/pmc_fetch -o run -- $B > $OUT/$W.pmc_fetch.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$W/pmc_write -o run -- $B > $OUT/$W.pmc_write.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/$W/pmc_sq -o run -- $B > $OUT/$W.pmc_sq.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 --output-format csv -d $OUT/$W/pmc_flops -o run -- $B > $OUT/$W.pmc_flops.log 2>&1
+done
 echo done

@@ -1,6 +1,7 @@
 """Summarise the rocprofv3 passes of tools/gpu_bench_prof.sh into profiles/ (dev tool).
 
 usage: python tools/pmc_summary.py gpurun_out/TAG ROUND ROBOT ENVS
+(PMC passes under gpurun_out/TAG/ROBOT/, the kernel trace under gpurun_out/TAG/trace/)
 writes profiles/ROUND_{kernel_stats,pmc_*}_<robot><envs/1024>k.csv copies and
 profiles/pmc_step_<robot>.json (per-launch medians of the step kernel), which bench.py
 reads for roofline.traffic and valu_roofline.
@@ -17,6 +18,13 @@ src, rnd, robot, envs = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(REPO, "profiles")
 tag = f"{robot}{envs // 1024}k"
+STRUCT = {"ant": "Ant", "humanoid": "Humanoid", "hopper": "Hopper", "halfcheetah": "HalfCheetah",
+          "walker2d": "Walker2D", "pendulum": "Pendulum"}[robot]
+KEY = f"pbg_models::{STRUCT}"
+
+
+def is_step(name):
+    return "step_kernel" in name and KEY in name
 
 
 def counter_csv(d):
@@ -28,16 +36,16 @@ def medians(path):
     per = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "step_kernel" not in r["Kernel_Name"]:
+            if not is_step(r["Kernel_Name"]):
                 continue
             per.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
             per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: statistics.median(v.values()) for k, v in per.items()}
 
 
-out = {"kernel": "pbg::step_kernel", "robot": robot, "envs": envs, "round": rnd}
+out = {"kernel": "pbg::*step_kernel<" + KEY + ">", "robot": robot, "envs": envs, "round": rnd}
 for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops"):
-    p = counter_csv(d)
+    p = counter_csv(os.path.join(robot, d))
     if not p:
         continue
     shutil.copy(p, os.path.join(prof, f"{rnd}_{d}_{tag}.csv"))
@@ -47,7 +55,7 @@ if st:
     shutil.copy(st[0], os.path.join(prof, f"{rnd}_kernel_stats_{tag}.csv"))
     with open(st[0]) as f:
         for r in csv.DictReader(f):
-            if "step_kernel" in r["Name"]:
+            if is_step(r["Name"]):
                 out["trace_avg_ns"] = float(r["AverageNs"])
                 out["trace_calls"] = int(r["Calls"])
 if "FETCH_SIZE_median" in out and "WRITE_SIZE_median" in out:
