@@ -48,7 +48,7 @@ int g_flags = 0;
 // ------------------------------------------------------------------ model view
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
-      floor, max_steps, robot_body;
+      floor, max_steps, robot_body, tip_link;
   double power, elec, stall, jal, z0fixed, dt_sub, base_mass;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
@@ -57,7 +57,7 @@ struct MV {
   const double *lower, *upper, *damping, *armature;
   const int *limited, *dof_jtype;
   const int* act_dof; const double* act_gain;
-  const int* obs_dof; const double* obs_vel_scale; const int* reset_dof;
+  const int* obs_dof; const double* obs_vel_scale; const int* reset_dof; const double* reset_offset;
   const int* part_link; const int* foot_link;
   const int* slot_link; const double (*slot_point)[3]; const double *slot_radius, *slot_mu;
   const int *pair_a, *pair_b; const double (*pa0)[3], (*pa1)[3], (*pb0)[3], (*pb1)[3];
@@ -70,7 +70,7 @@ MV view() {
   m.robot_id = R::robot_id; m.kind = R::kind; m.floating = R::floating; m.NL = R::NL; m.NJ = R::NJ;
   m.NDOF = R::NDOF; m.NA = R::NA; m.NO = R::NO; m.NR = R::NR; m.NF = R::NF; m.NP = R::NP;
   m.NS = R::NS; m.NPAIR = R::NPAIR; m.OBS = R::OBS; m.alive = R::alive; m.substeps = R::substeps;
-  m.floor = R::floor; m.max_steps = R::max_episode_steps; m.robot_body = R::robot_body;
+  m.floor = R::floor; m.max_steps = R::max_episode_steps; m.robot_body = R::robot_body; m.tip_link = R::tip_link;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
   m.base_mass = R::base_mass; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
@@ -81,6 +81,7 @@ MV view() {
   m.damping = R::dof_damping; m.armature = R::dof_armature; m.limited = R::dof_limited;
   m.dof_jtype = R::dof_jtype; m.act_dof = R::act_dof; m.act_gain = R::act_gain;
   m.obs_dof = R::obs_dof; m.obs_vel_scale = R::obs_vel_scale; m.reset_dof = R::reset_dof;
+  m.reset_offset = R::reset_offset;
   m.part_link = R::part_link; m.foot_link = R::foot_link; m.slot_link = R::slot_link;
   m.slot_point = R::slot_point; m.slot_radius = R::slot_radius; m.slot_mu = R::slot_mu;
   m.pair_a = R::pair_link_a; m.pair_b = R::pair_link_b; m.pa0 = R::pair_a0; m.pa1 = R::pair_a1;
@@ -89,10 +90,11 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[6] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[8] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                         view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
-                        view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>()};
-  if (robot < 0 || robot > 5) return nullptr;
+                        view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
+                        view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>()};
+  if (robot < 0 || robot > 7) return nullptr;
   return &views[robot];
 }
 
@@ -674,8 +676,8 @@ int pbg_oracle_info(int robot, int* out) {
   return 0;
 }
 
-static void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, double* rew,
-                         uint8_t* done);
+static void pendulum_obs(const MV& m, const double* jq, const double* jqd, const double* tip, float* obs,
+                         double* rew, uint8_t* done);
 
 // Walker pack: calc_state (robot_locomotors.py:31-64) + the reward/done part of
 // WalkerBaseBulletEnv._step (gym_locomotion_envs.py:59-114).  With act == NULL only the
@@ -684,8 +686,8 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  if (m.kind == 1) {  // pendulum: jq/jqd = (hinge, slider)
-    pendulum_obs(in->jq[0], in->jqd[0], in->jq[1], in->jqd[1], out->obs, &out->reward, &out->done);
+  if (m.kind == 1) {  // pendulums: jq/jqd = (hinge, [hinge2,] slider), pos = pole2 position
+    pendulum_obs(m, in->jq, in->jqd, in->body_pos, out->obs, &out->reward, &out->done);
     if (!in->act) { out->reward = 0; out->done = 0; }
     return 0;
   }
@@ -777,23 +779,48 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   return 0;
 }
 
-// Pendulum pack: calc_state + reward/done (robot_pendula.py:27-51, gym_pendulum_envs.py:26-39).
-// obs is float64 in the reference; written here as float32 (the C-ABI's obs dtype).
-static void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, double* rew,
-                         uint8_t* done) {
-  // robot_pendula.py:32-46: non-finite vx / theta / theta_dot are replaced by 0
+// Pendulum packs: calc_state + reward/done.  obs is float64 in the reference; written here
+// as float32 (the C-ABI's obs dtype).
+//  * InvertedPendulum / Swingup (robot_pendula.py:27-51, gym_pendulum_envs.py:26-39): non-finite
+//    vx / theta / theta_dot are replaced by 0 (:32-46); balance: reward 1, done |theta| > .2;
+//    swingup: reward cos(theta), never done.
+//  * InvertedDoublePendulum (robot_pendula.py:76-88, gym_pendulum_envs.py:69-80): obs
+//    [x, vx, pole2 x, cos th, sin th, th', cos g, sin g, g']; reward = sum([10, -dist_penalty, -0]),
+//    dist_penalty = 0.01 x2^2 + (y2 + 0.3 - 2)^2 with (x2, _, y2) = pole2.pose().xyz();
+//    done = y2 + 0.3 <= 1.
+static void pendulum_obs(const MV& m, const double* jq, const double* jqd, const double* tip, float* obs,
+                         double* rew, uint8_t* done) {
+  if (m.alive == 6) {
+    const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
+    const double px = tip[0], py = tip[2];
+    const double o[9] = {x, vx, px, cos(th), sin(th), thd, cos(g), sin(g), gd};
+    for (int i = 0; i < 9; i++) obs[i] = (float)o[i];
+    const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
+    if (rew) *rew = ((0.0 + 10.0) + -dist_penalty) + 0.0;
+    if (done) *done = py + 0.3 <= 1;
+    return;
+  }
+  double theta = jq[0], theta_dot = jqd[0], x = jq[1], vx = jqd[1];
   if (!isfinite(vx)) vx = 0.0;
   if (!isfinite(theta)) theta = 0.0;
   if (!isfinite(theta_dot)) theta_dot = 0.0;
   obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
   obs[4] = (float)theta_dot;
-  if (rew) *rew = 1.0;
-  if (done) *done = fabs(theta) > 0.2;
+  if (rew) *rew = m.alive == 5 ? cos(theta) : 1.0;
+  if (done) *done = m.alive == 5 ? 0 : fabs(theta) > 0.2;
 }
-static void pendulum_pack(const double* s, float* obs, double* rew, uint8_t* done) {
+static void pendulum_pack(const MV& m, const double* s, float* obs, double* rew, uint8_t* done) {
   const double* q = s + PBG_BASE_WORDS;
-  const double* qd = q + 2;
-  pendulum_obs(q[1], qd[1], q[0], qd[0], obs, rew, done);
+  const double* qd = q + m.NJ;
+  double jq[MAXD], jqd[MAXD], tip[3] = {0, 0, 0};
+  for (int i = 0; i < m.NO; i++) { jq[i] = q[m.obs_dof[i]]; jqd[i] = qd[m.obs_dof[i]]; }
+  if (m.tip_link >= 0) {
+    static thread_local Kin k;
+    forward_kinematics(m, s, k);
+    const V3 c = k.c[m.tip_link + 1];
+    tip[0] = c.x; tip[1] = c.y; tip[2] = c.z;
+  }
+  pendulum_obs(m, jq, jqd, tip, obs, rew, done);
 }
 
 // Gather the pack inputs from a physical state.
@@ -831,11 +858,12 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
     for (int i = 0; i < 3; i++) s[i] = m.base_pos[i];
     for (int i = 0; i < 4; i++) s[3 + i] = m.base_quat[i];
     for (int i = 7; i < PBG_BASE_WORDS + 2 * m.NJ; i++) s[i] = 0.0;
-    for (int r = 0; r < m.NR; r++) s[PBG_BASE_WORDS + m.reset_dof[r]] = qinit[(size_t)e * m.NR + r];
+    // robot_pendula.py:16 (swingup: 3.1415 + u)
+    for (int r = 0; r < m.NR; r++) s[PBG_BASE_WORDS + m.reset_dof[r]] = m.reset_offset[r] + qinit[(size_t)e * m.NR + r];
     float* ob = obs + (size_t)e * m.OBS;
     a[2] = 0.0;
     for (int i = 0; i < m.NF; i++) a[4 + i] = 0.0;
-    if (m.kind == 1) { pendulum_pack(s, ob, nullptr, nullptr); a[3] = 1.0; continue; }
+    if (m.kind == 1) { pendulum_pack(m, s, ob, nullptr, nullptr); a[3] = 1.0; continue; }
     static thread_local Kin k;
     double part_xyz[3 * (MAXL + 2)], quat[4], pos[3], vel[3], jq[MAXD], jqd[MAXD];
     int n_parts;
@@ -878,7 +906,7 @@ int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* a
     if (ncontact) ncontact[e] = nc;
     a[2] += 1.0;
     float* ob = obs + (size_t)e * m.OBS;
-    if (m.kind == 1) { pendulum_pack(s, ob, rew + e, done + e); continue; }
+    if (m.kind == 1) { pendulum_pack(m, s, ob, rew + e, done + e); continue; }
     uint8_t feet_new[8];
     for (int f = 0; f < m.NF; f++) {
       feet_new[f] = 0;

@@ -1,13 +1,14 @@
 """pybulletgym_amd: MI355X-native batched stepper for the roboschool locomotion envs of
-josiahls/pybullet-gym (InvertedPendulum, Hopper, HalfCheetah, Ant, Humanoid
-``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
+josiahls/pybullet-gym (InvertedPendulum, InvertedPendulumSwingup, InvertedDoublePendulum,
+Hopper, HalfCheetah, Ant, Humanoid, Walker2D ``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
 
     from pybulletgym_amd import VecEnv, make
     envs = VecEnv("AntPyBulletEnv-v0", 16384)      # device-resident batch, one launch per step
     env = make("AntPyBulletEnv-v0")                  # single env, gym.Env-style surface
 """
 ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
-           "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0")
+           "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
+           "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0")
 
 
 def __getattr__(name):

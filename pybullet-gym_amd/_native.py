@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpbg_amd.so")
 
 ROBOT_IDS = {"InvertedPendulumPyBulletEnv-v0": 0, "HopperPyBulletEnv-v0": 1, "HalfCheetahPyBulletEnv-v0": 2,
-             "AntPyBulletEnv-v0": 3, "HumanoidPyBulletEnv-v0": 4, "Walker2DPyBulletEnv-v0": 5}
+             "AntPyBulletEnv-v0": 3, "HumanoidPyBulletEnv-v0": 4, "Walker2DPyBulletEnv-v0": 5,
+             "InvertedPendulumSwingupPyBulletEnv-v0": 6, "InvertedDoublePendulumPyBulletEnv-v0": 7}
 
 
 class PbgError(RuntimeError):

@@ -40,7 +40,16 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
     ordered_names = [links[i].joint_name for i in ordered]
     if spec.motor_order is not None:
         assert spec.motor_order == ordered_names, "Humanoid motor order == ordered_joints order"
-    if spec.kind == robots.KIND_PENDULUM:
+    tip_link = -1
+    if spec.kind == robots.KIND_PENDULUM and spec.alive == robots.ALIVE_DOUBLE:
+        # robot_pendula.py:72-88: slider torque 200*clip(a0); reset randomises hinge, hinge2
+        # (:66-68); calc_state reads hinge, hinge2, slider and pole2's position (:81-83).
+        act_links = [model.link_index("cart")]
+        act_gain = [100.0 * spec.power]
+        reset_dof = [links[model.link_index("pole")].dof, links[model.link_index("pole2")].dof]
+        obs_links = [model.link_index("pole"), model.link_index("pole2"), model.link_index("cart")]
+        tip_link = model.link_index("pole2")
+    elif spec.kind == robots.KIND_PENDULUM:
         # robot_pendula.py:20-25: one action, slider torque 100*clip(a0); reset randomises
         # only the hinge (:16-17); calc_state reads hinge then slider (:28-29).
         act_links = [model.link_index("cart")]
@@ -149,7 +158,8 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         dof_damping=dof["damping"], dof_armature=dof["armature"], dof_jtype=dof["jtype"],
         dof_link=dof["link"],
         act_dof=act_dof, act_gain=act_gain, obs_dof=obs_dof, obs_vel_scale=vel_scale,
-        reset_dof=reset_dof,
+        reset_dof=reset_dof, reset_offset=[spec.reset_offset if i == 0 else 0.0 for i in range(len(reset_dof))],
+        tip_link=tip_link,
         act_joint_names=ordered_names,
         part_names=list(parts.keys()), part_link=list(parts.values()), robot_body=robot_body,
         foot_link=feet,
@@ -206,15 +216,14 @@ def _arr2(name, ctype, rows, w):
 
 
 def emit_struct(t: Dict) -> str:
-    cls = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah",
-           "ant": "Ant", "humanoid": "Humanoid", "walker2d": "Walker2D"}[t["key"]]
+    cls = STRUCTS[t["key"]]
     L = [f"// {t['env_id']}: generated by pybulletgym_amd.codegen from the reference MJCF asset",
          f"struct {cls} {{",
          f"  static constexpr int robot_id = {ROBOT_IDS[t['key']]};",
          f"  static constexpr int kind = {t['kind']};",
          f"  static constexpr bool floating = {'true' if t['floating'] else 'false'};"]
     for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "NG", "OBS", "alive", "substeps",
-              "floor", "max_episode_steps", "robot_body"):
+              "floor", "max_episode_steps", "robot_body", "tip_link"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
               "initial_z_fixed", "dt_sub", "base_mass"):
@@ -240,6 +249,7 @@ def emit_struct(t: Dict) -> str:
     L.append(_arr1("obs_dof", "int", t["obs_dof"]))
     L.append(_arr1("obs_vel_scale", "double", t["obs_vel_scale"]))
     L.append(_arr1("reset_dof", "int", t["reset_dof"]))
+    L.append(_arr1("reset_offset", "double", t["reset_offset"]))
     L.append(_arr1("part_link", "int", t["part_link"]))
     L.append(_arr1("foot_link", "int", t["foot_link"]))
     L.append(_arr1("slot_link", "int", t["slot_link"]))
@@ -262,7 +272,11 @@ def emit_struct(t: Dict) -> str:
     return "\n".join(L)
 
 
-ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5}
+ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
+             "pendulum_swingup": 6, "double_pendulum": 7}
+STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
+           "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
+           "double_pendulum": "DoublePendulum"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -25,13 +25,15 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[6][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[8][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
                                   {"HumanoidPyBulletEnv-v0", "humanoid"},
-                                  {"Walker2DPyBulletEnv-v0", "walker2d"}};
-  for (int i = 0; i < 6; i++)
+                                  {"Walker2DPyBulletEnv-v0", "walker2d"},
+                                  {"InvertedPendulumSwingupPyBulletEnv-v0", "pendulum_swingup"},
+                                  {"InvertedDoublePendulumPyBulletEnv-v0", "double_pendulum"}};
+  for (int i = 0; i < 8; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -63,9 +65,10 @@ pbg_info_t info_of(int rid) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
 
 const Ops* ops(int rid) {
-  static const Ops table[6] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
-                               PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5)};
-  return (rid >= 0 && rid < 6) ? &table[rid] : nullptr;
+  static const Ops table[8] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+                               PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5), PBG_OPS(PendulumSwingup, 6),
+                               PBG_OPS(DoublePendulum, 7)};
+  return (rid >= 0 && rid < 8) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {

@@ -879,7 +879,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   PackOut po;
   double pot_new = 0.0;
   if constexpr (R::kind == 1) {
-    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+    pendulum_pack<R>(s, obs, po);
   } else {
     PackIn<R> in;
     gather<R>(s, flags & 1u, in);

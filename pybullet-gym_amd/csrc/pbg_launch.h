@@ -37,4 +37,6 @@ PBG_DECLARE_ROBOT(HalfCheetah)
 PBG_DECLARE_ROBOT(Ant)
 PBG_DECLARE_ROBOT(Humanoid)
 PBG_DECLARE_ROBOT(Walker2D)
+PBG_DECLARE_ROBOT(PendulumSwingup)
+PBG_DECLARE_ROBOT(DoublePendulum)
 }  // namespace pbg

@@ -1103,16 +1103,33 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   out.reward = ((((0.0 + alive) + progress) + elec) + jal) + 0.0;
 }
 
-// robot_pendula.py:27-51 + gym_pendulum_envs.py:35-39
-PBG_DEV void pendulum_obs(double theta, double theta_dot, double x, double vx, float* obs, PackOut& out) {
-  if (!isfinite(vx)) vx = 0.0;
-  if (!isfinite(theta)) theta = 0.0;
-  if (!isfinite(theta_dot)) theta_dot = 0.0;
-  obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
-  obs[4] = (float)theta_dot;
-  out.reward = 1.0;
-  out.done = fabs(theta) > 0.2;
+// Pendulum packs (obs float64 in the reference, float32 through the C-ABI).
+//  InvertedPendulum / Swingup: robot_pendula.py:27-51 + gym_pendulum_envs.py:26-39 --
+//  non-finite vx / theta / theta_dot replaced by 0; balance: reward 1, done |theta| > .2;
+//  swingup: reward cos(theta), never done.
+template <class R>
+PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip, float* obs, PackOut& out) {
   out.potential = 0.0; out.initial_z = 0.0; out.feet_out = 0;
+  if constexpr (R::alive == 6) {
+    // InvertedDoublePendulum: robot_pendula.py:76-88, gym_pendulum_envs.py:69-80
+    const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
+    const double px = tip[0], py = tip[2];  // pos_x, _, pos_y = pole2.pose().xyz()
+    const double o[9] = {x, vx, px, cos(th), sin(th), thd, cos(g), sin(g), gd};
+#pragma unroll
+    for (int i = 0; i < 9; i++) obs[i] = (float)o[i];
+    const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
+    out.reward = ((0.0 + 10.0) + -dist_penalty) + 0.0;  // sum([alive 10, -dist, -vel 0])
+    out.done = py + 0.3 <= 1;
+  } else {
+    double theta = jq[0], theta_dot = jqd[0], x = jq[1], vx = jqd[1];
+    if (!isfinite(vx)) vx = 0.0;
+    if (!isfinite(theta)) theta = 0.0;
+    if (!isfinite(theta_dot)) theta_dot = 0.0;
+    obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
+    obs[4] = (float)theta_dot;
+    out.reward = R::alive == 5 ? cos(theta) : 1.0;
+    out.done = R::alive == 5 ? false : fabs(theta) > 0.2;
+  }
 }
 #pragma clang fp contract(on)
 
@@ -1199,6 +1216,22 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
   for (int i = 0; i < R::NO; i++) { in.jq[i] = s.q[R::obs_dof[i]]; in.jqd[i] = s.qd[R::obs_dof[i]]; }
 }
 
+// Pendulum pack from the physical state: obs joints (hinge[, hinge2], slider) and, for the
+// double pendulum, pole2's COM (getLinkState[0]).
+template <class R>
+PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
+  double jq[R::NO], jqd[R::NO], tip[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) { jq[i] = s.q[R::obs_dof[i]]; jqd[i] = s.qd[R::obs_dof[i]]; }
+  if constexpr (R::tip_link >= 0) {
+    Kin<R> k;
+    fk_pos<R>(s, k);
+    const f3 c = k.c[R::tip_link + 1];
+    tip[0] = c.x; tip[1] = c.y; tip[2] = c.z;
+  }
+  pendulum_obs<R>(jq, jqd, tip, obs, po);
+}
+
 // epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e]
 template <class R>
 PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
@@ -1206,7 +1239,7 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
   snapshot_state<R>(s);
   if (init_q) {
 #pragma unroll
-    for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = init_q[(size_t)e * R::NR + r];
+    for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = (float)R::reset_offset[r] + init_q[(size_t)e * R::NR + r];
   } else {
     // np_random.uniform(-0.1, 0.1) per ordered joint (robot_locomotors.py:18-19) -> Philox
     const uint32_t gid = (uint32_t)(B.env_offset + e);
@@ -1218,13 +1251,13 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int r = 4 * blk + t;
-        if (r < R::NR) s.q[R::reset_dof[r]] = fmaf(0.2f, u01(rr[t]), -0.1f);
+        if (r < R::NR) s.q[R::reset_dof[r]] = (float)R::reset_offset[r] + fmaf(0.2f, u01(rr[t]), -0.1f);
       }
     }
   }
   PackOut po;
   if constexpr (R::kind == 1) {
-    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+    pendulum_pack<R>(s, obs, po);
     has_floor = true; pot = 0.0; z0 = 0.f;
     return;
   } else {
@@ -1306,7 +1339,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   PackOut po;
   double pot_new = 0.0;
   if constexpr (R::kind == 1) {
-    pendulum_obs(s.q[1], s.qd[1], s.q[0], s.qd[0], obs, po);
+    pendulum_pack<R>(s, obs, po);
   } else {
     PackIn<R> in;
     gather<R>(s, flags & 1u, in);
@@ -1379,7 +1412,7 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = (float)r[o_act + i];
   if constexpr (R::kind == 1) {
-    pendulum_obs(r[o_jq], r[o_jqd], r[o_jq + 1], r[o_jqd + 1], obs, po);
+    pendulum_obs<R>(r + o_jq, r + o_jqd, r + o_pos, obs, po);  // pos: pole2 position (double pendulum)
   } else {
     PackIn<R> in;
     in.n_parts = (int)r[o_np];

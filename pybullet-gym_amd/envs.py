@@ -108,6 +108,10 @@ HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
 Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
 InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
+InvertedPendulumSwingup = _robot_class("pendulum_swingup", "InvertedPendulumSwingup")  # robot_pendula.py:54-55
+InvertedDoublePendulum = _robot_class("double_pendulum", "InvertedDoublePendulum")      # robot_pendula.py:58-88
+InvertedPendulum.swingup = False
+InvertedPendulumSwingup.swingup = True
 
 
 def _alive_bonus_hopper(self, z, pitch):
@@ -284,8 +288,40 @@ class InvertedPendulumBulletEnv(BaseBulletEnv):
         return obs[0].cpu().numpy().astype(np.float64)
 
 
+class InvertedPendulumSwingupBulletEnv(InvertedPendulumBulletEnv):
+    """gym_pendulum_envs.py:45-49: hinge reset at 3.1415 + U(-.1, .1); reward cos(theta),
+    never done (the TimeLimit ends episodes)."""
+    env_id = "InvertedPendulumSwingupPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = InvertedPendulumSwingup()
+        BaseBulletEnv.__init__(self, self.robot, render, device)
+        self.stateId = -1
+        self.scene = self.create_single_player_scene(None)
+
+
+class InvertedDoublePendulumBulletEnv(BaseBulletEnv):
+    """gym_pendulum_envs.py:52-86: obs float64 [x, vx, pole2 x, cos th, sin th, th', cos g,
+    sin g, g']; reward 10 - (0.01 x2^2 + (y2 + 0.3 - 2)^2); done y2 + 0.3 <= 1."""
+    env_id = "InvertedDoublePendulumPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = InvertedDoublePendulum()
+        BaseBulletEnv.__init__(self, self.robot, render, device)
+        self.stateId = -1
+        self.scene = self.create_single_player_scene(None)
+
+    def create_single_player_scene(self, bullet_client):
+        return SingleRobotEmptyScene(bullet_client, gravity=9.8, timestep=0.0165, frame_skip=1)
+
+    def _obs_out(self, obs):
+        return obs[0].cpu().numpy().astype(np.float64)
+
+
 ENV_CLASSES = {
     "InvertedPendulumPyBulletEnv-v0": InvertedPendulumBulletEnv,
+    "InvertedPendulumSwingupPyBulletEnv-v0": InvertedPendulumSwingupBulletEnv,
+    "InvertedDoublePendulumPyBulletEnv-v0": InvertedDoublePendulumBulletEnv,
     "HopperPyBulletEnv-v0": HopperBulletEnv,
     "Walker2DPyBulletEnv-v0": Walker2DBulletEnv,
     "HalfCheetahPyBulletEnv-v0": HalfCheetahBulletEnv,
@@ -295,6 +331,7 @@ ENV_CLASSES = {
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
 REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
+                    "InvertedPendulumSwingupPyBulletEnv-v0": 800.0, "InvertedDoublePendulumPyBulletEnv-v0": 9100.0,
                     "Walker2DPyBulletEnv-v0": 2500.0,
                     "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
 

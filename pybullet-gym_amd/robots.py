@@ -17,6 +17,8 @@ ALIVE_HALFCHEETAH = 1  # robot_locomotors.py:116-118 (+1 if |pitch|<1 and no con
 ALIVE_ANT = 2          # robot_locomotors.py:137-138 (+1 if z>0.26 else -1)
 ALIVE_HUMANOID = 3     # robot_locomotors.py:191-192 (+2 if z>0.78 else -1)
 ALIVE_PENDULUM = 4     # gym_pendulum_envs.py:35-39  (reward 1, done |theta|>0.2)
+ALIVE_SWINGUP = 5      # gym_pendulum_envs.py:31-34  (reward cos(theta), never done)
+ALIVE_DOUBLE = 6       # gym_pendulum_envs.py:69-80  (reward 10 - dist_penalty, done pos_y+0.3<=1)
 
 KIND_WALKER = 0
 KIND_PENDULUM = 1
@@ -45,6 +47,7 @@ class RobotSpec:
     floor: bool = True
     max_episode_steps: int = 1000                                # envs/__init__.py
     self_collision: bool = True
+    reset_offset: float = 0.0                                    # swingup hinge 3.1415 + u
 
 
 SPECS: Dict[str, RobotSpec] = OrderedDict()
@@ -57,6 +60,15 @@ def _add(s: RobotSpec):
 # InvertedPendulum: robot_pendula.py:5-51, gym_pendulum_envs.py:7-42, envs/__init__.py:4-9
 _add(RobotSpec("InvertedPendulumPyBulletEnv-v0", "pendulum", "inverted_pendulum.xml", "cart",
                action_dim=1, obs_dim=5, kind=KIND_PENDULUM, power=1.0, alive=ALIVE_PENDULUM,
+               timestep=0.0165, frame_skip=1, floor=False))
+# InvertedPendulumSwingup: robot_pendula.py:11-18,54-55 (hinge reset 3.1415 + u),
+# gym_pendulum_envs.py:26-34 (reward cos(theta), done False), envs/__init__.py:18-23
+_add(RobotSpec("InvertedPendulumSwingupPyBulletEnv-v0", "pendulum_swingup", "inverted_pendulum.xml", "cart",
+               action_dim=1, obs_dim=5, kind=KIND_PENDULUM, power=1.0, alive=ALIVE_SWINGUP,
+               timestep=0.0165, frame_skip=1, floor=False, reset_offset=3.1415))
+# InvertedDoublePendulum: robot_pendula.py:58-88, gym_pendulum_envs.py:45-86, envs/__init__.py:11-16
+_add(RobotSpec("InvertedDoublePendulumPyBulletEnv-v0", "double_pendulum", "inverted_double_pendulum.xml", "cart",
+               action_dim=1, obs_dim=9, kind=KIND_PENDULUM, power=2.0, alive=ALIVE_DOUBLE,
                timestep=0.0165, frame_skip=1, floor=False))
 # Hopper: robot_locomotors.py:82-90, envs/__init__.py:73-78
 _add(RobotSpec("HopperPyBulletEnv-v0", "hopper", "hopper.xml", "torso", action_dim=3, obs_dim=15,

@@ -44,6 +44,8 @@ ROBOTS = {
     "ant": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "AntBulletEnv"),
     "humanoid": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidBulletEnv"),
     "walker2d": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "Walker2DBulletEnv"),
+    "pendulum_swingup": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedPendulumSwingupBulletEnv"),
+    "double_pendulum": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedDoublePendulumBulletEnv"),
 }
 
 
@@ -294,8 +296,11 @@ def generate(key, episodes=3, steps=40, seed=1234):
             captured["feet_prev"] = np.array(self.feet_contact, dtype=np.float32)
             captured["initial_z_in"] = np.nan if self.initial_z is None else float(self.initial_z)
         else:
-            captured["jq"] = np.array([self.j1.get_state()[0], self.slider.get_state()[0]])
-            captured["jqd"] = np.array([self.j1.get_state()[1], self.slider.get_state()[1]])
+            js = [self.j1, self.j2, self.slider] if hasattr(self, "j2") else [self.j1, self.slider]
+            captured["jq"] = np.array([j.get_state()[0] for j in js])
+            captured["jqd"] = np.array([j.get_state()[1] for j in js])
+            if hasattr(self, "pole2"):  # InvertedDoublePendulum reads pole2.pose().xyz()
+                captured["body_pos"] = np.array(self.pole2.pose().xyz(), dtype=np.float64)
         return orig_calc(self)
 
     calc_cls.calc_state = spy_calc_state
@@ -322,6 +327,8 @@ def generate(key, episodes=3, steps=40, seed=1234):
             rec["initial_z_in"].append(captured["initial_z_in"])
             rec["initial_z_out"].append(float(robot.initial_z))
             part_names.append(captured["part_names"])
+        elif "body_pos" in captured:
+            rec["body_pos"].append(captured["body_pos"])
         rec["jq"].append(captured["jq"]); rec["jqd"].append(captured["jqd"])
         rec["act"].append(np.zeros(t["NA"], np.float32) if act is None else act)
         rec["potential_old"].append(pot_old)
@@ -355,7 +362,7 @@ def generate(key, episodes=3, steps=40, seed=1234):
 def main():
     install_stubs()
     sys.path.insert(0, REF)
-    for key in ROBOTS:
+    for key in (sys.argv[1:] or ROBOTS):
         data = generate(key)
         path = os.path.join(HERE, f"pack_{key}.npz")
         np.savez_compressed(path, **data)

@@ -50,17 +50,23 @@ def test_oracle_pack_bit_exact(key):
             np.testing.assert_array_equal(out["feet"], g["feet_out"][i][: len(out["feet"])])
 
 
-def test_oracle_pack_pendulum():
-    """robot_pendula.py:27-51 + gym_pendulum_envs.py:26-39.  The reference's obs is float64;
-    the C-ABI carries float32, so the check is f32(reference) bit-exact."""
-    g = load("pendulum")
+PENDULUMS = ["pendulum", "pendulum_swingup", "double_pendulum"]
+
+
+@pytest.mark.parametrize("key", PENDULUMS)
+def test_oracle_pack_pendulum(key):
+    """robot_pendula.py:27-51,76-88 + gym_pendulum_envs.py:26-39,69-80 (balance, swingup,
+    double).  The reference's obs is float64; the C-ABI carries float32, so the check is
+    f32(reference) bit-exact; reward (float64) exact."""
+    g = load(key)
     for i in range(len(g["kind"])):
         step = g["kind"][i] == 1
-        out = oracle.pack("pendulum", np.zeros((1, 3)), np.zeros(4), np.zeros(3), np.zeros(3), g["jq"][i],
+        pos = g["body_pos"][i] if "body_pos" in g.files and g["body_pos"].size else np.zeros(3)
+        out = oracle.pack(key, np.zeros((1, 3)), np.zeros(4), pos, np.zeros(3), g["jq"][i],
                           g["jqd"][i], np.zeros(1), np.zeros(1) if step else None, g["act"][i] if step else None,
                           0.0, 0.0)
         ref = g["obs"][i].astype(np.float32)
-        np.testing.assert_array_equal(out["obs"].view(np.uint32), ref.view(np.uint32))
+        np.testing.assert_array_equal(out["obs"].view(np.uint32), ref.view(np.uint32), err_msg=f"call {i}")
         if step:
-            assert out["done"] == bool(g["done"][i])
-            assert out["reward"] == g["reward"][i]
+            assert out["done"] == bool(g["done"][i]), f"call {i}"
+            assert out["reward"] == g["reward"][i], f"call {i}"

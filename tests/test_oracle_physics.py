@@ -132,7 +132,7 @@ def test_bias_accelerations_are_jdot_nu(key):
     np.testing.assert_allclose((w1 - w0) / (2 * eps), al, atol=1e-7 * max(1, np.abs(al).max()))
 
 
-@pytest.mark.parametrize("key", KEYS + ["pendulum"])
+@pytest.mark.parametrize("key", KEYS + ["pendulum", "pendulum_swingup", "double_pendulum"])
 def test_random_rollout_stays_finite(key):
     n = 32
     e = oracle.OracleEnvs(key, n, nthreads=4)
@@ -142,9 +142,9 @@ def test_random_rollout_stays_finite(key):
         obs, r, d, nc = e.step(rng.uniform(-1, 1, (n, e.info.NA)).astype(np.float32))
         assert np.isfinite(e.state).all()
         assert np.isfinite(obs).all() and np.isfinite(r).all()
-        if key != "pendulum":
+        if "pendulum" not in key:
             assert np.abs(obs).max() <= 5.0  # robot_locomotors.py:64 (the pendulum does not clip)
-    if key != "pendulum":
+    if "pendulum" not in key:
         assert (e.state[:, 13 + e.info.NJ:] ** 2).max() <= 100.0 ** 2 + 1e-6  # maxCoordinateVelocity
 
 
