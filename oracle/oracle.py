@@ -14,12 +14,13 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
-             "pendulum_swingup": 6, "double_pendulum": 7}
+             "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8}
 ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
             "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
             "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d",
             "InvertedPendulumSwingupPyBulletEnv-v0": "pendulum_swingup",
-            "InvertedDoublePendulumPyBulletEnv-v0": "double_pendulum"}
+            "InvertedDoublePendulumPyBulletEnv-v0": "double_pendulum",
+            "HumanoidFlagrunPyBulletEnv-v0": "humanoid_flagrun"}
 
 _lib = None
 
@@ -39,6 +40,8 @@ def lib():
         L.pbg_oracle_reset.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
         L.pbg_oracle_step.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int]
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
+        L.pbg_oracle_pack_flag.argtypes = [ctypes.c_int, P, P, P, P]
+        L.pbg_oracle_set_rng.argtypes = [ctypes.c_uint64, ctypes.c_int]
         L.pbg_oracle_dynamics.argtypes = [ctypes.c_int, P, P, P]
         L.pbg_oracle_link_com.argtypes = [ctypes.c_int, P, P]
         _lib = L
@@ -67,7 +70,9 @@ class Info:
 class OracleEnvs:
     """Batch of n envs stepped by the CPU oracle (float64 physics)."""
 
-    def __init__(self, name: str, n: int, nthreads: int = 1):
+    def __init__(self, name: str, n: int, nthreads: int = 1, seed: int = 0, env_offset: int = 0):
+        """seed / env_offset key the Philox draws of HumanoidFlagrun's flag (as the kernels')."""
+        lib().pbg_oracle_set_rng(seed, env_offset)
         self.rid = robot_id(name)
         self.info = Info(self.rid)
         self.n = n
@@ -114,18 +119,20 @@ class _PackIn(ctypes.Structure):
                 ("body_quat", ctypes.c_void_p), ("body_pos", ctypes.c_void_p),
                 ("body_vel", ctypes.c_void_p), ("jq", ctypes.c_void_p), ("jqd", ctypes.c_void_p),
                 ("feet_prev", ctypes.c_void_p), ("feet_new", ctypes.c_void_p), ("act", ctypes.c_void_p),
-                ("potential_old", ctypes.c_double), ("initial_z", ctypes.c_double)]
+                ("potential_old", ctypes.c_double), ("initial_z", ctypes.c_double),
+                ("target_x", ctypes.c_double), ("target_y", ctypes.c_double)]
 
 
 class _PackOut(ctypes.Structure):
     _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_double), ("done", ctypes.c_uint8),
                 ("potential", ctypes.c_double), ("initial_z", ctypes.c_double),
-                ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5)]
+                ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5), ("dist", ctypes.c_double)]
 
 
 def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet_new, act,
-         potential_old, initial_z):
-    """Run the oracle's pack on explicit inputs (golden-vector tests)."""
+         potential_old, initial_z, flag=None):
+    """Run the oracle's pack on explicit inputs (golden-vector tests).  flag (HumanoidFlagrun):
+    [target x, y, flag_timeout, next draw x, y]; the result then carries flag_out."""
     rid = robot_id(name)
     info = Info(rid)
     arrs = dict(part_xyz=np.ascontiguousarray(part_xyz, dtype=np.float64),
@@ -138,12 +145,18 @@ def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet
     ac = None if act is None else np.ascontiguousarray(act, dtype=np.float32)
     pin = _PackIn(_p(arrs["part_xyz"]), len(arrs["part_xyz"]), _p(arrs["body_quat"]), _p(arrs["body_pos"]),
                   _p(arrs["body_vel"]), _p(arrs["jq"]), _p(arrs["jqd"]), _p(arrs["feet_prev"]), _p(fn),
-                  _p(ac), float(potential_old), float(initial_z))
+                  _p(ac), float(potential_old), float(initial_z), 1e3, 0.0)
     obs = np.zeros(info.OBS, dtype=np.float32)
     feet_out = np.zeros(max(1, info.NF), dtype=np.float32)
     pout = _PackOut()
     pout.obs = _p(obs)
     pout.feet_out = _p(feet_out)
-    assert lib().pbg_oracle_pack(rid, ctypes.byref(pin), ctypes.byref(pout)) == 0
+    flag_out = np.zeros(3)
+    if flag is None:
+        assert lib().pbg_oracle_pack(rid, ctypes.byref(pin), ctypes.byref(pout)) == 0
+    else:
+        fin = np.ascontiguousarray(flag, dtype=np.float64)
+        assert lib().pbg_oracle_pack_flag(rid, ctypes.byref(pin), ctypes.byref(pout), _p(fin), _p(flag_out)) == 0
     return dict(obs=obs, reward=pout.reward, done=bool(pout.done), potential=pout.potential,
-                initial_z=pout.initial_z, feet=feet_out[:info.NF].copy(), rewards=list(pout.rewards))
+                initial_z=pout.initial_z, feet=feet_out[:info.NF].copy(), rewards=list(pout.rewards),
+                flag_out=flag_out)

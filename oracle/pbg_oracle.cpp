@@ -48,7 +48,7 @@ int g_flags = 0;
 // ------------------------------------------------------------------ model view
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
-      floor, max_steps, robot_body, tip_link;
+      floor, max_steps, robot_body, tip_link, flagrun;
   double power, elec, stall, jal, z0fixed, dt_sub, base_mass;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
@@ -71,6 +71,7 @@ MV view() {
   m.NDOF = R::NDOF; m.NA = R::NA; m.NO = R::NO; m.NR = R::NR; m.NF = R::NF; m.NP = R::NP;
   m.NS = R::NS; m.NPAIR = R::NPAIR; m.OBS = R::OBS; m.alive = R::alive; m.substeps = R::substeps;
   m.floor = R::floor; m.max_steps = R::max_episode_steps; m.robot_body = R::robot_body; m.tip_link = R::tip_link;
+  m.flagrun = R::flagrun;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
   m.base_mass = R::base_mass; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
@@ -90,11 +91,12 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[8] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[9] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                         view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                         view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
-                        view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>()};
-  if (robot < 0 || robot > 7) return nullptr;
+                        view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
+                        view<pbg_models::HumanoidFlagrun>()};
+  if (robot < 0 || robot > 8) return nullptr;
   return &views[robot];
 }
 
@@ -612,6 +614,31 @@ void euler_from_quat(const double* q, double* rpy) {
 
 inline float clip5(float v) { return v < -5.0f ? -5.0f : (v > 5.0f ? 5.0f : v); }  // NaN passes
 
+// Philox4x32-10 (Salmon et al. 2011), as the kernels use it for their random draws.
+void philox(uint32_t ctr[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0], p1 = (uint64_t)0xCD9E8D57u * ctr[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ ctr[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ ctr[3] ^ k1;
+    ctr[1] = (uint32_t)p1; ctr[3] = (uint32_t)p0; ctr[0] = n0; ctr[2] = n2;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+uint64_t g_seed = 0;
+int g_env_offset = 0;
+
+// HumanoidFlagrun walk target (robot_locomotors.py:195-226): flag_reposition draws
+// U(+-halflen) x U(+-halfwidth) times 0.5 (here Philox, counter (global env, draw index)).
+struct Flag { double tx, ty; int timeout, count; };
+void flag_draw(int e, Flag& f) {
+  uint32_t c[4] = {(uint32_t)(g_env_offset + e), (uint32_t)f.count, 0xF1A6u, 0x5EEDu};
+  philox(c, (uint32_t)g_seed, (uint32_t)(g_seed >> 32));
+  const double u0 = (double)(c[0] >> 8) * (1.0 / 16777216.0), u1 = (double)(c[1] >> 8) * (1.0 / 16777216.0);
+  f.tx = (-PBG_STADIUM_HALFLEN + 2.0 * PBG_STADIUM_HALFLEN * u0) * PBG_FLAG_COMPACT;
+  f.ty = (-PBG_STADIUM_HALFWIDTH + 2.0 * PBG_STADIUM_HALFWIDTH * u1) * PBG_FLAG_COMPACT;
+  f.timeout = PBG_FLAG_TIMEOUT;
+  f.count++;
+}
+
 }  // namespace
 
 extern "C" {
@@ -630,12 +657,14 @@ typedef struct {
   const float* act;          // [NA] raw action (nullable: reset)
   double potential_old;
   double initial_z;          // NaN: take it from this calc_state (robot_locomotors.py:44-45)
+  double target_x, target_y; // robot.walk_target_x / _y (1e3, 0 except HumanoidFlagrun)
 } pbg_pack_in;
 
 typedef struct {
   float* obs; double reward; uint8_t done; double potential; double initial_z;
   float* feet_out;           // [NF]
   double rewards[5];         // alive, progress, electricity, joints_at_limit, feet_collision
+  double dist;               // walk_target_dist
 } pbg_pack_out;
 
 void pbg_oracle_set_flags(int flags) { g_flags = flags; }
@@ -671,7 +700,8 @@ int pbg_oracle_info(int robot, int* out) {
   const MV* m = model(robot);
   if (!m) return -1;
   int v[] = {m->NL, m->NJ, m->NDOF, m->NA, m->NO, m->NR, m->NF, m->NP, m->NS, m->NPAIR, m->OBS,
-             PBG_BASE_WORDS + 2 * m->NJ, PBG_AUX_WORDS + m->NF, m->floating, m->kind, m->substeps};
+             PBG_BASE_WORDS + 2 * m->NJ, PBG_AUX_WORDS + m->NF + (m->flagrun ? 4 : 0), m->floating, m->kind,
+             m->substeps};
   memcpy(out, v, sizeof(v));
   return 0;
 }
@@ -712,9 +742,10 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   double rpy[3];
   euler_from_quat(in->body_quat, rpy);
   double z0 = isnan(in->initial_z) ? bz : in->initial_z;
-  double theta = atan2(PBG_WALK_TARGET_Y - by, PBG_WALK_TARGET_X - bx);
-  double dy = PBG_WALK_TARGET_Y - by, dx = PBG_WALK_TARGET_X - bx;
+  double theta = atan2(in->target_y - by, in->target_x - bx);
+  double dy = in->target_y - by, dx = in->target_x - bx;
   double dist = sqrt(dy * dy + dx * dx);
+  out->dist = dist;
   double ang = theta - rpy[2];
   double cy = cos(-rpy[2]), sy = sin(-rpy[2]);
   double vx = cy * in->body_vel[0] + -sy * in->body_vel[1] + 0.0 * in->body_vel[2];
@@ -776,6 +807,47 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   out->rewards[3] = jal; out->rewards[4] = 0.0;
   out->reward = ((((0.0 + alive) + progress) + elec) + jal) + 0.0;
   out->done = done;
+  return 0;
+}
+
+// calc_state with HumanoidFlagrun's bookkeeping (robot_locomotors.py:219-226): timeout
+// countdown, pack against the current flag, re-draw and pack again when the target is
+// within 1 m or the timeout ran out.  `next` (nullable) replaces the draw (golden tests).
+static void flag_pack(int robot, const MV& m, pbg_pack_in* in, pbg_pack_out* out, Flag& f, int e,
+                      const double* next) {
+  if (!m.flagrun) { pbg_oracle_pack(robot, in, out); return; }
+  f.timeout -= 1;
+  in->target_x = f.tx; in->target_y = f.ty;
+  pbg_oracle_pack(robot, in, out);
+  if (out->dist < 1.0 || f.timeout <= 0) {
+    if (next) { f.tx = next[0]; f.ty = next[1]; f.timeout = PBG_FLAG_TIMEOUT; f.count++; }
+    else flag_draw(e, f);
+    in->target_x = f.tx; in->target_y = f.ty;
+    pbg_oracle_pack(robot, in, out);
+  }
+}
+static Flag load_flag(const MV& m, const double* a) {
+  Flag f = {0.0, 0.0, 0, 0};
+  if (m.flagrun) { f.tx = a[4 + m.NF]; f.ty = a[5 + m.NF]; f.timeout = (int)a[6 + m.NF]; f.count = (int)a[7 + m.NF]; }
+  return f;
+}
+static void store_flag(const MV& m, double* a, const Flag& f) {
+  if (m.flagrun) { a[4 + m.NF] = f.tx; a[5 + m.NF] = f.ty; a[6 + m.NF] = f.timeout; a[7 + m.NF] = f.count; }
+}
+
+// Flag RNG of the kernels: Philox key = seed, env ids offset by env_offset.
+void pbg_oracle_set_rng(uint64_t seed, int env_offset) { g_seed = seed; g_env_offset = env_offset; }
+
+// Golden-vector form: flag_in = [target x, y, flag_timeout, next draw x, y],
+// flag_out = [target x, y, flag_timeout] after the calc_state.
+int pbg_oracle_pack_flag(int robot, const pbg_pack_in* in, pbg_pack_out* out, const double* flag_in,
+                         double* flag_out) {
+  const MV* mp = model(robot);
+  if (!mp) return -1;
+  pbg_pack_in in2 = *in;
+  Flag f = {flag_in[0], flag_in[1], (int)flag_in[2], 0};
+  flag_pack(robot, *mp, &in2, out, f, 0, flag_in + 3);
+  flag_out[0] = f.tx; flag_out[1] = f.ty; flag_out[2] = f.timeout;
   return 0;
 }
 
@@ -851,7 +923,7 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_WORDS + m.NF;
+  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_WORDS + m.NF + (m.flagrun ? 4 : 0);
   for (int e = 0; e < n; e++) {
     double* s = state + (size_t)e * SD;
     double* a = aux + (size_t)e * AD;
@@ -870,10 +942,13 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
     gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd);
     float feet_prev[8] = {0}, feet_out[8];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, nullptr, nullptr, 0.0,
-                      m.z0fixed};
+                      m.z0fixed, PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
-    pbg_oracle_pack(robot, &in, &out);
+    Flag fl = load_flag(m, a);
+    if (m.flagrun) flag_draw(e, fl);  // robot_specific_reset -> flag_reposition (:199-201)
+    flag_pack(robot, m, &in, &out, fl, e, nullptr);
+    store_flag(m, a, fl);
     a[0] = out.potential;
     a[1] = out.initial_z;
     a[3] = 1.0;  // the floor is in robot.parts from now on
@@ -888,7 +963,7 @@ int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* a
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_WORDS + m.NF;
+  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_WORDS + m.NF + (m.flagrun ? 4 : 0);
 #pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
   for (int e = 0; e < n; e++) {
     double* s = state + (size_t)e * SD;
@@ -920,10 +995,12 @@ int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* a
     float feet_prev[8], feet_out[8];
     for (int f = 0; f < m.NF; f++) feet_prev[f] = (float)a[4 + f];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, feet_new, ac,
-                      a[0], a[1]};
+                      a[0], a[1], PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
-    pbg_oracle_pack(robot, &in, &out);
+    Flag fl = load_flag(m, a);
+    flag_pack(robot, m, &in, &out, fl, e, nullptr);
+    store_flag(m, a, fl);
     rew[e] = out.reward;
     done[e] = out.done;
     a[0] = out.potential;

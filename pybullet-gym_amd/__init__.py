@@ -1,6 +1,6 @@
 """pybulletgym_amd: MI355X-native batched stepper for the roboschool locomotion envs of
 josiahls/pybullet-gym (InvertedPendulum, InvertedPendulumSwingup, InvertedDoublePendulum,
-Hopper, HalfCheetah, Ant, Humanoid, Walker2D ``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
+Hopper, HalfCheetah, Ant, Humanoid, HumanoidFlagrun, Walker2D ``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
 
     from pybulletgym_amd import VecEnv, make
     envs = VecEnv("AntPyBulletEnv-v0", 16384)      # device-resident batch, one launch per step
@@ -8,7 +8,8 @@ Hopper, HalfCheetah, Ant, Humanoid, Walker2D ``*PyBulletEnv-v0``).  Import as ``
 """
 ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
            "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
-           "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0")
+           "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
+           "HumanoidFlagrunPyBulletEnv-v0")
 
 
 def __getattr__(name):

@@ -159,7 +159,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         dof_link=dof["link"],
         act_dof=act_dof, act_gain=act_gain, obs_dof=obs_dof, obs_vel_scale=vel_scale,
         reset_dof=reset_dof, reset_offset=[spec.reset_offset if i == 0 else 0.0 for i in range(len(reset_dof))],
-        tip_link=tip_link,
+        tip_link=tip_link, flagrun=int(spec.flagrun),
         act_joint_names=ordered_names,
         part_names=list(parts.keys()), part_link=list(parts.values()), robot_body=robot_body,
         foot_link=feet,
@@ -223,7 +223,7 @@ def emit_struct(t: Dict) -> str:
          f"  static constexpr int kind = {t['kind']};",
          f"  static constexpr bool floating = {'true' if t['floating'] else 'false'};"]
     for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "NG", "OBS", "alive", "substeps",
-              "floor", "max_episode_steps", "robot_body", "tip_link"):
+              "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
               "initial_z_fixed", "dt_sub", "base_mass"):
@@ -273,10 +273,10 @@ def emit_struct(t: Dict) -> str:
 
 
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
-             "pendulum_swingup": 6, "double_pendulum": 7}
+             "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
-           "double_pendulum": "DoublePendulum"}
+           "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -25,15 +25,16 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[8][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[9][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
                                   {"HumanoidPyBulletEnv-v0", "humanoid"},
                                   {"Walker2DPyBulletEnv-v0", "walker2d"},
                                   {"InvertedPendulumSwingupPyBulletEnv-v0", "pendulum_swingup"},
-                                  {"InvertedDoublePendulumPyBulletEnv-v0", "double_pendulum"}};
-  for (int i = 0; i < 8; i++)
+                                  {"InvertedDoublePendulumPyBulletEnv-v0", "double_pendulum"},
+                                  {"HumanoidFlagrunPyBulletEnv-v0", "humanoid_flagrun"}};
+  for (int i = 0; i < 9; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -65,10 +66,10 @@ pbg_info_t info_of(int rid) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
 
 const Ops* ops(int rid) {
-  static const Ops table[8] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+  static const Ops table[9] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
                                PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5), PBG_OPS(PendulumSwingup, 6),
-                               PBG_OPS(DoublePendulum, 7)};
-  return (rid >= 0 && rid < 8) ? &table[rid] : nullptr;
+                               PBG_OPS(DoublePendulum, 7), PBG_OPS(HumanoidFlagrun, 8)};
+  return (rid >= 0 && rid < 9) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {
@@ -143,6 +144,8 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
   e |= hip_check(hipMalloc(&B.elapsed, sizeof(int) * n), "hipMalloc elapsed");
   e |= hip_check(hipMalloc(&B.flags, sizeof(uint32_t) * n), "hipMalloc flags");
   e |= hip_check(hipMalloc(&B.episode, sizeof(uint32_t) * n), "hipMalloc episode");
+  e |= hip_check(hipMalloc(&B.tgt, sizeof(double) * 2 * n), "hipMalloc walk target");
+  e |= hip_check(hipMalloc(&B.ftm, sizeof(int32_t) * 2 * n), "hipMalloc flag counters");
   e |= hip_check(hipMalloc(&h->scratch, sizeof(float) * n * h->geo.scratch_words_per_env), "hipMalloc scratch");
   if (!e) {
     e |= hip_check(hipMemset(B.st, 0, sizeof(float) * n * h->info.state_words), "hipMemset");
@@ -151,6 +154,8 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
     e |= hip_check(hipMemset(B.elapsed, 0, sizeof(int) * n), "hipMemset");
     e |= hip_check(hipMemset(B.flags, 0, sizeof(uint32_t) * n), "hipMemset");
     e |= hip_check(hipMemset(B.episode, 0, sizeof(uint32_t) * n), "hipMemset");
+    e |= hip_check(hipMemset(B.tgt, 0, sizeof(double) * 2 * n), "hipMemset");
+    e |= hip_check(hipMemset(B.ftm, 0, sizeof(int32_t) * 2 * n), "hipMemset");
     e |= hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   }
   if (e) {
@@ -164,7 +169,7 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
 void pbg_destroy(pbg_handle* h) {
   if (!h) return;
   DeviceGuard dg(h->device);
-  void* bufs[] = {h->B.st, h->B.pot, h->B.z0, h->B.elapsed, h->B.flags, h->B.episode, h->scratch};
+  void* bufs[] = {h->B.st, h->B.pot, h->B.z0, h->B.elapsed, h->B.flags, h->B.episode, h->B.tgt, h->B.ftm, h->scratch};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   delete h;

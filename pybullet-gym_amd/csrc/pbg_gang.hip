@@ -878,6 +878,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   float obs[R::OBS];
   PackOut po;
   double pot_new = 0.0;
+  Flag fl = load_flag<R>(B, e);
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
   } else {
@@ -896,7 +897,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     in.feet_new = fnew;
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
-    walker_pack<R>(in, act, obs, po);
+    flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
@@ -920,7 +921,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     // every lane reads the episode counter (one load instruction) before the writer bumps it
     const uint32_t epi = B.episode[e];
     if (w0) B.episode[e] = epi + 1;
-    reset_env_epi<R>(B, e, s, nullptr, obs, has_floor, pot, z0, epi);
+    reset_env_epi<R>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl);
     if (w0) {
       B.pot[e] = pot;
       B.z0[e] = z0;
@@ -934,6 +935,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   }
   if (w0) {
     store_state<R>(s, B.st, B.n, e);
+    store_flag<R>(B, e, fl);
 #pragma unroll
     for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
   }

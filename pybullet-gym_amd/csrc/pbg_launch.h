@@ -39,4 +39,5 @@ PBG_DECLARE_ROBOT(Humanoid)
 PBG_DECLARE_ROBOT(Walker2D)
 PBG_DECLARE_ROBOT(PendulumSwingup)
 PBG_DECLARE_ROBOT(DoublePendulum)
+PBG_DECLARE_ROBOT(HumanoidFlagrun)
 }  // namespace pbg

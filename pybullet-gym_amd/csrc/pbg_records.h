@@ -7,14 +7,16 @@ namespace pbg {
 // record is float64: [part_xyz (NP+1)*3 | n_parts | quat 4 | pos 3 | vel 3 | jq NO | jqd NO |
 // feet_prev NF | feet_new NF | act NA | potential_old | initial_z_in | is_step]; the output
 // record: [obs OBS | reward | done | potential | initial_z | feet_out NF].
+// HumanoidFlagrun appends to the input [target x, y | flag_timeout | next target x, y] (the
+// draw a reposition would take) and to the output [target x, y | flag_timeout].
 template <class R>
 struct PackRec {
-  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3;
-  static constexpr int OUT = R::OBS + 4 + R::NF;
+  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3 + (R::flagrun ? 5 : 0);
+  static constexpr int OUT = R::OBS + 4 + R::NF + (R::flagrun ? 3 : 0);
 };
 template <class R>
 struct Records {
-  static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;  // physical state words
-  static constexpr int AD = PBG_AUX_WORDS + R::NF;       // bookkeeping words
+  static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;                       // physical state words
+  static constexpr int AD = PBG_AUX_WORDS + R::NF + (R::flagrun ? 4 : 0);     // bookkeeping words
 };
 }  // namespace pbg

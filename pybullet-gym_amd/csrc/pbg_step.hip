@@ -1001,9 +1001,10 @@ struct PackIn {
   float feet_prev[R::NF > 0 ? R::NF : 1];
   uint32_t feet_new;  // bitmask
   double potential_old, initial_z;  // initial_z NaN: take from this calc_state
+  double target_x = PBG_WALK_TARGET_X, target_y = PBG_WALK_TARGET_Y;  // robot.walk_target_x/y
 };
 struct PackOut {
-  double reward, potential, initial_z;
+  double reward, potential, initial_z, dist;  // dist: walk_target_dist
   uint32_t feet_out;  // bitmask
   bool done;
 };
@@ -1047,7 +1048,7 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   const double pitch = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
   const double yaw = atan2(2 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
   const double z0 = isnan(in.initial_z) ? bz : in.initial_z;
-  const double dy = PBG_WALK_TARGET_Y - by, dx = PBG_WALK_TARGET_X - bx;
+  const double dy = in.target_y - by, dx = in.target_x - bx;
   const double theta = atan2(dy, dx);
   const double dist = sqrt(dy * dy + dx * dx);
   const double ang = theta - yaw;
@@ -1066,6 +1067,7 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
 #pragma unroll
   for (int i = 0; i < R::NF; i++) { obs[o] = clip5(in.feet_prev[i]); o++; }
   out.initial_z = z0;
+  out.dist = dist;
   out.potential = -dist / (R::dt_sub * R::substeps);  // robot_locomotors.py:79; scene_bases.py:17
   uint32_t fb = 0;
 #pragma unroll
@@ -1101,6 +1103,52 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   elec += R::stall_torque_cost * (double)mean_s;
   const double jal = R::joints_at_limit_cost * (double)at_limit;
   out.reward = ((((0.0 + alive) + progress) + elec) + jal) + 0.0;
+}
+
+// HumanoidFlagrun walk target (robot_locomotors.py:195-226).
+struct Flag {
+  double tx, ty;  // walk_target_x / _y (float64, as the reference's)
+  int timeout;    // flag_timeout
+  int count;      // draws so far: the Philox counter of the next draw (never reset)
+};
+// flag_reposition (:203-216): np_random.uniform(+-halflen), uniform(+-halfwidth), times
+// more_compact; here Philox4x32-10 keyed by the seed, counter (global env, draw index).
+PBG_DEV void flag_draw(const Buffers& B, int e, Flag& f) {
+  u4 ctr = {(uint32_t)(B.env_offset + e), (uint32_t)f.count, 0xF1A6u, 0x5EEDu};
+  const u4 r = philox4x32_10(ctr, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
+  f.tx = (-PBG_STADIUM_HALFLEN + 2.0 * PBG_STADIUM_HALFLEN * (double)u01(r.x)) * PBG_FLAG_COMPACT;
+  f.ty = (-PBG_STADIUM_HALFWIDTH + 2.0 * PBG_STADIUM_HALFWIDTH * (double)u01(r.y)) * PBG_FLAG_COMPACT;
+  f.timeout = PBG_FLAG_TIMEOUT;
+  f.count++;
+}
+// calc_state with HumanoidFlagrun's bookkeeping (:219-226): count the timeout down, pack
+// against the current flag, and if the target is within 1 m or the timeout ran out, re-draw
+// (`redraw(f)`) and pack again against the new flag.  Other robots: plain walker_pack.
+template <class R, class Redraw>
+PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po, Flag& f, Redraw&& redraw) {
+  if constexpr (R::flagrun) {
+    f.timeout -= 1;
+    in.target_x = f.tx; in.target_y = f.ty;
+    walker_pack<R>(in, act, obs, po);
+    if (po.dist < 1.0 || f.timeout <= 0) {
+      redraw(f);
+      in.target_x = f.tx; in.target_y = f.ty;
+      walker_pack<R>(in, act, obs, po);
+    }
+  } else {
+    (void)f; (void)redraw;
+    walker_pack<R>(in, act, obs, po);
+  }
+}
+template <class R>
+PBG_DEV Flag load_flag(const Buffers& B, int e) {
+  Flag f = {0.0, 0.0, 0, 0};
+  if constexpr (R::flagrun) { f.tx = B.tgt[e]; f.ty = B.tgt[B.n + e]; f.timeout = B.ftm[e]; f.count = B.ftm[B.n + e]; }
+  return f;
+}
+template <class R>
+PBG_DEV void store_flag(const Buffers& B, int e, const Flag& f) {
+  if constexpr (R::flagrun) { B.tgt[e] = f.tx; B.tgt[B.n + e] = f.ty; B.ftm[e] = f.timeout; B.ftm[B.n + e] = f.count; }
 }
 
 // Pendulum packs (obs float64 in the reference, float32 through the C-ABI).
@@ -1235,7 +1283,7 @@ PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
 // epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e]
 template <class R>
 PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                           double& pot, float& z0, uint32_t epi) {
+                           double& pot, float& z0, uint32_t epi, Flag& fl) {
   snapshot_state<R>(s);
   if (init_q) {
 #pragma unroll
@@ -1268,7 +1316,9 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
   in.feet_new = 0;
   in.potential_old = 0.0;
   in.initial_z = R::initial_z_fixed;
-  walker_pack<R>(in, nullptr, obs, po);
+  auto draw = [&](Flag& f) { flag_draw(B, e, f); };
+  if constexpr (R::flagrun) draw(fl);  // robot_specific_reset -> flag_reposition (:199-201)
+  flag_pack<R>(in, nullptr, obs, po, fl, draw);
   pot = po.potential;
   z0 = (float)po.initial_z;
   has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
@@ -1280,7 +1330,9 @@ PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q
                        double& pot, float& z0) {
   const uint32_t epi = B.episode[e];
   B.episode[e] = epi + 1;
-  reset_env_epi<R>(B, e, s, init_q, obs, has_floor, pot, z0, epi);
+  Flag fl = load_flag<R>(B, e);
+  reset_env_epi<R>(B, e, s, init_q, obs, has_floor, pot, z0, epi, fl);
+  store_flag<R>(B, e, fl);
 }
 
 template <class R>
@@ -1356,7 +1408,9 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     in.feet_new = fnew;
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
-    walker_pack<R>(in, act, obs, po);
+    Flag fl = load_flag<R>(B, e);
+    flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
+    store_flag<R>(B, e, fl);
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
@@ -1430,9 +1484,22 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
     in.feet_new = fn;
     in.potential_old = r[o_pot];
     in.initial_z = r[o_pot + 1];
-    // the step's part counts take the kernels' compile-time path (what this test pins)
-    if (in.n_parts == R::NP || in.n_parts == R::NP + 1) walker_pack<R>(in, is_step ? act : nullptr, obs, po);
-    else walker_pack<R, true>(in, is_step ? act : nullptr, obs, po);
+    if constexpr (R::flagrun) {
+      // [target x, y | flag_timeout | next target x, y]: the reposition takes the recorded draw
+      const int o_f = o_pot + 3;
+      Flag f = {r[o_f], r[o_f + 1], (int)r[o_f + 2], 0};
+      flag_pack<R>(in, is_step ? act : nullptr, obs, po, f, [&](Flag& g) {
+        g.tx = r[o_f + 3]; g.ty = r[o_f + 4]; g.timeout = PBG_FLAG_TIMEOUT; g.count++;
+      });
+      w[R::OBS + 4 + R::NF] = f.tx;
+      w[R::OBS + 4 + R::NF + 1] = f.ty;
+      w[R::OBS + 4 + R::NF + 2] = f.timeout;
+    } else if (in.n_parts == R::NP || in.n_parts == R::NP + 1) {
+      // the step's part counts take the kernels' compile-time path (what this test pins)
+      walker_pack<R>(in, is_step ? act : nullptr, obs, po);
+    } else {
+      walker_pack<R, true>(in, is_step ? act : nullptr, obs, po);
+    }
   }
   if (!is_step) { po.reward = 0.0; po.done = false; }
 #pragma unroll
@@ -1450,7 +1517,7 @@ template <class R>
 __global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __restrict__ phys, double* __restrict__ aux) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
-  constexpr int SD = Dims<R>::SD, AD = PBG_AUX_WORDS + R::NF;
+  constexpr int SD = Dims<R>::SD, AD = Records<R>::AD;
   for (int i = 0; i < SD; i++) phys[(size_t)e * SD + i] = (double)B.st[(size_t)i * B.n + e];
   double* a = aux + (size_t)e * AD;
   a[0] = B.pot[e];
@@ -1458,12 +1525,16 @@ __global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __rest
   a[2] = (double)B.elapsed[e];
   a[3] = (double)(B.flags[e] & 1u);
   for (int f = 0; f < R::NF; f++) a[4 + f] = (double)((B.flags[e] >> (8 + f)) & 1u);
+  if constexpr (R::flagrun) {
+    const Flag fl = load_flag<R>(B, e);
+    a[4 + R::NF] = fl.tx; a[5 + R::NF] = fl.ty; a[6 + R::NF] = fl.timeout; a[7 + R::NF] = fl.count;
+  }
 }
 template <class R>
 __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* __restrict__ phys, const double* __restrict__ aux) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
-  constexpr int SD = Dims<R>::SD, AD = PBG_AUX_WORDS + R::NF;
+  constexpr int SD = Dims<R>::SD, AD = Records<R>::AD;
   for (int i = 0; i < SD; i++) B.st[(size_t)i * B.n + e] = (float)phys[(size_t)e * SD + i];
   if (aux) {
     const double* a = aux + (size_t)e * AD;
@@ -1473,6 +1544,8 @@ __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* 
     uint32_t fl = a[3] != 0.0 ? 1u : 0u;
     for (int f = 0; f < R::NF; f++) fl |= (a[4 + f] != 0.0 ? 1u : 0u) << (8 + f);
     B.flags[e] = fl;
+    if constexpr (R::flagrun)
+      store_flag<R>(B, e, Flag{a[4 + R::NF], a[5 + R::NF], (int)a[6 + R::NF], (int)a[7 + R::NF]});
   }
 }
 

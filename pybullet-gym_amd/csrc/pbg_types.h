@@ -11,6 +11,8 @@ struct Buffers {
   int* elapsed;            // [n] steps in episode
   uint32_t* flags;         // [n] bit0 floor-in-parts, bits 8.. feet_contact
   uint32_t* episode;       // [n] resets so far (RNG counter)
+  double* tgt;             // [2][n] walk target x, y (HumanoidFlagrun)
+  int32_t* ftm;            // [2][n] flag_timeout, flag draws so far (HumanoidFlagrun RNG counter)
   uint64_t seed;
   int env_offset;          // global id of env 0 (multi-GPU sharding)
 };

@@ -18,6 +18,12 @@
 #define PBG_ANGULAR_MOTION_THRESHOLD 0.7853981633974483  // [EXT] 0.5*SIMD_HALF_PI
 #define PBG_WALK_TARGET_X 1000.0        // robot_locomotors.py:12 walk_target_x = 1e3
 #define PBG_WALK_TARGET_Y 0.0           // robot_locomotors.py:13
+// HumanoidFlagrun (robot_locomotors.py:203-213): flag at U(+-halflen) x U(+-halfwidth) times
+// 0.5, re-drawn when the walk target is within 1 m or after 600 / frame_skip calc_states
+#define PBG_STADIUM_HALFLEN 26.25       // scene_stadium.py:14 105*0.25
+#define PBG_STADIUM_HALFWIDTH 12.5      // scene_stadium.py:15 50*0.25
+#define PBG_FLAG_COMPACT 0.5            // robot_locomotors.py:206 more_compact
+#define PBG_FLAG_TIMEOUT 150            // robot_locomotors.py:216 600/frame_skip
 #define PBG_OBS_CLIP 5.0                // robot_locomotors.py:64 np.clip(..., -5, +5)
 #define PBG_JOINT_AT_LIMIT 0.99f        // robot_locomotors.py:36 (float32 compare)
 
@@ -31,4 +37,5 @@
 // Per-env bookkeeping record (float64):
 //   [0] potential  [1] initial_z  [2] elapsed steps  [3] floor-in-parts flag
 //   [4 .. 4+NF) feet_contact (as written into the observation)
+//   HumanoidFlagrun only: [4+NF .. 4+NF+4) walk target x, y, flag_timeout, flag draws so far
 #define PBG_AUX_WORDS 4

@@ -107,6 +107,7 @@ Walker2D = _robot_class("walker2d", "Walker2D")              # :93-106
 HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
 Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
+HumanoidFlagrun = _robot_class("humanoid_flagrun", "HumanoidFlagrun")  # :195-226
 InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
 InvertedPendulumSwingup = _robot_class("pendulum_swingup", "InvertedPendulumSwingup")  # robot_pendula.py:54-55
 InvertedDoublePendulum = _robot_class("double_pendulum", "InvertedDoublePendulum")      # robot_pendula.py:58-88
@@ -130,6 +131,7 @@ Hopper.alive_bonus = _alive_bonus_hopper
 Walker2D.alive_bonus = _alive_bonus_hopper  # robot_locomotors.py:100-101 (same rule as Hopper)
 Ant.alive_bonus = _alive_bonus_ant
 Humanoid.alive_bonus = _alive_bonus_humanoid
+HumanoidFlagrun.alive_bonus = _alive_bonus_humanoid
 
 
 # ----------------------------------------------------------------------------- envs
@@ -271,6 +273,16 @@ class HumanoidBulletEnv(WalkerBaseBulletEnv):
         self.stall_torque_cost = 4.25 * WalkerBaseBulletEnv.stall_torque_cost
 
 
+class HumanoidFlagrunBulletEnv(HumanoidBulletEnv):
+    """gym_locomotion_envs.py:154-164: the Humanoid chasing a flag that is re-drawn
+    (U(+-13.125) x U(+-6.25)) when reached within 1 m or after 150 steps; the walk target and
+    flag_timeout live in the device state (aux words), the draws are Philox (not np_random)."""
+    env_id = "HumanoidFlagrunPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        HumanoidBulletEnv.__init__(self, HumanoidFlagrun(), render, device)
+
+
 class InvertedPendulumBulletEnv(BaseBulletEnv):
     """gym_pendulum_envs.py:7-42: obs float64 [x, vx, cos(theta), sin(theta), theta_dot]."""
     env_id = "InvertedPendulumPyBulletEnv-v0"
@@ -327,6 +339,7 @@ ENV_CLASSES = {
     "HalfCheetahPyBulletEnv-v0": HalfCheetahBulletEnv,
     "AntPyBulletEnv-v0": AntBulletEnv,
     "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
+    "HumanoidFlagrunPyBulletEnv-v0": HumanoidFlagrunBulletEnv,
 }
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}

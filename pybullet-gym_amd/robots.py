@@ -48,6 +48,7 @@ class RobotSpec:
     max_episode_steps: int = 1000                                # envs/__init__.py
     self_collision: bool = True
     reset_offset: float = 0.0                                    # swingup hinge 3.1415 + u
+    flagrun: bool = False                                        # HumanoidFlagrun walk target
 
 
 SPECS: Dict[str, RobotSpec] = OrderedDict()
@@ -104,6 +105,14 @@ _add(RobotSpec("HumanoidPyBulletEnv-v0", "humanoid", "humanoid_symmetric.xml", "
                            "right_shoulder1": 75, "right_shoulder2": 75, "right_elbow": 75,
                            "left_shoulder1": 75, "left_shoulder2": 75, "left_elbow": 75},
                initial_z=0.8, electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1))
+
+# HumanoidFlagrun: robot_locomotors.py:195-226 (flag_reposition / calc_state), the Humanoid
+# physics and rewards (gym_locomotion_envs.py:146-163), envs/__init__.py:86-91
+_add(RobotSpec("HumanoidFlagrunPyBulletEnv-v0", "humanoid_flagrun", "humanoid_symmetric.xml", "torso",
+               action_dim=17, obs_dim=44, kind=KIND_WALKER, power=0.41, foot_list=["right_foot", "left_foot"],
+               alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
+               power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8,
+               electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1, flagrun=True))
 
 ENV_IDS = {s.env_id: s for s in SPECS.values()}
 

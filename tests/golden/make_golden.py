@@ -46,6 +46,7 @@ ROBOTS = {
     "walker2d": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "Walker2DBulletEnv"),
     "pendulum_swingup": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedPendulumSwingupBulletEnv"),
     "double_pendulum": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedDoublePendulumBulletEnv"),
+    "humanoid_flagrun": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidFlagrunBulletEnv"),
 }
 
 
@@ -157,6 +158,7 @@ class FakeClient:
         self.q = np.zeros(self.L)
         self.qd = np.zeros(self.L)
         self.saved = None
+        self.target_hook = None
         self.new_state(initial=True)
 
     # --- state script
@@ -169,6 +171,11 @@ class FakeClient:
         vs = 30.0 if rng.random() < 0.1 else 2.0
         self.base_lin = tuple(float(v) for v in rng.normal(0, vs, 3))
         self.base_ang = tuple(float(v) for v in rng.normal(0, 2.0, 3))
+        if self.target_hook is not None and not initial and rng.random() < 0.08:
+            # HumanoidFlagrun: put the body next to the flag (walk_target_dist < 1 re-draws it)
+            tx, ty = self.target_hook()
+            self.base_pos = (float(tx + rng.uniform(-0.3, 0.3)), float(ty + rng.uniform(-0.3, 0.3)),
+                             self.base_pos[2])
         self.link_pos = [tuple(float(v) for v in np.array(self.base_pos) + rng.normal(0, 0.5, 3)) for _ in range(L)]
         self.link_orn = [rand_quat(rng, 0.7) for _ in range(L)]
         self.link_lin = [tuple(float(v) for v in rng.normal(0, vs, 3)) for _ in range(L)]
@@ -197,6 +204,8 @@ class FakeClient:
     def setJointMotorControl2(self, *a, **k): pass
     def loadSDF(self, path): return (self.floor_uid,)
     def loadMJCF(self, path, flags=0): return (self.robot_uid,)
+    def loadURDF(self, path, pos=None, *a, **k): return 5  # HumanoidFlagrun's flag sphere (no collision)
+    def resetBasePositionAndOrientation(self, *a, **k): pass
     def saveState(self): return 3
     def restoreState(self, sid): self.q[:] = 0.0; self.qd[:] = 0.0
     def stepSimulation(self): self.new_state()
@@ -276,9 +285,11 @@ def generate(key, episodes=3, steps=40, seed=1234):
     env_bases.bullet_client.BulletClient = lambda connection_mode=None: fake
     env = getattr(envmod, clsname)()
     robot = env.robot
+    if t.get("flagrun"):
+        fake.target_hook = lambda: (robot.walk_target_x, robot.walk_target_y)
     rec = {k: [] for k in ("kind", "part_xyz", "n_parts", "body_quat", "body_pos", "body_vel", "jq", "jqd",
                            "feet_prev", "feet_new", "act", "potential_old", "initial_z_in", "obs", "reward",
-                           "done", "potential", "feet_out", "initial_z_out", "rewards")}
+                           "done", "potential", "feet_out", "initial_z_out", "rewards", "flag_in", "flag_out")}
     part_names = []
     captured = {}
     calc_cls = type(robot)
@@ -295,6 +306,9 @@ def generate(key, episodes=3, steps=40, seed=1234):
             captured["jq"] = np.array([s[0] for s in js]); captured["jqd"] = np.array([s[1] for s in js])
             captured["feet_prev"] = np.array(self.feet_contact, dtype=np.float32)
             captured["initial_z_in"] = np.nan if self.initial_z is None else float(self.initial_z)
+            if t.get("flagrun"):  # walk target and flag_timeout before HumanoidFlagrun.calc_state
+                captured["flag_before"] = (float(self.walk_target_x), float(self.walk_target_y),
+                                           float(self.flag_timeout))
         else:
             js = [self.j1, self.j2, self.slider] if hasattr(self, "j2") else [self.j1, self.slider]
             captured["jq"] = np.array([j.get_state()[0] for j in js])
@@ -325,6 +339,13 @@ def generate(key, episodes=3, steps=40, seed=1234):
                 fn[i] = fake.contacts[t["link_name"].index(f)]
             rec["feet_new"].append(fn)
             rec["initial_z_in"].append(captured["initial_z_in"])
+            if t.get("flagrun"):
+                bx, by, bt = captured["flag_before"]
+                after = (float(robot.walk_target_x), float(robot.walk_target_y), float(robot.flag_timeout))
+                moved = after[:2] != (bx, by)
+                # the draw a reposition took (NaN: none happened during this calc_state)
+                rec["flag_in"].append([bx, by, bt, after[0] if moved else np.nan, after[1] if moved else np.nan])
+                rec["flag_out"].append(list(after))
             rec["initial_z_out"].append(float(robot.initial_z))
             part_names.append(captured["part_names"])
         elif "body_pos" in captured:
@@ -363,7 +384,8 @@ def main():
     install_stubs()
     sys.path.insert(0, REF)
     for key in (sys.argv[1:] or ROBOTS):
-        data = generate(key)
+        # flagrun: long enough for flag_timeout (150 calc_states) to run out
+        data = generate(key, episodes=2, steps=170) if key == "humanoid_flagrun" else generate(key)
         path = os.path.join(HERE, f"pack_{key}.npz")
         np.savez_compressed(path, **data)
         print(key, "calls", len(data["kind"]), "->", os.path.relpath(path, REPO))

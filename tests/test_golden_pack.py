@@ -8,7 +8,7 @@ import pytest
 import oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d"]
+WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d", "humanoid_flagrun"]
 
 
 def load(key):
@@ -36,8 +36,11 @@ def test_oracle_pack_bit_exact(key):
         out = oracle.pack(key, g["part_xyz"][i][: g["n_parts"][i]], g["body_quat"][i], g["body_pos"][i],
                           g["body_vel"][i], g["jq"][i], g["jqd"][i], g["feet_prev"][i],
                           g["feet_new"][i] if step else None, g["act"][i] if step else None,
-                          g["potential_old"][i], g["initial_z_in"][i])
+                          g["potential_old"][i], g["initial_z_in"][i],
+                          flag=g["flag_in"][i] if "flag_in" in g.files else None)
         ref_obs = g["obs"][i].astype(np.float32)
+        if "flag_out" in g.files:  # HumanoidFlagrun: target and flag_timeout after calc_state
+            np.testing.assert_array_equal(out["flag_out"], g["flag_out"][i], err_msg=f"call {i}")
         assert out["obs"].dtype == np.float32
         np.testing.assert_array_equal(out["obs"].view(np.uint32), ref_obs.view(np.uint32), err_msg=f"call {i}")
         assert out["potential"] == pytest.approx(g["potential"][i], abs=1e-9, rel=0)

@@ -26,7 +26,8 @@ pytestmark = pytest.mark.gpu
 
 ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
         "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
-        "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0"]
+        "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
+        "HumanoidFlagrunPyBulletEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -74,6 +75,8 @@ def test_device_pack_matches_reference_golden(env_id):
         rec[i, o] = g["potential_old"][i]
         rec[i, o + 1] = g["initial_z_in"][i] if info.kind == 0 else 0.0
         rec[i, o + 2] = float(g["kind"][i] == 1)
+        if "flag_in" in g.files:  # HumanoidFlagrun: target, flag_timeout, the recorded re-draw
+            rec[i, o + 3:o + 8] = g["flag_in"][i]
     out = pack(env_id, torch.from_numpy(rec).cuda()).cpu().numpy()
     obs = out[:, : info.OBS].astype(np.float32)
     ref = g["obs"].astype(np.float32)
@@ -84,7 +87,9 @@ def test_device_pack_matches_reference_golden(env_id):
     if info.kind == 0:
         np.testing.assert_allclose(out[:, info.OBS + 2], g["potential"], atol=1e-9, rtol=0)
         np.testing.assert_array_equal(out[:, info.OBS + 3], g["initial_z_out"])
-        np.testing.assert_array_equal(out[:, info.OBS + 4:], g["feet_out"][:, : info.NF])
+        np.testing.assert_array_equal(out[:, info.OBS + 4:info.OBS + 4 + info.NF], g["feet_out"][:, : info.NF])
+    if "flag_out" in g.files:
+        np.testing.assert_array_equal(out[:, info.OBS + 4 + info.NF:], g["flag_out"])
 
 
 # ------------------------------------------------------------------ reset
@@ -92,7 +97,7 @@ def test_device_pack_matches_reference_golden(env_id):
 def test_reset_matches_oracle(env_id):
     n = 128
     env = VecEnv(env_id, n, seed=5, autoreset=False)
-    orc = oracle.OracleEnvs(env_id, n)
+    orc = oracle.OracleEnvs(env_id, n, seed=5)
     q0 = np.random.default_rng(0).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
     obs = env.reset(init_q=torch.from_numpy(q0)).cpu().numpy()
     obs_o = orc.reset(q0.astype(np.float64))
@@ -123,7 +128,7 @@ def test_rng_reset_matches_host_philox(env_id):
 def test_step_teacher_forced_parity(env_id):
     n, steps = 256, 40
     env = VecEnv(env_id, n, seed=3, autoreset=False)
-    orc = oracle.OracleEnvs(env_id, n, nthreads=8)
+    orc = oracle.OracleEnvs(env_id, n, nthreads=8, seed=3)
     r = np.random.default_rng(1)
     q0 = r.uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
     env.reset(init_q=torch.from_numpy(q0))
@@ -404,3 +409,32 @@ def test_gang_kernel_determinism_and_offset_invariance(env_id):
     a = run(97, 0)
     np.testing.assert_array_equal(a, run(97, 0))
     np.testing.assert_array_equal(a[:, 41:], run(56, 41))
+
+
+# ------------------------------------------------------------------ HumanoidFlagrun
+def test_flagrun_redraws_match_oracle():
+    """HumanoidFlagrun's flag bookkeeping (robot_locomotors.py:219-226) over 155 teacher-forced
+    steps, past the 150-calc_state timeout: walk target, flag_timeout and the draw counter
+    identical to the oracle's (same Philox stream), obs within the step tolerances."""
+    n, steps, seed = 64, 155, 17
+    env = VecEnv("HumanoidFlagrunPyBulletEnv-v0", n, seed=seed, autoreset=False)
+    orc = oracle.OracleEnvs("HumanoidFlagrunPyBulletEnv-v0", n, nthreads=8, seed=seed)
+    r = np.random.default_rng(2)
+    env.reset(init_q=torch.from_numpy(r.uniform(-0.1, 0.1, (n, 17)).astype(np.float32)))
+    NF = env.info.n_feet
+    errs, redraws = [], 0
+    for t in range(steps):
+        phys, aux = env.get_state()
+        orc.state[:] = phys.cpu().numpy()
+        orc.aux[:] = aux.cpu().numpy()
+        before = orc.aux[:, 4 + NF + 3].copy()
+        a = r.uniform(-1, 1, (n, 17)).astype(np.float32)
+        og = env.step(torch.from_numpy(a).cuda()).obs.cpu().numpy()
+        oo, _, _, _ = orc.step(a)
+        _, aux2 = env.get_state()
+        np.testing.assert_array_equal(aux2.cpu().numpy()[:, 4 + NF:], orc.aux[:, 4 + NF:])
+        redraws += int((orc.aux[:, 4 + NF + 3] != before).sum())
+        errs.append(np.abs(og - oo).max(axis=1))
+    assert redraws >= n  # every env's flag timed out at least once
+    e = np.concatenate(errs)
+    assert np.median(e) <= 1e-4 and np.percentile(e, 99) <= 1e-2
