@@ -49,7 +49,7 @@ int g_flags = 0;
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
       floor, max_steps, robot_body, tip_link, flagrun;
-  double power, elec, stall, jal, z0fixed, dt_sub, base_mass;
+  double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
   const double (*off_pos)[3], (*axis)[3], (*anchor)[3], (*com)[3], (*off_quat)[4], (*inertia)[6];
@@ -74,7 +74,7 @@ MV view() {
   m.flagrun = R::flagrun;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
-  m.base_mass = R::base_mass; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
+  m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
   m.base_quat = R::base_quat; m.link_parent = R::link_parent; m.link_jtype = R::link_jtype;
   m.link_dof = R::link_dof; m.off_pos = R::link_offset_pos; m.axis = R::link_axis;
   m.anchor = R::link_anchor; m.com = R::link_com; m.off_quat = R::link_offset_quat;
@@ -91,12 +91,13 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[9] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
-                        view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
-                        view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
-                        view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
-                        view<pbg_models::HumanoidFlagrun>()};
-  if (robot < 0 || robot > 8) return nullptr;
+  static MV views[12] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+                         view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
+                         view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
+                         view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
+                         view<pbg_models::HumanoidFlagrun>(), view<pbg_models::HopperMuJoCo>(),
+                         view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>()};
+  if (robot < 0 || robot > 11) return nullptr;
   return &views[robot];
 }
 
@@ -708,6 +709,8 @@ int pbg_oracle_info(int robot, int* out) {
 
 static void pendulum_obs(const MV& m, const double* jq, const double* jqd, const double* tip, float* obs,
                          double* rew, uint8_t* done);
+static void mujoco_planar_obs(const MV& m, const double* jq, const double* jqd, double x_after, double x_before,
+                              const float* act, pbg_pack_out* out);
 
 // Walker pack: calc_state (robot_locomotors.py:31-64) + the reward/done part of
 // WalkerBaseBulletEnv._step (gym_locomotion_envs.py:59-114).  With act == NULL only the
@@ -716,6 +719,10 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
+  if (m.kind == 2) {  // MuJoCo planar: jq/jqd all ordered joints, body_pos = robot_body, potential_old = x_before
+    mujoco_planar_obs(m, in->jq, in->jqd, in->body_pos[0], in->potential_old, in->act, out);
+    return 0;
+  }
   if (m.kind == 1) {  // pendulums: jq/jqd = (hinge, [hinge2,] slider), pos = pole2 position
     pendulum_obs(m, in->jq, in->jqd, in->body_pos, out->obs, &out->reward, &out->done);
     if (!in->act) { out->reward = 0; out->done = 0; }
@@ -851,6 +858,42 @@ int pbg_oracle_pack_flag(int robot, const pbg_pack_in* in, pbg_pack_out* out, co
   return 0;
 }
 
+// MuJoCo-observation planar walkers (mujoco robot_locomotors.py:93-196, mujoco
+// gym_locomotion_envs.py:121-252): obs float32 [qpos[1:], clip(qvel, +-10)] (HalfCheetah
+// unclipped) over every ordered joint incl. the ignored root joints; potential =
+// (x_after - x_before) / dt; reward = sum([potential, 1.0, c * sum(a^2) (float32)]).
+static void mujoco_planar_obs(const MV& m, const double* jq, const double* jqd, double x_after, double x_before,
+                              const float* act, pbg_pack_out* out) {
+  const float c = (float)m.qvel_clip;
+  int o = 0;
+  for (int i = 1; i < m.NO; i++) out->obs[o++] = (float)jq[i];
+  for (int i = 0; i < m.NO; i++) {
+    const float v = (float)jqd[i];
+    out->obs[o++] = c > 0.f ? (v < -c ? -c : (v > c ? c : v)) : v;
+  }
+  out->potential = x_after; out->initial_z = 0.0; out->dist = 0.0;
+  for (int i = 0; i < 5; i++) out->rewards[i] = 0.0;
+  if (!act) { out->reward = 0.0; out->done = 0; return; }
+  const double potential = (x_after - x_before) / (m.dt_sub * m.substeps);
+  float sq[MAXD];
+  for (int i = 0; i < m.NA; i++) sq[i] = act[i] * act[i];
+  const float power_cost = (float)m.power_cost * np_sum_f32(sq, m.NA);
+  bool finite = true, small = true;
+  for (int i = 0; i < m.OBS; i++) {
+    finite = finite && isfinite(out->obs[i]);
+    if (i >= 2) small = small && fabsf(out->obs[i]) < 100.f;
+  }
+  const float h = out->obs[0], ang = out->obs[1];
+  if (m.alive == 12) {
+    out->reward = (0.0 + potential) + (double)power_cost;
+    out->done = 0;
+  } else {
+    out->reward = ((0.0 + potential) + 1.0) + (double)power_cost;
+    out->done = m.alive == 10 ? !(finite && small && h > -0.3f && fabsf(ang) < 0.2f)
+                              : !(finite && small && (1.0f > h && h > -0.2f) && (-1.0f < ang && ang < 1.0f));
+  }
+}
+
 // Pendulum packs: calc_state + reward/done.  obs is float64 in the reference; written here
 // as float32 (the C-ABI's obs dtype).
 //  * InvertedPendulum / Swingup (robot_pendula.py:27-51, gym_pendulum_envs.py:26-39): non-finite
@@ -895,6 +938,25 @@ static void pendulum_pack(const MV& m, const double* s, float* obs, double* rew,
   pendulum_obs(m, jq, jqd, tip, obs, rew, done);
 }
 
+// MuJoCo planar pack from a physical state; returns x_after (robot_body COM x).
+static double mujoco_planar_pack(const MV& m, const double* s, double x_before, const float* act, float* obs,
+                                 double* rew, uint8_t* done) {
+  const double* q = s + PBG_BASE_WORDS;
+  const double* qd = q + m.NJ;
+  double jq[MAXD], jqd[MAXD];
+  for (int i = 0; i < m.NO; i++) { jq[i] = q[m.obs_dof[i]]; jqd[i] = qd[m.obs_dof[i]]; }
+  static thread_local Kin k;
+  forward_kinematics(m, s, k);
+  const double x_after = k.c[m.robot_body + 1].x;
+  float feet[8];
+  pbg_pack_out out;
+  out.obs = obs; out.feet_out = feet;
+  mujoco_planar_obs(m, jq, jqd, x_after, x_before, act, &out);
+  if (rew) *rew = out.reward;
+  if (done) *done = out.done;
+  return x_after;
+}
+
 // Gather the pack inputs from a physical state.
 static void gather(const MV& m, const double* s, const double* aux, Kin& k, double* part_xyz,
                    int& n_parts, double* quat, double* pos, double* vel, double* jq, double* jqd) {
@@ -936,6 +998,7 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
     a[2] = 0.0;
     for (int i = 0; i < m.NF; i++) a[4 + i] = 0.0;
     if (m.kind == 1) { pendulum_pack(m, s, ob, nullptr, nullptr); a[3] = 1.0; continue; }
+    if (m.kind == 2) { a[0] = mujoco_planar_pack(m, s, 0.0, nullptr, ob, nullptr, nullptr); a[3] = 1.0; continue; }
     static thread_local Kin k;
     double part_xyz[3 * (MAXL + 2)], quat[4], pos[3], vel[3], jq[MAXD], jqd[MAXD];
     int n_parts;
@@ -982,6 +1045,7 @@ int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* a
     a[2] += 1.0;
     float* ob = obs + (size_t)e * m.OBS;
     if (m.kind == 1) { pendulum_pack(m, s, ob, rew + e, done + e); continue; }
+    if (m.kind == 2) { a[0] = mujoco_planar_pack(m, s, a[0], ac, ob, rew + e, done + e); continue; }
     uint8_t feet_new[8];
     for (int f = 0; f < m.NF; f++) {
       feet_new[f] = 0;

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "libpbg_amd.so")
 ROBOT_IDS = {"InvertedPendulumPyBulletEnv-v0": 0, "HopperPyBulletEnv-v0": 1, "HalfCheetahPyBulletEnv-v0": 2,
              "AntPyBulletEnv-v0": 3, "HumanoidPyBulletEnv-v0": 4, "Walker2DPyBulletEnv-v0": 5,
              "InvertedPendulumSwingupPyBulletEnv-v0": 6, "InvertedDoublePendulumPyBulletEnv-v0": 7,
-             "HumanoidFlagrunPyBulletEnv-v0": 8}
+             "HumanoidFlagrunPyBulletEnv-v0": 8, "HopperMuJoCoEnv-v0": 9, "Walker2DMuJoCoEnv-v0": 10,
+             "HalfCheetahMuJoCoEnv-v0": 11}
 
 
 class PbgError(RuntimeError):

@@ -56,6 +56,15 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         act_gain = [100.0]
         reset_dof = [links[model.link_index("pole")].dof]
         obs_links = [model.link_index("pole"), model.link_index("cart")]
+    elif spec.kind == robots.KIND_MUJOCO_PLANAR:
+        # mujoco/robot_bases.py:82-95 add_ignored_joints: the ignored root joints join
+        # ordered_joints (power_coef 0, skipped by apply_action, mujoco robot_locomotors.py:26-33)
+        # and are re-randomised at reset (:17-19) and read by calc_state like the others.
+        all_ordered = [i for i, l in enumerate(links) if l.dof >= 0 and l.joint_name[:8] != "jointfix"]
+        act_links = list(ordered)
+        act_gain = [spec.power * spec.power_coef.get(links[i].joint_name, 100.0) for i in ordered]
+        reset_dof = [links[i].dof for i in all_ordered]
+        obs_links = all_ordered
     else:
         act_links = list(ordered)
         act_gain = [spec.power * spec.power_coef.get(links[i].joint_name, 100.0)  # robot_locomotors.py:29,
@@ -159,7 +168,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         dof_link=dof["link"],
         act_dof=act_dof, act_gain=act_gain, obs_dof=obs_dof, obs_vel_scale=vel_scale,
         reset_dof=reset_dof, reset_offset=[spec.reset_offset if i == 0 else 0.0 for i in range(len(reset_dof))],
-        tip_link=tip_link, flagrun=int(spec.flagrun),
+        tip_link=tip_link, flagrun=int(spec.flagrun), power_cost=spec.power_cost, qvel_clip=spec.qvel_clip,
         act_joint_names=ordered_names,
         part_names=list(parts.keys()), part_link=list(parts.values()), robot_body=robot_body,
         foot_link=feet,
@@ -226,7 +235,7 @@ def emit_struct(t: Dict) -> str:
               "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
-              "initial_z_fixed", "dt_sub", "base_mass"):
+              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip"):
         L.append(f"  static constexpr double {k} = {_num(t[k])};")
     L.append(_arr1("base_inertia", "double", t["base_inertia"]))
     L.append(_arr1("base_pos", "double", t["base_pos"]))
@@ -273,10 +282,13 @@ def emit_struct(t: Dict) -> str:
 
 
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
-             "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8}
+             "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
+             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
-           "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun"}
+           "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun",
+           "hopper_mujoco": "HopperMuJoCo", "walker2d_mujoco": "Walker2DMuJoCo",
+           "halfcheetah_mujoco": "HalfCheetahMuJoCo"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -881,6 +881,9 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   Flag fl = load_flag<R>(B, e);
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
+  } else if constexpr (R::kind == 2) {
+    mujoco_planar_pack_state<R>(s, B.pot[e], act, obs, po);
+    pot_new = po.potential;
   } else {
     PackIn<R> in;
     gather<R>(s, flags & 1u, in);

@@ -40,4 +40,7 @@ PBG_DECLARE_ROBOT(Walker2D)
 PBG_DECLARE_ROBOT(PendulumSwingup)
 PBG_DECLARE_ROBOT(DoublePendulum)
 PBG_DECLARE_ROBOT(HumanoidFlagrun)
+PBG_DECLARE_ROBOT(HopperMuJoCo)
+PBG_DECLARE_ROBOT(Walker2DMuJoCo)
+PBG_DECLARE_ROBOT(HalfCheetahMuJoCo)
 }  // namespace pbg

@@ -1151,6 +1151,61 @@ PBG_DEV void store_flag(const Buffers& B, int e, const Flag& f) {
   if constexpr (R::flagrun) { B.tgt[e] = f.tx; B.tgt[B.n + e] = f.ty; B.ftm[e] = f.timeout; B.ftm[B.n + e] = f.count; }
 }
 
+// MuJoCo-observation planar walkers (envs/mujoco, add_ignored_joints=True):
+// calc_state = [qpos[1:], clip(qvel, -10, 10)] (HalfCheetah: qvel unclipped) over every
+// ordered joint incl. the ignored root joints, float32 (mujoco robot_locomotors.py:93-102,
+// 124-133, 172-181); calc_potential = (x_after - x_before) / dt of robot_body's x (:104-121);
+// reward = sum([potential, alive 1.0, power_cost]) with power_cost = c * sum(a^2) in float32
+// (HalfCheetah: no alive term), done per robot (mujoco gym_locomotion_envs.py:121-252).
+// out.potential carries x_after (the next step's x_before).
+template <class R>
+PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_after, double x_before, const float* act,
+                                float* obs, PackOut& out) {
+  constexpr int NO = R::NO;
+  constexpr float c = (float)R::qvel_clip;
+  int o = 0;
+#pragma unroll
+  for (int i = 1; i < NO; i++) obs[o++] = (float)jq[i];
+#pragma unroll
+  for (int i = 0; i < NO; i++) {
+    const float v = (float)jqd[i];
+    obs[o++] = c > 0.f ? (v < -c ? -c : (v > c ? c : v)) : v;  // np.clip keeps NaN
+  }
+  out.potential = x_after; out.initial_z = 0.0; out.dist = 0.0; out.feet_out = 0;
+  if (!act) { out.reward = 0.0; out.done = false; return; }
+  const double potential = (x_after - x_before) / (R::dt_sub * R::substeps);
+  float sq[R::NA];
+#pragma unroll
+  for (int i = 0; i < R::NA; i++) sq[i] = act[i] * act[i];
+  const float power_cost = (float)R::power_cost * np_sum_n<R::NA>(sq);
+  bool finite = true, small = true;
+#pragma unroll
+  for (int i = 0; i < R::OBS; i++) {
+    finite &= isfinite(obs[i]);
+    if (i >= 2) small &= fabsf(obs[i]) < 100.f;
+  }
+  const float height = obs[0], ang = obs[1];
+  if constexpr (R::alive == 12) {  // HalfCheetah: never done
+    out.reward = (0.0 + potential) + (double)power_cost;
+    out.done = false;
+  } else {
+    out.reward = ((0.0 + potential) + 1.0) + (double)power_cost;
+    if constexpr (R::alive == 10)  // Hopper
+      out.done = !(finite && small && height > -0.3f && fabsf(ang) < 0.2f);
+    else  // Walker2D
+      out.done = !(finite && small && (1.0f > height && height > -0.2f) && (-1.0f < ang && ang < 1.0f));
+  }
+}
+template <class R>
+PBG_DEV void mujoco_planar_pack_state(const State<R>& s, double x_before, const float* act, float* obs, PackOut& po) {
+  double jq[R::NO], jqd[R::NO];
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) { jq[i] = s.q[R::obs_dof[i]]; jqd[i] = s.qd[R::obs_dof[i]]; }
+  Kin<R> k;
+  fk_pos<R>(s, k);
+  mujoco_planar_pack<R>(jq, jqd, (double)k.c[R::robot_body + 1].x, x_before, act, obs, po);
+}
+
 // Pendulum packs (obs float64 in the reference, float32 through the C-ABI).
 //  InvertedPendulum / Swingup: robot_pendula.py:27-51 + gym_pendulum_envs.py:26-39 --
 //  non-finite vx / theta / theta_dot replaced by 0; balance: reward 1, done |theta| > .2;
@@ -1308,6 +1363,11 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
     pendulum_pack<R>(s, obs, po);
     has_floor = true; pot = 0.0; z0 = 0.f;
     return;
+  } else if constexpr (R::kind == 2) {
+    // reset: calc_state, then env.potential = calc_potential() stores x_after (env_bases.py:69-70)
+    mujoco_planar_pack_state<R>(s, 0.0, nullptr, obs, po);
+    has_floor = true; pot = po.potential; z0 = 0.f;
+    return;
   } else {
   PackIn<R> in;
   gather<R>(s, has_floor, in);
@@ -1392,6 +1452,9 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   double pot_new = 0.0;
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
+  } else if constexpr (R::kind == 2) {
+    mujoco_planar_pack_state<R>(s, B.pot[e], act, obs, po);
+    pot_new = po.potential;
   } else {
     PackIn<R> in;
     gather<R>(s, flags & 1u, in);
@@ -1467,6 +1530,9 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
   for (int i = 0; i < R::NA; i++) act[i] = (float)r[o_act + i];
   if constexpr (R::kind == 1) {
     pendulum_obs<R>(r + o_jq, r + o_jqd, r + o_pos, obs, po);  // pos: pole2 position (double pendulum)
+  } else if constexpr (R::kind == 2) {
+    // pos: robot_body position (x_after), potential_old: x_before
+    mujoco_planar_pack<R>(r + o_jq, r + o_jqd, r[o_pos], r[o_pot], is_step ? act : nullptr, obs, po);
   } else {
     PackIn<R> in;
     in.n_parts = (int)r[o_np];

@@ -86,13 +86,14 @@ class WalkerBase(XmlBasedRobot):
 def _robot_class(key, base_cls):
     spec = _robots.spec_for(key)
 
-    bases = (WalkerBase, MJCFBasedRobot) if spec.kind == _robots.KIND_WALKER else (MJCFBasedRobot,)
+    walker = spec.kind in (_robots.KIND_WALKER, _robots.KIND_MUJOCO_PLANAR)
+    bases = (WalkerBase, MJCFBasedRobot) if walker else (MJCFBasedRobot,)
 
     class _R(*bases):
         foot_list = list(spec.foot_list)
 
         def __init__(self):
-            if spec.kind == _robots.KIND_WALKER:
+            if walker:
                 WalkerBase.__init__(self, power=spec.power)
             MJCFBasedRobot.__init__(self, spec.mjcf, spec.robot_name, action_dim=spec.action_dim,
                                     obs_dim=spec.obs_dim)
@@ -108,6 +109,9 @@ HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
 Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
 HumanoidFlagrun = _robot_class("humanoid_flagrun", "HumanoidFlagrun")  # :195-226
+HopperMuJoCo = _robot_class("hopper_mujoco", "Hopper")                # mujoco/robot_locomotors.py:82-121
+Walker2DMuJoCo = _robot_class("walker2d_mujoco", "Walker2D")          # :124-164
+HalfCheetahMuJoCo = _robot_class("halfcheetah_mujoco", "HalfCheetah")  # :167-207
 InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
 InvertedPendulumSwingup = _robot_class("pendulum_swingup", "InvertedPendulumSwingup")  # robot_pendula.py:54-55
 InvertedDoublePendulum = _robot_class("double_pendulum", "InvertedDoublePendulum")      # robot_pendula.py:58-88
@@ -283,6 +287,38 @@ class HumanoidFlagrunBulletEnv(HumanoidBulletEnv):
         HumanoidBulletEnv.__init__(self, HumanoidFlagrun(), render, device)
 
 
+class WalkerBaseMuJoCoEnv(WalkerBaseBulletEnv):
+    """envs/mujoco/gym_locomotion_envs.py:8-118 (MuJoCo-style observations on the same
+    pybullet physics)."""
+
+
+class HopperMuJoCoEnv(WalkerBaseMuJoCoEnv):
+    """mujoco/gym_locomotion_envs.py:121-160: obs [qpos[1:], clip(qvel, -10, 10)] (11),
+    reward x-progress + 1 - 1e-3 sum(a^2), done unless height > -0.3 and |angle| < .2."""
+    env_id = "HopperMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        WalkerBaseMuJoCoEnv.__init__(self, HopperMuJoCo(), render, device)
+
+
+class Walker2DMuJoCoEnv(WalkerBaseMuJoCoEnv):
+    """mujoco/gym_locomotion_envs.py:163-203: obs (17); done unless 1 > height > -0.2 and
+    -1 < angle < 1."""
+    env_id = "Walker2DMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        WalkerBaseMuJoCoEnv.__init__(self, Walker2DMuJoCo(), render, device)
+
+
+class HalfCheetahMuJoCoEnv(WalkerBaseMuJoCoEnv):
+    """mujoco/gym_locomotion_envs.py:206-240: obs [qpos[1:], qvel] (17), reward x-progress
+    - 0.1 sum(a^2), never done."""
+    env_id = "HalfCheetahMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        WalkerBaseMuJoCoEnv.__init__(self, HalfCheetahMuJoCo(), render, device)
+
+
 class InvertedPendulumBulletEnv(BaseBulletEnv):
     """gym_pendulum_envs.py:7-42: obs float64 [x, vx, cos(theta), sin(theta), theta_dot]."""
     env_id = "InvertedPendulumPyBulletEnv-v0"
@@ -340,12 +376,16 @@ ENV_CLASSES = {
     "AntPyBulletEnv-v0": AntBulletEnv,
     "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
     "HumanoidFlagrunPyBulletEnv-v0": HumanoidFlagrunBulletEnv,
+    "HopperMuJoCoEnv-v0": HopperMuJoCoEnv,
+    "Walker2DMuJoCoEnv-v0": Walker2DMuJoCoEnv,
+    "HalfCheetahMuJoCoEnv-v0": HalfCheetahMuJoCoEnv,
 }
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
 REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
                     "InvertedPendulumSwingupPyBulletEnv-v0": 800.0, "InvertedDoublePendulumPyBulletEnv-v0": 9100.0,
-                    "Walker2DPyBulletEnv-v0": 2500.0,
+                    "Walker2DPyBulletEnv-v0": 2500.0, "Walker2DMuJoCoEnv-v0": 2500.0,
+                    "HalfCheetahMuJoCoEnv-v0": 3000.0, "HopperMuJoCoEnv-v0": 2500.0,
                     "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
 
 

@@ -22,6 +22,11 @@ ALIVE_DOUBLE = 6       # gym_pendulum_envs.py:69-80  (reward 10 - dist_penalty, 
 
 KIND_WALKER = 0
 KIND_PENDULUM = 1
+KIND_MUJOCO_PLANAR = 2  # envs/mujoco Hopper / Walker2D / HalfCheetah: qpos/qvel obs, x-progress
+
+ALIVE_MJ_HOPPER = 10    # mujoco/gym_locomotion_envs.py:127-137 (height > -0.3, |ang| < .2)
+ALIVE_MJ_WALKER = 11    # :171-181 (1 > height > -0.2, -1 < ang < 1)
+ALIVE_MJ_CHEETAH = 12   # :214-222 (never done, no alive bonus)
 
 
 @dataclass
@@ -49,6 +54,8 @@ class RobotSpec:
     self_collision: bool = True
     reset_offset: float = 0.0                                    # swingup hinge 3.1415 + u
     flagrun: bool = False                                        # HumanoidFlagrun walk target
+    power_cost: float = 0.0                                      # MuJoCo planar: coef of sum(a^2)
+    qvel_clip: float = 0.0                                       # MuJoCo planar: obs qvel clip (0: none)
 
 
 SPECS: Dict[str, RobotSpec] = OrderedDict()
@@ -113,6 +120,20 @@ _add(RobotSpec("HumanoidFlagrunPyBulletEnv-v0", "humanoid_flagrun", "humanoid_sy
                alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
                power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8,
                electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1, flagrun=True))
+
+# MuJoCo-observation planar walkers (envs/mujoco, add_ignored_joints=True): obs
+# qpos[1:] + qvel of every ordered joint incl. the ignored root joints, reward
+# x-progress (+1 alive) + power cost; robot_locomotors.py (mujoco) :82-196,
+# gym_locomotion_envs.py (mujoco) :121-252, envs/__init__.py:121-146
+_add(RobotSpec("HopperMuJoCoEnv-v0", "hopper_mujoco", "hopper.xml", "torso", action_dim=3, obs_dim=11,
+               kind=KIND_MUJOCO_PLANAR, power=0.75, alive=ALIVE_MJ_HOPPER, power_cost=-1e-3, qvel_clip=10.0))
+_add(RobotSpec("Walker2DMuJoCoEnv-v0", "walker2d_mujoco", "walker2d.xml", "torso", action_dim=6, obs_dim=17,
+               kind=KIND_MUJOCO_PLANAR, power=0.40, alive=ALIVE_MJ_WALKER,
+               power_coef={"foot_joint": 30.0, "foot_left_joint": 30.0}, power_cost=-1e-3, qvel_clip=10.0))
+_add(RobotSpec("HalfCheetahMuJoCoEnv-v0", "halfcheetah_mujoco", "half_cheetah.xml", "torso", action_dim=6,
+               obs_dim=17, kind=KIND_MUJOCO_PLANAR, power=1.0, alive=ALIVE_MJ_CHEETAH,
+               power_coef={"bthigh": 120.0, "bshin": 90.0, "bfoot": 60.0, "fthigh": 140.0,
+                           "fshin": 60.0, "ffoot": 30.0}, power_cost=-0.1, qvel_clip=0.0))
 
 ENV_IDS = {s.env_id: s for s in SPECS.values()}
 

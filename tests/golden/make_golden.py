@@ -47,6 +47,9 @@ ROBOTS = {
     "pendulum_swingup": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedPendulumSwingupBulletEnv"),
     "double_pendulum": ("pybulletgym.envs.roboschool.gym_pendulum_envs", "InvertedDoublePendulumBulletEnv"),
     "humanoid_flagrun": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidFlagrunBulletEnv"),
+    "hopper_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HopperMuJoCoEnv"),
+    "walker2d_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "Walker2DMuJoCoEnv"),
+    "halfcheetah_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HalfCheetahMuJoCoEnv"),
 }
 
 
@@ -295,8 +298,19 @@ def generate(key, episodes=3, steps=40, seed=1234):
     calc_cls = type(robot)
     orig_calc = calc_cls.calc_state
 
+    orig_pot = calc_cls.calc_potential
+
+    def spy_calc_potential(self):  # MuJoCo planar: x-progress of robot_body
+        captured["x_before"] = float(self.pos_after)
+        r = orig_pot(self)
+        captured["x_after"] = float(self.pos_after)
+        return r
+
     def spy_calc_state(self):
-        if t["kind"] == 0:
+        if t["kind"] == 2:  # MuJoCo planar: every ordered joint incl. the ignored root joints
+            captured["jq"] = np.array([j.get_position() for j in self.ordered_joints], dtype=np.float64)
+            captured["jqd"] = np.array([j.get_velocity() for j in self.ordered_joints], dtype=np.float64)
+        elif t["kind"] == 0:
             captured["part_xyz"] = np.array([p.pose().xyz() for p in self.parts.values()], dtype=np.float64)
             captured["part_names"] = list(self.parts.keys())
             captured["body_quat"] = np.array(self.robot_body.pose().orientation(), dtype=np.float64)
@@ -318,6 +332,8 @@ def generate(key, episodes=3, steps=40, seed=1234):
         return orig_calc(self)
 
     calc_cls.calc_state = spy_calc_state
+    if t["kind"] == 2:
+        calc_cls.calc_potential = spy_calc_potential
     NPMAX = t["NP"] + 1
     nf = max(1, t["NF"])
 
@@ -348,15 +364,17 @@ def generate(key, episodes=3, steps=40, seed=1234):
                 rec["flag_out"].append(list(after))
             rec["initial_z_out"].append(float(robot.initial_z))
             part_names.append(captured["part_names"])
+        elif t["kind"] == 2:
+            rec["body_pos"].append(np.array([captured["x_after"], 0.0, 0.0]))
         elif "body_pos" in captured:
             rec["body_pos"].append(captured["body_pos"])
         rec["jq"].append(captured["jq"]); rec["jqd"].append(captured["jqd"])
         rec["act"].append(np.zeros(t["NA"], np.float32) if act is None else act)
-        rec["potential_old"].append(pot_old)
+        rec["potential_old"].append(captured["x_before"] if t["kind"] == 2 else pot_old)
         rec["obs"].append(np.asarray(obs))
         rec["reward"].append(reward)
         rec["done"].append(bool(done))
-        rec["potential"].append(float(getattr(env, "potential", 0.0)))
+        rec["potential"].append(captured["x_after"] if t["kind"] == 2 else float(getattr(env, "potential", 0.0)))
         rw = getattr(env, "rewards", [0.0] * 5)
         rr = np.zeros(5); rr[:len(rw)] = rw
         rec["rewards"].append(rr)
@@ -374,6 +392,7 @@ def generate(key, episodes=3, steps=40, seed=1234):
             obs, r, done, info = env.step(a)
             push(1, a, pot_old, obs, float(r), done)
     calc_cls.calc_state = orig_calc
+    calc_cls.calc_potential = orig_pot
     out = {k: np.array(v) for k, v in rec.items() if len(v)}
     out["part_names"] = np.array(["|".join(p) for p in part_names]) if part_names else np.array([])
     out["numpy_version"] = np.array(np.__version__)

@@ -73,3 +73,25 @@ def test_oracle_pack_pendulum(key):
         if step:
             assert out["done"] == bool(g["done"][i]), f"call {i}"
             assert out["reward"] == g["reward"][i], f"call {i}"
+
+
+MUJOCO_PLANAR = ["hopper_mujoco", "walker2d_mujoco", "halfcheetah_mujoco"]
+
+
+@pytest.mark.parametrize("key", MUJOCO_PLANAR)
+def test_oracle_pack_mujoco_planar(key):
+    """envs/mujoco Hopper / Walker2D / HalfCheetah (add_ignored_joints): obs [qpos[1:],
+    clip(qvel)] float32 bit-exact, reward (x-progress + alive + float32 power cost) and done
+    exact, x_after exact."""
+    g = load(key)
+    for i in range(len(g["kind"])):
+        step = g["kind"][i] == 1
+        out = oracle.pack(key, np.zeros((1, 3)), np.zeros(4), g["body_pos"][i], np.zeros(3), g["jq"][i],
+                          g["jqd"][i], np.zeros(1), np.zeros(1) if step else None, g["act"][i] if step else None,
+                          g["potential_old"][i], 0.0)
+        np.testing.assert_array_equal(out["obs"].view(np.uint32), g["obs"][i].astype(np.float32).view(np.uint32),
+                                      err_msg=f"call {i}")
+        assert out["potential"] == g["potential"][i]
+        if step:
+            assert out["done"] == bool(g["done"][i]), f"call {i}"
+            assert out["reward"] == g["reward"][i] or (np.isnan(out["reward"]) and np.isnan(g["reward"][i])), f"call {i}"

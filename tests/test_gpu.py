@@ -27,7 +27,8 @@ pytestmark = pytest.mark.gpu
 ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
         "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
         "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
-        "HumanoidFlagrunPyBulletEnv-v0"]
+        "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0",
+        "HalfCheetahMuJoCoEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -60,7 +61,7 @@ def test_device_pack_matches_reference_golden(env_id):
             rec[i, o:o + 4] = g["body_quat"][i]
             rec[i, o + 4:o + 7] = g["body_pos"][i]
             rec[i, o + 7:o + 10] = g["body_vel"][i]
-        elif "body_pos" in g.files and g["body_pos"].size:  # double pendulum: pole2 position
+        elif "body_pos" in g.files and g["body_pos"].size:  # double pendulum: pole2; MuJoCo: robot_body
             rec[i, o + 4:o + 7] = g["body_pos"][i]
         o += 10
         rec[i, o:o + info.NO] = g["jq"][i]
@@ -84,6 +85,8 @@ def test_device_pack_matches_reference_golden(env_id):
     step = g["kind"] == 1
     np.testing.assert_array_equal(out[step, info.OBS + 1].astype(bool), g["done"][step])
     np.testing.assert_allclose(out[step, info.OBS], g["reward"][step], atol=1e-9, rtol=0)
+    if info.kind == 2:  # MuJoCo planar: x_after
+        np.testing.assert_array_equal(out[:, info.OBS + 2], g["potential"])
     if info.kind == 0:
         np.testing.assert_allclose(out[:, info.OBS + 2], g["potential"], atol=1e-9, rtol=0)
         np.testing.assert_array_equal(out[:, info.OBS + 3], g["initial_z_out"])
