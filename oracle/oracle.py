@@ -15,14 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
-             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11}
+             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13}
 ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
             "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
             "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d",
             "InvertedPendulumSwingupPyBulletEnv-v0": "pendulum_swingup",
             "InvertedDoublePendulumPyBulletEnv-v0": "double_pendulum",
             "HumanoidFlagrunPyBulletEnv-v0": "humanoid_flagrun", "HopperMuJoCoEnv-v0": "hopper_mujoco",
-            "Walker2DMuJoCoEnv-v0": "walker2d_mujoco", "HalfCheetahMuJoCoEnv-v0": "halfcheetah_mujoco"}
+            "Walker2DMuJoCoEnv-v0": "walker2d_mujoco", "HalfCheetahMuJoCoEnv-v0": "halfcheetah_mujoco",
+            "AntMuJoCoEnv-v0": "ant_mujoco", "HumanoidMuJoCoEnv-v0": "humanoid_mujoco"}
 
 _lib = None
 
@@ -122,17 +123,19 @@ class _PackIn(ctypes.Structure):
                 ("body_vel", ctypes.c_void_p), ("jq", ctypes.c_void_p), ("jqd", ctypes.c_void_p),
                 ("feet_prev", ctypes.c_void_p), ("feet_new", ctypes.c_void_p), ("act", ctypes.c_void_p),
                 ("potential_old", ctypes.c_double), ("initial_z", ctypes.c_double),
-                ("target_x", ctypes.c_double), ("target_y", ctypes.c_double)]
+                ("target_x", ctypes.c_double), ("target_y", ctypes.c_double),
+                ("body_avel", ctypes.c_void_p)]
 
 
 class _PackOut(ctypes.Structure):
     _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_double), ("done", ctypes.c_uint8),
                 ("potential", ctypes.c_double), ("initial_z", ctypes.c_double),
-                ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5), ("dist", ctypes.c_double)]
+                ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5), ("dist", ctypes.c_double),
+                ("pitch", ctypes.c_double), ("at_limit", ctypes.c_int)]
 
 
 def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet_new, act,
-         potential_old, initial_z, flag=None):
+         potential_old, initial_z, flag=None, body_avel=None):
     """Run the oracle's pack on explicit inputs (golden-vector tests).  flag (HumanoidFlagrun):
     [target x, y, flag_timeout, next draw x, y]; the result then carries flag_out."""
     rid = robot_id(name)
@@ -147,7 +150,10 @@ def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet
     ac = None if act is None else np.ascontiguousarray(act, dtype=np.float32)
     pin = _PackIn(_p(arrs["part_xyz"]), len(arrs["part_xyz"]), _p(arrs["body_quat"]), _p(arrs["body_pos"]),
                   _p(arrs["body_vel"]), _p(arrs["jq"]), _p(arrs["jqd"]), _p(arrs["feet_prev"]), _p(fn),
-                  _p(ac), float(potential_old), float(initial_z), 1e3, 0.0)
+                  _p(ac), float(potential_old), float(initial_z), 1e3, 0.0, None)
+    if body_avel is not None:
+        arrs["body_avel"] = np.ascontiguousarray(body_avel, dtype=np.float64)
+        pin.body_avel = _p(arrs["body_avel"])
     obs = np.zeros(info.OBS, dtype=np.float32)
     feet_out = np.zeros(max(1, info.NF), dtype=np.float32)
     pout = _PackOut()

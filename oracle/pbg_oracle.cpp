@@ -91,13 +91,14 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[12] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[14] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                          view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                          view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
                          view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
                          view<pbg_models::HumanoidFlagrun>(), view<pbg_models::HopperMuJoCo>(),
-                         view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>()};
-  if (robot < 0 || robot > 11) return nullptr;
+                         view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>(),
+                         view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>()};
+  if (robot < 0 || robot > 13) return nullptr;
   return &views[robot];
 }
 
@@ -659,6 +660,7 @@ typedef struct {
   double potential_old;
   double initial_z;          // NaN: take it from this calc_state (robot_locomotors.py:44-45)
   double target_x, target_y; // robot.walk_target_x / _y (1e3, 0 except HumanoidFlagrun)
+  const double* body_avel;   // base angular velocity (MuJoCo-observation Ant / Humanoid; nullable)
 } pbg_pack_in;
 
 typedef struct {
@@ -666,6 +668,8 @@ typedef struct {
   float* feet_out;           // [NF]
   double rewards[5];         // alive, progress, electricity, joints_at_limit, feet_collision
   double dist;               // walk_target_dist
+  double pitch;              // body_rpy[1]
+  int at_limit;              // joints_at_limit
 } pbg_pack_out;
 
 void pbg_oracle_set_flags(int flags) { g_flags = flags; }
@@ -711,14 +715,24 @@ static void pendulum_obs(const MV& m, const double* jq, const double* jqd, const
                          double* rew, uint8_t* done);
 static void mujoco_planar_obs(const MV& m, const double* jq, const double* jqd, double x_after, double x_before,
                               const float* act, pbg_pack_out* out);
+static void mujoco3d_obs(const MV& m, const pbg_pack_in* in, pbg_pack_out* out);
 
 // Walker pack: calc_state (robot_locomotors.py:31-64) + the reward/done part of
 // WalkerBaseBulletEnv._step (gym_locomotion_envs.py:59-114).  With act == NULL only the
 // calc_state half runs (reset path).
+static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* out);
+
 int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
+  if (m.kind == 3) {  // MuJoCo Ant / Humanoid: WalkerBase.calc_state side effects, then qpos/qvel obs
+    pbg_pack_in w = *in;
+    w.act = nullptr;
+    walker_pack_body(m, &w, out);
+    mujoco3d_obs(m, in, out);
+    return 0;
+  }
   if (m.kind == 2) {  // MuJoCo planar: jq/jqd all ordered joints, body_pos = robot_body, potential_old = x_before
     mujoco_planar_obs(m, in->jq, in->jqd, in->body_pos[0], in->potential_old, in->act, out);
     return 0;
@@ -728,6 +742,10 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
     if (!in->act) { out->reward = 0; out->done = 0; }
     return 0;
   }
+  return walker_pack_body(m, in, out);
+}
+
+static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* out) {
   // joints: np.array([...], dtype=float32) of (pos_rel, vel_scaled) pairs  (robot_bases.py:306-321)
   float j[2 * MAXD];
   for (int i = 0; i < m.NO; i++) {
@@ -765,6 +783,8 @@ int pbg_oracle_pack(int robot, const pbg_pack_in* in, pbg_pack_out* out) {
   for (int i = 0; i < 2 * m.NO; i++) out->obs[o++] = clip5(j[i]);
   for (int i = 0; i < m.NF; i++) out->obs[o++] = clip5(in->feet_prev[i]);
   out->initial_z = z0;
+  out->pitch = rpy[1];
+  out->at_limit = at_limit;
   double dt = m.dt_sub * m.substeps;  // scene.dt = timestep*frame_skip (scene_bases.py:17)
   out->potential = -dist / dt;         // robot_locomotors.py:79
   for (int i = 0; i < m.NF; i++) out->feet_out[i] = in->feet_prev[i];
@@ -894,6 +914,33 @@ static void mujoco_planar_obs(const MV& m, const double* jq, const double* jqd, 
   }
 }
 
+// MuJoCo-observation Ant / Humanoid (mujoco robot_locomotors.py:210-319, mujoco
+// gym_locomotion_envs.py:53-114): obs [z, quat, joint q, v, w, joint qd, zeros] (float64 in
+// the reference), reward sum([alive(state[0] + initial_z), progress, -0.1 at_limit, 0]).
+static void mujoco3d_obs(const MV& m, const pbg_pack_in* in, pbg_pack_out* out) {
+  double st[5 + 2 * MAXD + 6];
+  int o = 0;
+  st[o++] = in->body_pos[2];
+  for (int i = 0; i < 4; i++) st[o++] = in->body_quat[i];
+  for (int i = 0; i < m.NO; i++) st[o++] = in->jq[i];
+  for (int i = 0; i < 3; i++) st[o++] = in->body_vel[i];
+  for (int i = 0; i < 3; i++) st[o++] = in->body_avel ? in->body_avel[i] : 0.0;
+  for (int i = 0; i < m.NO; i++) st[o++] = in->jqd[i];
+  bool finite = true;
+  for (int i = 0; i < o; i++) { out->obs[i] = (float)st[i]; finite = finite && isfinite(st[i]); }
+  for (int i = o; i < m.OBS; i++) out->obs[i] = 0.f;
+  for (int i = 0; i < m.NF; i++) out->feet_out[i] = in->feet_new ? (in->feet_new[i] ? 1.f : 0.f) : in->feet_prev[i];
+  for (int i = 0; i < 5; i++) out->rewards[i] = 0.0;
+  if (!in->act) { out->reward = 0.0; out->done = 0; return; }
+  const double z = st[0] + out->initial_z;
+  const double alive = m.alive == 2 ? (z > 0.26 ? 1.0 : -1.0) : (z > 0.78 ? 2.0 : -1.0);
+  out->done = alive < 0 || !finite;
+  const double progress = out->potential - in->potential_old;
+  const double jal = -0.1 * (double)out->at_limit;
+  out->rewards[0] = alive; out->rewards[1] = progress; out->rewards[2] = jal;  // [alive, progress, jal, 0]
+  out->reward = (((0.0 + alive) + progress) + jal) + 0.0;
+}
+
 // Pendulum packs: calc_state + reward/done.  obs is float64 in the reference; written here
 // as float32 (the C-ABI's obs dtype).
 //  * InvertedPendulum / Swingup (robot_pendula.py:27-51, gym_pendulum_envs.py:26-39): non-finite
@@ -1005,7 +1052,7 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
     gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd);
     float feet_prev[8] = {0}, feet_out[8];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, nullptr, nullptr, 0.0,
-                      m.z0fixed, PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y};
+                      m.z0fixed, PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);
@@ -1059,7 +1106,7 @@ int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* a
     float feet_prev[8], feet_out[8];
     for (int f = 0; f < m.NF; f++) feet_prev[f] = (float)a[4 + f];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, feet_new, ac,
-                      a[0], a[1], PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y};
+                      a[0], a[1], PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);

@@ -283,12 +283,12 @@ def emit_struct(t: Dict) -> str:
 
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
-             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11}
+             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
            "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun",
            "hopper_mujoco": "HopperMuJoCo", "walker2d_mujoco": "Walker2DMuJoCo",
-           "halfcheetah_mujoco": "HalfCheetahMuJoCo"}
+           "halfcheetah_mujoco": "HalfCheetahMuJoCo", "ant_mujoco": "AntMuJoCo", "humanoid_mujoco": "HumanoidMuJoCo"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

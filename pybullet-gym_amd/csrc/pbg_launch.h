@@ -43,4 +43,6 @@ PBG_DECLARE_ROBOT(HumanoidFlagrun)
 PBG_DECLARE_ROBOT(HopperMuJoCo)
 PBG_DECLARE_ROBOT(Walker2DMuJoCo)
 PBG_DECLARE_ROBOT(HalfCheetahMuJoCo)
+PBG_DECLARE_ROBOT(AntMuJoCo)
+PBG_DECLARE_ROBOT(HumanoidMuJoCo)
 }  // namespace pbg

@@ -8,10 +8,12 @@ namespace pbg {
 // feet_prev NF | feet_new NF | act NA | potential_old | initial_z_in | is_step]; the output
 // record: [obs OBS | reward | done | potential | initial_z | feet_out NF].
 // HumanoidFlagrun appends to the input [target x, y | flag_timeout | next target x, y] (the
-// draw a reposition would take) and to the output [target x, y | flag_timeout].
+// draw a reposition would take) and to the output [target x, y | flag_timeout].  The
+// MuJoCo-observation Ant / Humanoid append the base angular velocity (3) to the input.
 template <class R>
 struct PackRec {
-  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3 + (R::flagrun ? 5 : 0);
+  static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3 + (R::flagrun ? 5 : 0) +
+                            (R::kind == 3 ? 3 : 0);
   static constexpr int OUT = R::OBS + 4 + R::NF + (R::flagrun ? 3 : 0);
 };
 template <class R>

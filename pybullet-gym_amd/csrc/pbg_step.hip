@@ -1002,9 +1002,12 @@ struct PackIn {
   uint32_t feet_new;  // bitmask
   double potential_old, initial_z;  // initial_z NaN: take from this calc_state
   double target_x = PBG_WALK_TARGET_X, target_y = PBG_WALK_TARGET_Y;  // robot.walk_target_x/y
+  double avel[3] = {0.0, 0.0, 0.0};  // base angular velocity (MuJoCo-observation walkers)
 };
 struct PackOut {
   double reward, potential, initial_z, dist;  // dist: walk_target_dist
+  double pitch;                               // body_rpy[1]
+  int at_limit;                               // joints_at_limit
   uint32_t feet_out;  // bitmask
   bool done;
 };
@@ -1068,6 +1071,8 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   for (int i = 0; i < R::NF; i++) { obs[o] = clip5(in.feet_prev[i]); o++; }
   out.initial_z = z0;
   out.dist = dist;
+  out.pitch = pitch;
+  out.at_limit = at_limit;
   out.potential = -dist / (R::dt_sub * R::substeps);  // robot_locomotors.py:79; scene_bases.py:17
   uint32_t fb = 0;
 #pragma unroll
@@ -1206,6 +1211,45 @@ PBG_DEV void mujoco_planar_pack_state(const State<R>& s, double x_before, const 
   mujoco_planar_pack<R>(jq, jqd, (double)k.c[R::robot_body + 1].x, x_before, act, obs, po);
 }
 
+// MuJoCo-observation Ant / Humanoid (mujoco robot_locomotors.py:210-319): WalkerBase.calc_state
+// runs for its side effects (joints_at_limit, body_xyz / rpy, initial_z, walk_target_dist),
+// then obs = [qpos[2:] = (z, quat x y z w, joint q), qvel = (v, w, joint qd), zeros] (float64
+// in the reference, float32 through the C-ABI).  _step (mujoco gym_locomotion_envs.py:53-114):
+// alive = alive_bonus(state[0] + initial_z), done = alive < 0 or a non-finite state,
+// reward = sum([alive, progress, -0.1 joints_at_limit, 0]) -- no electricity term.
+template <class R, bool GEN = false>
+PBG_DEV void mujoco3d_pack(const PackIn<R>& in, const float* act, float* obs, PackOut& out) {
+  walker_pack<R, GEN>(in, nullptr, obs, out);  // calc_state side effects (obs overwritten below)
+  double st[5 + 2 * R::NO + 6];
+  int o = 0;
+  st[o++] = in.pos[2];
+#pragma unroll
+  for (int i = 0; i < 4; i++) st[o++] = in.quat[i];
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) st[o++] = in.jq[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) st[o++] = in.vel[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) st[o++] = in.avel[i];
+#pragma unroll
+  for (int i = 0; i < R::NO; i++) st[o++] = in.jqd[i];
+  bool finite = true;
+#pragma unroll
+  for (int i = 0; i < o; i++) { obs[i] = (float)st[i]; finite &= isfinite(st[i]); }
+#pragma unroll
+  for (int i = o; i < R::OBS; i++) obs[i] = 0.f;  // cfrc_ext / cinert / cvel / qfrc_actuator: zeros
+  if (!act) { out.reward = 0.0; out.done = false; return; }  // reset: feet_contact stays as packed
+  out.feet_out = in.feet_new;
+  const double z = st[0] + out.initial_z;
+  double alive;
+  if constexpr (R::alive == 2) alive = z > 0.26 ? 1.0 : -1.0;  // Ant :307-308
+  else alive = z > 0.78 ? 2.0 : -1.0;                         // Humanoid :318-319
+  out.done = alive < 0 || !finite;
+  const double progress = out.potential - in.potential_old;
+  const double jal = -0.1 * (double)out.at_limit;
+  out.reward = (((0.0 + alive) + progress) + jal) + 0.0;
+}
+
 // Pendulum packs (obs float64 in the reference, float32 through the C-ABI).
 //  InvertedPendulum / Swingup: robot_pendula.py:27-51 + gym_pendulum_envs.py:26-39 --
 //  non-finite vx / theta / theta_dot replaced by 0; balance: reward 1, done |theta| > .2;
@@ -1315,6 +1359,7 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
     vel = v[b];
   }
   in.vel[0] = vel.x; in.vel[1] = vel.y; in.vel[2] = vel.z;
+  if constexpr (R::floating) { in.avel[0] = s.bw[0]; in.avel[1] = s.bw[1]; in.avel[2] = s.bw[2]; }
 #pragma unroll
   for (int i = 0; i < R::NO; i++) { in.jq[i] = s.q[R::obs_dof[i]]; in.jqd[i] = s.qd[R::obs_dof[i]]; }
 }
@@ -1378,7 +1423,8 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
   in.initial_z = R::initial_z_fixed;
   auto draw = [&](Flag& f) { flag_draw(B, e, f); };
   if constexpr (R::flagrun) draw(fl);  // robot_specific_reset -> flag_reposition (:199-201)
-  flag_pack<R>(in, nullptr, obs, po, fl, draw);
+  if constexpr (R::kind == 3) mujoco3d_pack<R>(in, nullptr, obs, po);
+  else flag_pack<R>(in, nullptr, obs, po, fl, draw);
   pot = po.potential;
   z0 = (float)po.initial_z;
   has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
@@ -1472,7 +1518,8 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
     Flag fl = load_flag<R>(B, e);
-    flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
+    if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
+    else flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
     store_flag<R>(B, e, fl);
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
@@ -1550,7 +1597,12 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
     in.feet_new = fn;
     in.potential_old = r[o_pot];
     in.initial_z = r[o_pot + 1];
-    if constexpr (R::flagrun) {
+    if constexpr (R::kind == 3) {
+#pragma unroll
+      for (int i = 0; i < 3; i++) in.avel[i] = r[o_pot + 3 + i];  // base angular velocity
+      if (in.n_parts == R::NP || in.n_parts == R::NP + 1) mujoco3d_pack<R>(in, is_step ? act : nullptr, obs, po);
+      else mujoco3d_pack<R, true>(in, is_step ? act : nullptr, obs, po);
+    } else if constexpr (R::flagrun) {
       // [target x, y | flag_timeout | next target x, y]: the reposition takes the recorded draw
       const int o_f = o_pot + 3;
       Flag f = {r[o_f], r[o_f + 1], (int)r[o_f + 2], 0};

@@ -84,7 +84,7 @@ struct Team {
   static constexpr int NC = R::NS;      // contact capacity
   static constexpr int W = NDB + 9;     // contact row: y_b | y_base(6) | meff | target | lambda
   static constexpr int check() {
-    if (!R::floating || R::kind != 0 || R::NPAIR != 0 || R::robot_body != -1 || B != 4) return false;
+    if (!R::floating || (R::kind != 0 && R::kind != 3) || R::NPAIR != 0 || R::robot_body != -1 || B != 4) return false;
     if (NL % B || NJ % B || (R::NS - NS0) % B || NDB < 1 || NDB > 8) return false;
     for (int s = 0; s < NS0; s++)
       if (R::slot_link[s] != -1) return false;
@@ -1050,7 +1050,7 @@ PBG_DEV void team_gather(const TState<R>& s, const Lane& L, const TRows<R, ES>& 
 #pragma unroll
   for (int i = 0; i < 4; i++) in.quat[i] = s.bq[i];
 #pragma unroll
-  for (int i = 0; i < 3; i++) { in.pos[i] = s.bp[i]; in.vel[i] = s.bv[i]; }
+  for (int i = 0; i < 3; i++) { in.pos[i] = s.bp[i]; in.vel[i] = s.bv[i]; in.avel[i] = s.bw[i]; }
 #pragma unroll
   for (int i = 0; i < R::NO; i++) {
     in.jq[i] = rw.stage(2 * NL + R::obs_dof[i]);
@@ -1098,7 +1098,8 @@ PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, co
   in.potential_old = 0.0;
   in.initial_z = R::initial_z_fixed;
   PackOut po;
-  walker_pack<R>(in, nullptr, obs, po);
+  if constexpr (R::kind == 3) mujoco3d_pack<R>(in, nullptr, obs, po);
+  else walker_pack<R>(in, nullptr, obs, po);
   pot = po.potential;
   z0 = (float)po.initial_z;
   has_floor = true;
@@ -1174,7 +1175,8 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     in.feet_new = fnew;
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
-    walker_pack<R>(in, act, obs, po);
+    if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
+    else walker_pack<R>(in, act, obs, po);
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
   STAMP(8)

@@ -86,7 +86,7 @@ class WalkerBase(XmlBasedRobot):
 def _robot_class(key, base_cls):
     spec = _robots.spec_for(key)
 
-    walker = spec.kind in (_robots.KIND_WALKER, _robots.KIND_MUJOCO_PLANAR)
+    walker = spec.kind in (_robots.KIND_WALKER, _robots.KIND_MUJOCO_PLANAR, _robots.KIND_MUJOCO_3D)
     bases = (WalkerBase, MJCFBasedRobot) if walker else (MJCFBasedRobot,)
 
     class _R(*bases):
@@ -112,6 +112,8 @@ HumanoidFlagrun = _robot_class("humanoid_flagrun", "HumanoidFlagrun")  # :195-22
 HopperMuJoCo = _robot_class("hopper_mujoco", "Hopper")                # mujoco/robot_locomotors.py:82-121
 Walker2DMuJoCo = _robot_class("walker2d_mujoco", "Walker2D")          # :124-164
 HalfCheetahMuJoCo = _robot_class("halfcheetah_mujoco", "HalfCheetah")  # :167-207
+AntMuJoCo = _robot_class("ant_mujoco", "Ant")                          # :210-239
+HumanoidMuJoCo = _robot_class("humanoid_mujoco", "Humanoid")           # :242-319
 InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
 InvertedPendulumSwingup = _robot_class("pendulum_swingup", "InvertedPendulumSwingup")  # robot_pendula.py:54-55
 InvertedDoublePendulum = _robot_class("double_pendulum", "InvertedDoublePendulum")      # robot_pendula.py:58-88
@@ -319,6 +321,30 @@ class HalfCheetahMuJoCoEnv(WalkerBaseMuJoCoEnv):
         WalkerBaseMuJoCoEnv.__init__(self, HalfCheetahMuJoCo(), render, device)
 
 
+class AntMuJoCoEnv(WalkerBaseMuJoCoEnv):
+    """mujoco/gym_locomotion_envs.py:243-246: obs float64 [qpos[2:], qvel, cfrc_ext zeros] (111),
+    reward alive(state[0] + initial_z) + progress - 0.1 joints_at_limit."""
+    env_id = "AntMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        WalkerBaseMuJoCoEnv.__init__(self, AntMuJoCo(), render, device)
+
+    def _obs_out(self, obs):
+        return obs[0].cpu().numpy().astype(np.float64)
+
+
+class HumanoidMuJoCoEnv(WalkerBaseMuJoCoEnv):
+    """mujoco/gym_locomotion_envs.py:249-255: obs float64 [qpos[2:], qvel, cinert, cvel,
+    qfrc_actuator, cfrc_ext] (376; the last four are zeros in the reference)."""
+    env_id = "HumanoidMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        WalkerBaseMuJoCoEnv.__init__(self, HumanoidMuJoCo(), render, device)
+
+    def _obs_out(self, obs):
+        return obs[0].cpu().numpy().astype(np.float64)
+
+
 class InvertedPendulumBulletEnv(BaseBulletEnv):
     """gym_pendulum_envs.py:7-42: obs float64 [x, vx, cos(theta), sin(theta), theta_dot]."""
     env_id = "InvertedPendulumPyBulletEnv-v0"
@@ -379,13 +405,15 @@ ENV_CLASSES = {
     "HopperMuJoCoEnv-v0": HopperMuJoCoEnv,
     "Walker2DMuJoCoEnv-v0": Walker2DMuJoCoEnv,
     "HalfCheetahMuJoCoEnv-v0": HalfCheetahMuJoCoEnv,
+    "AntMuJoCoEnv-v0": AntMuJoCoEnv,
+    "HumanoidMuJoCoEnv-v0": HumanoidMuJoCoEnv,
 }
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
 REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
                     "InvertedPendulumSwingupPyBulletEnv-v0": 800.0, "InvertedDoublePendulumPyBulletEnv-v0": 9100.0,
                     "Walker2DPyBulletEnv-v0": 2500.0, "Walker2DMuJoCoEnv-v0": 2500.0,
-                    "HalfCheetahMuJoCoEnv-v0": 3000.0, "HopperMuJoCoEnv-v0": 2500.0,
+                    "HalfCheetahMuJoCoEnv-v0": 3000.0, "HopperMuJoCoEnv-v0": 2500.0, "AntMuJoCoEnv-v0": 2500.0,
                     "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
 
 

@@ -23,6 +23,7 @@ ALIVE_DOUBLE = 6       # gym_pendulum_envs.py:69-80  (reward 10 - dist_penalty, 
 KIND_WALKER = 0
 KIND_PENDULUM = 1
 KIND_MUJOCO_PLANAR = 2  # envs/mujoco Hopper / Walker2D / HalfCheetah: qpos/qvel obs, x-progress
+KIND_MUJOCO_3D = 3      # envs/mujoco Ant / Humanoid: qpos[2:]/qvel (+ zero padding) obs, walker reward
 
 ALIVE_MJ_HOPPER = 10    # mujoco/gym_locomotion_envs.py:127-137 (height > -0.3, |ang| < .2)
 ALIVE_MJ_WALKER = 11    # :171-181 (1 > height > -0.2, -1 < ang < 1)
@@ -134,6 +135,18 @@ _add(RobotSpec("HalfCheetahMuJoCoEnv-v0", "halfcheetah_mujoco", "half_cheetah.xm
                obs_dim=17, kind=KIND_MUJOCO_PLANAR, power=1.0, alive=ALIVE_MJ_CHEETAH,
                power_coef={"bthigh": 120.0, "bshin": 90.0, "bfoot": 60.0, "fthigh": 140.0,
                            "fshin": 60.0, "ffoot": 30.0}, power_cost=-0.1, qvel_clip=0.0))
+
+# MuJoCo-observation floating-base walkers: obs [qpos[2:], qvel, zeros] (float64 in the
+# reference), reward alive(state[0] + initial_z) + progress + joints_at_limit (no electricity);
+# mujoco robot_locomotors.py:210-319, gym_locomotion_envs.py:39-118,243-260, envs/__init__.py:134-152
+_add(RobotSpec("AntMuJoCoEnv-v0", "ant_mujoco", "ant.xml", "torso", action_dim=8, obs_dim=111,
+               kind=KIND_MUJOCO_3D, power=2.5,
+               foot_list=["front_left_foot", "front_right_foot", "left_back_foot", "right_back_foot"],
+               alive=ALIVE_ANT))
+_add(RobotSpec("HumanoidMuJoCoEnv-v0", "humanoid_mujoco", "humanoid_symmetric.xml", "torso", action_dim=17,
+               obs_dim=376, kind=KIND_MUJOCO_3D, power=0.41, foot_list=["right_foot", "left_foot"],
+               alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
+               power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8))
 
 ENV_IDS = {s.env_id: s for s in SPECS.values()}
 

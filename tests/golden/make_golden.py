@@ -50,6 +50,8 @@ ROBOTS = {
     "hopper_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HopperMuJoCoEnv"),
     "walker2d_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "Walker2DMuJoCoEnv"),
     "halfcheetah_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HalfCheetahMuJoCoEnv"),
+    "ant_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "AntMuJoCoEnv"),
+    "humanoid_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HumanoidMuJoCoEnv"),
 }
 
 
@@ -292,7 +294,8 @@ def generate(key, episodes=3, steps=40, seed=1234):
         fake.target_hook = lambda: (robot.walk_target_x, robot.walk_target_y)
     rec = {k: [] for k in ("kind", "part_xyz", "n_parts", "body_quat", "body_pos", "body_vel", "jq", "jqd",
                            "feet_prev", "feet_new", "act", "potential_old", "initial_z_in", "obs", "reward",
-                           "done", "potential", "feet_out", "initial_z_out", "rewards", "flag_in", "flag_out")}
+                           "done", "potential", "feet_out", "initial_z_out", "rewards", "flag_in", "flag_out",
+                           "body_avel")}
     part_names = []
     captured = {}
     calc_cls = type(robot)
@@ -310,7 +313,9 @@ def generate(key, episodes=3, steps=40, seed=1234):
         if t["kind"] == 2:  # MuJoCo planar: every ordered joint incl. the ignored root joints
             captured["jq"] = np.array([j.get_position() for j in self.ordered_joints], dtype=np.float64)
             captured["jqd"] = np.array([j.get_velocity() for j in self.ordered_joints], dtype=np.float64)
-        elif t["kind"] == 0:
+        elif t["kind"] in (0, 3):
+            if t["kind"] == 3:  # MuJoCo Ant / Humanoid also read the torso's angular velocity
+                captured["body_avel"] = np.array(self.parts["torso"].get_velocity()[1], dtype=np.float64)
             captured["part_xyz"] = np.array([p.pose().xyz() for p in self.parts.values()], dtype=np.float64)
             captured["part_names"] = list(self.parts.keys())
             captured["body_quat"] = np.array(self.robot_body.pose().orientation(), dtype=np.float64)
@@ -339,7 +344,9 @@ def generate(key, episodes=3, steps=40, seed=1234):
 
     def push(kind, act, pot_old, obs, reward, done):
         rec["kind"].append(kind)
-        if t["kind"] == 0:
+        if t["kind"] == 3:
+            rec["body_avel"].append(captured["body_avel"])
+        if t["kind"] in (0, 3):
             px = np.zeros((NPMAX, 3))
             n = len(captured["part_xyz"])
             px[:n] = captured["part_xyz"]

@@ -8,7 +8,8 @@ import pytest
 import oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d", "humanoid_flagrun"]
+WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d", "humanoid_flagrun", "ant_mujoco",
+           "humanoid_mujoco"]
 
 
 def load(key):
@@ -37,7 +38,8 @@ def test_oracle_pack_bit_exact(key):
                           g["body_vel"][i], g["jq"][i], g["jqd"][i], g["feet_prev"][i],
                           g["feet_new"][i] if step else None, g["act"][i] if step else None,
                           g["potential_old"][i], g["initial_z_in"][i],
-                          flag=g["flag_in"][i] if "flag_in" in g.files else None)
+                          flag=g["flag_in"][i] if "flag_in" in g.files else None,
+                          body_avel=g["body_avel"][i] if "body_avel" in g.files else None)
         ref_obs = g["obs"][i].astype(np.float32)
         if "flag_out" in g.files:  # HumanoidFlagrun: target and flag_timeout after calc_state
             np.testing.assert_array_equal(out["flag_out"], g["flag_out"][i], err_msg=f"call {i}")

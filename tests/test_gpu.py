@@ -28,7 +28,7 @@ ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPy
         "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
         "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
         "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0",
-        "HalfCheetahMuJoCoEnv-v0"]
+        "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -51,13 +51,13 @@ def test_device_pack_matches_reference_golden(env_id):
     NP1 = info.NP + 1
     for i in range(n):
         o = 0
-        if info.kind == 0:
+        if info.kind in (0, 3):
             px = np.zeros((NP1, 3))
             px[: g["n_parts"][i]] = g["part_xyz"][i][: g["n_parts"][i]]
             rec[i, : 3 * NP1] = px.ravel()
             rec[i, 3 * NP1] = g["n_parts"][i]
         o = 3 * NP1 + 1
-        if info.kind == 0:
+        if info.kind in (0, 3):
             rec[i, o:o + 4] = g["body_quat"][i]
             rec[i, o + 4:o + 7] = g["body_pos"][i]
             rec[i, o + 7:o + 10] = g["body_vel"][i]
@@ -67,17 +67,19 @@ def test_device_pack_matches_reference_golden(env_id):
         rec[i, o:o + info.NO] = g["jq"][i]
         rec[i, o + info.NO:o + 2 * info.NO] = g["jqd"][i]
         o += 2 * info.NO
-        if info.kind == 0:
+        if info.kind in (0, 3):
             rec[i, o:o + info.NF] = g["feet_prev"][i][: info.NF]
             rec[i, o + info.NF:o + 2 * info.NF] = g["feet_new"][i][: info.NF]
         o += 2 * info.NF
         rec[i, o:o + info.NA] = g["act"][i]
         o += info.NA
         rec[i, o] = g["potential_old"][i]
-        rec[i, o + 1] = g["initial_z_in"][i] if info.kind == 0 else 0.0
+        rec[i, o + 1] = g["initial_z_in"][i] if info.kind in (0, 3) else 0.0
         rec[i, o + 2] = float(g["kind"][i] == 1)
         if "flag_in" in g.files:  # HumanoidFlagrun: target, flag_timeout, the recorded re-draw
             rec[i, o + 3:o + 8] = g["flag_in"][i]
+        if "body_avel" in g.files:  # MuJoCo Ant / Humanoid: torso angular velocity
+            rec[i, o + 3:o + 6] = g["body_avel"][i]
     out = pack(env_id, torch.from_numpy(rec).cuda()).cpu().numpy()
     obs = out[:, : info.OBS].astype(np.float32)
     ref = g["obs"].astype(np.float32)
@@ -87,7 +89,7 @@ def test_device_pack_matches_reference_golden(env_id):
     np.testing.assert_allclose(out[step, info.OBS], g["reward"][step], atol=1e-9, rtol=0)
     if info.kind == 2:  # MuJoCo planar: x_after
         np.testing.assert_array_equal(out[:, info.OBS + 2], g["potential"])
-    if info.kind == 0:
+    if info.kind in (0, 3):
         np.testing.assert_allclose(out[:, info.OBS + 2], g["potential"], atol=1e-9, rtol=0)
         np.testing.assert_array_equal(out[:, info.OBS + 3], g["initial_z_out"])
         np.testing.assert_array_equal(out[:, info.OBS + 4:info.OBS + 4 + info.NF], g["feet_out"][:, : info.NF])
@@ -235,7 +237,8 @@ def test_sanity_check_every_env(env_id):
     assert obs.shape == env.observation_space.shape
     obs, r, done, info = env.step(np.random.random(env.action_space.shape))
     assert isinstance(r, float) and isinstance(done, bool) and isinstance(info, dict)
-    assert obs.dtype == (np.float64 if "Pendulum" in env_id else np.float32)
+    f64 = "Pendulum" in env_id or env_id in ("AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0")  # float64 in the reference
+    assert obs.dtype == (np.float64 if f64 else np.float32)
     env.close()
 
 

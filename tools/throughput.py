@@ -9,7 +9,7 @@ cfg = [("InvertedPendulumPyBulletEnv-v0", 16384), ("HopperPyBulletEnv-v0", 4096)
        ("AntPyBulletEnv-v0", 16384), ("HumanoidPyBulletEnv-v0", 4096), ("Walker2DPyBulletEnv-v0", 4096),
        ("InvertedPendulumSwingupPyBulletEnv-v0", 16384), ("InvertedDoublePendulumPyBulletEnv-v0", 16384),
        ("HumanoidFlagrunPyBulletEnv-v0", 4096), ("HopperMuJoCoEnv-v0", 4096), ("Walker2DMuJoCoEnv-v0", 4096),
-       ("HalfCheetahMuJoCoEnv-v0", 8192)]
+       ("HalfCheetahMuJoCoEnv-v0", 8192), ("AntMuJoCoEnv-v0", 16384), ("HumanoidMuJoCoEnv-v0", 4096)]
 if len(sys.argv) > 1:
     cfg = [(a, int(b)) for a, b in (x.split(":") for x in sys.argv[1:])]
 for env_id, n in cfg:
