@@ -15,7 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
-             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13}
+             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
+             "double_pendulum_mujoco": 14}
 ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
             "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
             "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d",
@@ -23,7 +24,8 @@ ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0"
             "InvertedDoublePendulumPyBulletEnv-v0": "double_pendulum",
             "HumanoidFlagrunPyBulletEnv-v0": "humanoid_flagrun", "HopperMuJoCoEnv-v0": "hopper_mujoco",
             "Walker2DMuJoCoEnv-v0": "walker2d_mujoco", "HalfCheetahMuJoCoEnv-v0": "halfcheetah_mujoco",
-            "AntMuJoCoEnv-v0": "ant_mujoco", "HumanoidMuJoCoEnv-v0": "humanoid_mujoco"}
+            "AntMuJoCoEnv-v0": "ant_mujoco", "HumanoidMuJoCoEnv-v0": "humanoid_mujoco",
+            "InvertedDoublePendulumMuJoCoEnv-v0": "double_pendulum_mujoco"}
 
 _lib = None
 

@@ -91,14 +91,15 @@ MV view() {
 }
 
 const MV* model(int robot) {
-  static MV views[14] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[15] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                          view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                          view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
                          view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
                          view<pbg_models::HumanoidFlagrun>(), view<pbg_models::HopperMuJoCo>(),
                          view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>(),
-                         view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>()};
-  if (robot < 0 || robot > 13) return nullptr;
+                         view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>(),
+                         view<pbg_models::DoublePendulumMuJoCo>()};
+  if (robot < 0 || robot > 14) return nullptr;
   return &views[robot];
 }
 
@@ -952,6 +953,18 @@ static void mujoco3d_obs(const MV& m, const pbg_pack_in* in, pbg_pack_out* out) 
 //    done = y2 + 0.3 <= 1.
 static void pendulum_obs(const MV& m, const double* jq, const double* jqd, const double* tip, float* obs,
                          double* rew, uint8_t* done) {
+  if (m.alive == 7) {  // MuJoCo obs (mujoco robot_pendula.py:75-89, mujoco gym_pendulum_envs.py:60-72)
+    const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
+    const double px = tip[0], py = tip[2];
+    auto clip10 = [](double v) { return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v); };
+    const double o[11] = {x, sin(th), sin(g), cos(th), cos(g), clip10(vx), clip10(thd), clip10(gd), 0.0, 0.0, 0.0};
+    for (int i = 0; i < 11; i++) obs[i] = (float)o[i];
+    const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
+    const double vel_penalty = 1e-3 * (thd * thd) + 5e-3 * (gd * gd);
+    if (rew) *rew = ((0.0 + 10.0) + -dist_penalty) + -vel_penalty;
+    if (done) *done = py + 0.3 <= 1;
+    return;
+  }
   if (m.alive == 6) {
     const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
     const double px = tip[0], py = tip[2];

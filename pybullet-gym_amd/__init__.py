@@ -10,7 +10,7 @@ ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheeta
            "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
            "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
            "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0",
-           "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0")
+           "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0")
 
 
 def __getattr__(name):

@@ -15,7 +15,8 @@ ROBOT_IDS = {"InvertedPendulumPyBulletEnv-v0": 0, "HopperPyBulletEnv-v0": 1, "Ha
              "AntPyBulletEnv-v0": 3, "HumanoidPyBulletEnv-v0": 4, "Walker2DPyBulletEnv-v0": 5,
              "InvertedPendulumSwingupPyBulletEnv-v0": 6, "InvertedDoublePendulumPyBulletEnv-v0": 7,
              "HumanoidFlagrunPyBulletEnv-v0": 8, "HopperMuJoCoEnv-v0": 9, "Walker2DMuJoCoEnv-v0": 10,
-             "HalfCheetahMuJoCoEnv-v0": 11, "AntMuJoCoEnv-v0": 12, "HumanoidMuJoCoEnv-v0": 13}
+             "HalfCheetahMuJoCoEnv-v0": 11, "AntMuJoCoEnv-v0": 12, "HumanoidMuJoCoEnv-v0": 13,
+             "InvertedDoublePendulumMuJoCoEnv-v0": 14}
 
 
 class PbgError(RuntimeError):

@@ -41,7 +41,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
     if spec.motor_order is not None:
         assert spec.motor_order == ordered_names, "Humanoid motor order == ordered_joints order"
     tip_link = -1
-    if spec.kind == robots.KIND_PENDULUM and spec.alive == robots.ALIVE_DOUBLE:
+    if spec.kind == robots.KIND_PENDULUM and spec.alive in (robots.ALIVE_DOUBLE, robots.ALIVE_DOUBLE_MJ):
         # robot_pendula.py:72-88: slider torque 200*clip(a0); reset randomises hinge, hinge2
         # (:66-68); calc_state reads hinge, hinge2, slider and pole2's position (:81-83).
         act_links = [model.link_index("cart")]
@@ -283,12 +283,14 @@ def emit_struct(t: Dict) -> str:
 
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
-             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13}
+             "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
+             "double_pendulum_mujoco": 14}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
            "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun",
            "hopper_mujoco": "HopperMuJoCo", "walker2d_mujoco": "Walker2DMuJoCo",
-           "halfcheetah_mujoco": "HalfCheetahMuJoCo", "ant_mujoco": "AntMuJoCo", "humanoid_mujoco": "HumanoidMuJoCo"}
+           "halfcheetah_mujoco": "HalfCheetahMuJoCo", "ant_mujoco": "AntMuJoCo", "humanoid_mujoco": "HumanoidMuJoCo",
+           "double_pendulum_mujoco": "DoublePendulumMuJoCo"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -25,7 +25,7 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[14][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[15][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
@@ -38,8 +38,9 @@ int env_robot_id(const char* env_id) {
                                   {"Walker2DMuJoCoEnv-v0", "walker2d_mujoco"},
                                   {"HalfCheetahMuJoCoEnv-v0", "halfcheetah_mujoco"},
                                   {"AntMuJoCoEnv-v0", "ant_mujoco"},
-                                  {"HumanoidMuJoCoEnv-v0", "humanoid_mujoco"}};
-  for (int i = 0; i < 14; i++)
+                                  {"HumanoidMuJoCoEnv-v0", "humanoid_mujoco"},
+                                  {"InvertedDoublePendulumMuJoCoEnv-v0", "double_pendulum_mujoco"}};
+  for (int i = 0; i < 15; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -71,12 +72,12 @@ pbg_info_t info_of(int rid) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
 
 const Ops* ops(int rid) {
-  static const Ops table[14] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+  static const Ops table[15] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
                                 PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5), PBG_OPS(PendulumSwingup, 6),
                                 PBG_OPS(DoublePendulum, 7), PBG_OPS(HumanoidFlagrun, 8), PBG_OPS(HopperMuJoCo, 9),
                                 PBG_OPS(Walker2DMuJoCo, 10), PBG_OPS(HalfCheetahMuJoCo, 11), PBG_OPS(AntMuJoCo, 12),
-                                PBG_OPS(HumanoidMuJoCo, 13)};
-  return (rid >= 0 && rid < 14) ? &table[rid] : nullptr;
+                                PBG_OPS(HumanoidMuJoCo, 13), PBG_OPS(DoublePendulumMuJoCo, 14)};
+  return (rid >= 0 && rid < 15) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {

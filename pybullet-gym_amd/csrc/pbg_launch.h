@@ -45,4 +45,5 @@ PBG_DECLARE_ROBOT(Walker2DMuJoCo)
 PBG_DECLARE_ROBOT(HalfCheetahMuJoCo)
 PBG_DECLARE_ROBOT(AntMuJoCo)
 PBG_DECLARE_ROBOT(HumanoidMuJoCo)
+PBG_DECLARE_ROBOT(DoublePendulumMuJoCo)
 }  // namespace pbg

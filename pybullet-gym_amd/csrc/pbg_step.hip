@@ -1257,7 +1257,21 @@ PBG_DEV void mujoco3d_pack(const PackIn<R>& in, const float* act, float* obs, Pa
 template <class R>
 PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip, float* obs, PackOut& out) {
   out.potential = 0.0; out.initial_z = 0.0; out.feet_out = 0;
-  if constexpr (R::alive == 6) {
+  if constexpr (R::alive == 7) {
+    // InvertedDoublePendulumMuJoCo: mujoco/robot_pendula.py:75-89 obs [x, sin th, sin g, cos th,
+    // cos g, clip(vx, th', g', +-10), qfrc_constraint zeros (3)]; mujoco/gym_pendulum_envs.py:60-72
+    // reward sum([10, -dist_penalty, -(1e-3 th'^2 + 5e-3 g'^2)]), done y2 + 0.3 <= 1
+    const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
+    const double px = tip[0], py = tip[2];
+    auto clip10 = [](double v) { return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v); };
+    const double o[11] = {x, sin(th), sin(g), cos(th), cos(g), clip10(vx), clip10(thd), clip10(gd), 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 11; i++) obs[i] = (float)o[i];
+    const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
+    const double vel_penalty = 1e-3 * (thd * thd) + 5e-3 * (gd * gd);
+    out.reward = ((0.0 + 10.0) + -dist_penalty) + -vel_penalty;
+    out.done = py + 0.3 <= 1;
+  } else if constexpr (R::alive == 6) {
     // InvertedDoublePendulum: robot_pendula.py:76-88, gym_pendulum_envs.py:69-80
     const double th = jq[0], thd = jqd[0], g = jq[1], gd = jqd[1], x = jq[2], vx = jqd[2];
     const double px = tip[0], py = tip[2];  // pos_x, _, pos_y = pole2.pose().xyz()

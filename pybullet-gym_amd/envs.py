@@ -117,6 +117,7 @@ HumanoidMuJoCo = _robot_class("humanoid_mujoco", "Humanoid")           # :242-31
 InvertedPendulum = _robot_class("pendulum", "InvertedPendulum")  # robot_pendula.py:5-51
 InvertedPendulumSwingup = _robot_class("pendulum_swingup", "InvertedPendulumSwingup")  # robot_pendula.py:54-55
 InvertedDoublePendulum = _robot_class("double_pendulum", "InvertedDoublePendulum")      # robot_pendula.py:58-88
+InvertedDoublePendulumMuJoCo = _robot_class("double_pendulum_mujoco", "InvertedDoublePendulum")  # mujoco/robot_pendula.py:51-89
 InvertedPendulum.swingup = False
 InvertedPendulumSwingup.swingup = True
 
@@ -392,6 +393,18 @@ class InvertedDoublePendulumBulletEnv(BaseBulletEnv):
         return obs[0].cpu().numpy().astype(np.float64)
 
 
+class InvertedDoublePendulumMuJoCoEnv(InvertedDoublePendulumBulletEnv):
+    """mujoco/gym_pendulum_envs.py:44-75: obs float64 [x, sin th, sin g, cos th, cos g,
+    clip(vx, th', g'), zeros(3)]; reward 10 - dist_penalty - (1e-3 th'^2 + 5e-3 g'^2)."""
+    env_id = "InvertedDoublePendulumMuJoCoEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = InvertedDoublePendulumMuJoCo()
+        BaseBulletEnv.__init__(self, self.robot, render, device)
+        self.stateId = -1
+        self.scene = self.create_single_player_scene(None)
+
+
 ENV_CLASSES = {
     "InvertedPendulumPyBulletEnv-v0": InvertedPendulumBulletEnv,
     "InvertedPendulumSwingupPyBulletEnv-v0": InvertedPendulumSwingupBulletEnv,
@@ -407,11 +420,13 @@ ENV_CLASSES = {
     "HalfCheetahMuJoCoEnv-v0": HalfCheetahMuJoCoEnv,
     "AntMuJoCoEnv-v0": AntMuJoCoEnv,
     "HumanoidMuJoCoEnv-v0": HumanoidMuJoCoEnv,
+    "InvertedDoublePendulumMuJoCoEnv-v0": InvertedDoublePendulumMuJoCoEnv,
 }
 # envs/__init__.py:4-103 registry facts
 MAX_EPISODE_STEPS = {k: 1000 for k in ENV_CLASSES}
 REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-v0": 2500.0,
                     "InvertedPendulumSwingupPyBulletEnv-v0": 800.0, "InvertedDoublePendulumPyBulletEnv-v0": 9100.0,
+                    "InvertedDoublePendulumMuJoCoEnv-v0": 9100.0,
                     "Walker2DPyBulletEnv-v0": 2500.0, "Walker2DMuJoCoEnv-v0": 2500.0,
                     "HalfCheetahMuJoCoEnv-v0": 3000.0, "HopperMuJoCoEnv-v0": 2500.0, "AntMuJoCoEnv-v0": 2500.0,
                     "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}

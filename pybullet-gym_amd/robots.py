@@ -19,6 +19,7 @@ ALIVE_HUMANOID = 3     # robot_locomotors.py:191-192 (+2 if z>0.78 else -1)
 ALIVE_PENDULUM = 4     # gym_pendulum_envs.py:35-39  (reward 1, done |theta|>0.2)
 ALIVE_SWINGUP = 5      # gym_pendulum_envs.py:31-34  (reward cos(theta), never done)
 ALIVE_DOUBLE = 6       # gym_pendulum_envs.py:69-80  (reward 10 - dist_penalty, done pos_y+0.3<=1)
+ALIVE_DOUBLE_MJ = 7    # mujoco/gym_pendulum_envs.py:60-72 (also - vel_penalty; MuJoCo obs)
 
 KIND_WALKER = 0
 KIND_PENDULUM = 1
@@ -78,6 +79,12 @@ _add(RobotSpec("InvertedPendulumSwingupPyBulletEnv-v0", "pendulum_swingup", "inv
 # InvertedDoublePendulum: robot_pendula.py:58-88, gym_pendulum_envs.py:45-86, envs/__init__.py:11-16
 _add(RobotSpec("InvertedDoublePendulumPyBulletEnv-v0", "double_pendulum", "inverted_double_pendulum.xml", "cart",
                action_dim=1, obs_dim=9, kind=KIND_PENDULUM, power=2.0, alive=ALIVE_DOUBLE,
+               timestep=0.0165, frame_skip=1, floor=False))
+# InvertedDoublePendulumMuJoCoEnv: mujoco/robot_pendula.py:51-89, mujoco/gym_pendulum_envs.py:44-75,
+# envs/__init__.py:113-118 (InvertedPendulumMuJoCoEnv-v0 is not built: its reset reads
+# `self.swingup`, which the mujoco InvertedPendulum never defines -> AttributeError)
+_add(RobotSpec("InvertedDoublePendulumMuJoCoEnv-v0", "double_pendulum_mujoco", "inverted_double_pendulum.xml",
+               "cart", action_dim=1, obs_dim=11, kind=KIND_PENDULUM, power=2.0, alive=ALIVE_DOUBLE_MJ,
                timestep=0.0165, frame_skip=1, floor=False))
 # Hopper: robot_locomotors.py:82-90, envs/__init__.py:73-78
 _add(RobotSpec("HopperPyBulletEnv-v0", "hopper", "hopper.xml", "torso", action_dim=3, obs_dim=15,

@@ -52,6 +52,7 @@ ROBOTS = {
     "halfcheetah_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HalfCheetahMuJoCoEnv"),
     "ant_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "AntMuJoCoEnv"),
     "humanoid_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HumanoidMuJoCoEnv"),
+    "double_pendulum_mujoco": ("pybulletgym.envs.mujoco.gym_pendulum_envs", "InvertedDoublePendulumMuJoCoEnv"),
 }
 
 

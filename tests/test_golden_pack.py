@@ -55,7 +55,7 @@ def test_oracle_pack_bit_exact(key):
             np.testing.assert_array_equal(out["feet"], g["feet_out"][i][: len(out["feet"])])
 
 
-PENDULUMS = ["pendulum", "pendulum_swingup", "double_pendulum"]
+PENDULUMS = ["pendulum", "pendulum_swingup", "double_pendulum", "double_pendulum_mujoco"]
 
 
 @pytest.mark.parametrize("key", PENDULUMS)
@@ -74,7 +74,7 @@ def test_oracle_pack_pendulum(key):
         np.testing.assert_array_equal(out["obs"].view(np.uint32), ref.view(np.uint32), err_msg=f"call {i}")
         if step:
             assert out["done"] == bool(g["done"][i]), f"call {i}"
-            assert out["reward"] == g["reward"][i], f"call {i}"
+            assert out["reward"] == g["reward"][i] or (np.isnan(out["reward"]) and np.isnan(g["reward"][i])), f"call {i}"
 
 
 MUJOCO_PLANAR = ["hopper_mujoco", "walker2d_mujoco", "halfcheetah_mujoco"]

@@ -28,7 +28,7 @@ ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPy
         "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
         "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
         "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0",
-        "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0"]
+        "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
