@@ -822,6 +822,29 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   return nc;
 }
 
+// The env's final stores dealt over the gang (state and obs are bitwise identical in every
+// lane): lane t writes state words t, t+T, ... ([word][env]) and observation entries t,
+// t+T, ... ([env][D]) -- a few full-wave stores instead of one partial store per word from
+// lane 0, whose queue of ~100 outstanding stores stalled the wave.
+template <class R, int T>
+PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __restrict__ st, int n,
+                        float* __restrict__ obs_out, int e, int t) {
+  constexpr int SW = PBG_BASE_WORDS + 2 * R::NJ;
+  float w[SW];  // store_state's word order
+#pragma unroll
+  for (int i = 0; i < 3; i++) { w[i] = s.bp[i]; w[7 + i] = s.bv[i]; w[10 + i] = s.bw[i]; }
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[3 + i] = s.bq[i];
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) { w[PBG_BASE_WORDS + d] = s.q[d]; w[PBG_BASE_WORDS + R::NJ + d] = s.qd[d]; }
+  static_for<0, (SW + T - 1) / T>([&](auto m_c) {
+    constexpr int m = decltype(m_c)::value;
+    const float v = lanes_pick<T, m, SW>(w, t);
+    if (m * T + t < SW) st[(size_t)(m * T + t) * n + e] = v;
+  });
+  lanes_store_row<R, T>(obs, obs_out, e, t);
+}
+
 template <class R, int T, bool DIST>
 __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
@@ -915,10 +938,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     if (io.trunc) io.trunc[e] = trunc && !term;
   }
   if (io.autoreset && (term || trunc)) {
-    if (io.term_obs && w0) {
-#pragma unroll
-      for (int i = 0; i < R::OBS; i++) io.term_obs[(size_t)e * R::OBS + i] = obs[i];
-    }
+    if (io.term_obs) lanes_store_row<R, T>(obs, io.term_obs, e, X.t);
     bool has_floor = flags & 1u;
     double pot;
     float z0;
@@ -937,12 +957,8 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     B.elapsed[e] = el;
     B.flags[e] = flags;
   }
-  if (w0) {
-    store_state<R>(s, B.st, B.n, e);
-    store_flag<R>(B, e, fl);
-#pragma unroll
-    for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
-  }
+  if (w0) store_flag<R>(B, e, fl);
+  gang_store<R, T>(s, obs, B.st, B.n, io.obs, e, X.t);
   STAMP(9)
   STAMP_FLUSH
 }

@@ -258,6 +258,26 @@ PBG_DEV void store_state(const State<R>& s, float* __restrict__ st, int n, int e
   for (int d = 0; d < R::NJ; d++) st[(size_t)(PBG_BASE_WORDS + R::NJ + d) * n + e] = s.qd[d];
 }
 
+// Stores of a value replicated over T cooperating lanes (gang / quad kernels), dealt over
+// them: lane t stores elements t, t+T, ... -- each element picked by selects, so the
+// register arrays are never indexed at run time.
+template <int T, int M, int W>
+PBG_DEV float lanes_pick(const float (&v)[W], int t) {  // v[M*T + t] by selects (no indexed registers)
+  float r = v[M * T];
+  static_for<1, T>([&](auto k_c) {
+    constexpr int k = decltype(k_c)::value;
+    if constexpr (M * T + k < W) r = t == k ? v[M * T + k] : r;
+  });
+  return r;
+}
+template <class R, int T>
+PBG_DEV void lanes_store_row(const float (&obs)[R::OBS], float* __restrict__ out, int e, int t) {  // out[e][:]
+  static_for<0, (R::OBS + T - 1) / T>([&](auto m_c) {
+    constexpr int m = decltype(m_c)::value;
+    const float v = lanes_pick<T, m, R::OBS>(obs, t);
+    if (m * T + t < R::OBS) out[(size_t)e * R::OBS + m * T + t] = v;
+  });
+}
 // load snapshot (gym_locomotion_envs.py:23-25 restoreState) + reset noise on reset dofs
 template <class R>
 PBG_DEV void snapshot_state(State<R>& s) {

@@ -1189,10 +1189,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     if (io.trunc) io.trunc[e] = trunc && !term;
   }
   if (io.autoreset && (term || trunc)) {
-    if (io.term_obs && kb == 0) {
-#pragma unroll
-      for (int i = 0; i < R::OBS; i++) io.term_obs[(size_t)e * R::OBS + i] = obs[i];
-    }
+    if (io.term_obs) lanes_store_row<R, 4>(obs, io.term_obs, e, kb);
     bool has_floor = flags & 1u;
     double pot;
     float z0;
@@ -1208,17 +1205,16 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     B.elapsed[e] = el;
     B.flags[e] = flags;
   }
-  if (kb == 0) {
-#pragma unroll
-    for (int i = 0; i < 3; i++) B.st[(size_t)i * B.n + e] = s.bp[i];
-#pragma unroll
-    for (int i = 0; i < 4; i++) B.st[(size_t)(3 + i) * B.n + e] = s.bq[i];
-#pragma unroll
-    for (int i = 0; i < 3; i++) B.st[(size_t)(7 + i) * B.n + e] = s.bv[i];
-#pragma unroll
-    for (int i = 0; i < 3; i++) B.st[(size_t)(10 + i) * B.n + e] = s.bw[i];
-#pragma unroll
-    for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
+  {
+    // replicated base words and obs dealt over the quad (lane kb: elements kb, kb+4, ...)
+    const float bw[PBG_BASE_WORDS] = {s.bp[0], s.bp[1], s.bp[2], s.bq[0], s.bq[1], s.bq[2], s.bq[3],
+                                      s.bv[0], s.bv[1], s.bv[2], s.bw[0], s.bw[1], s.bw[2]};
+    static_for<0, (PBG_BASE_WORDS + 3) / 4>([&](auto m_c) {
+      constexpr int m = decltype(m_c)::value;
+      const float v = lanes_pick<4, m, PBG_BASE_WORDS>(bw, kb);
+      if (4 * m + kb < PBG_BASE_WORDS) B.st[(size_t)(4 * m + kb) * B.n + e] = v;
+    });
+    lanes_store_row<R, 4>(obs, io.obs, e, kb);
   }
 #pragma unroll
   for (int j = 0; j < NDB; j++) {

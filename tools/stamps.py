@@ -12,8 +12,9 @@ L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
 names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS", "integrate", "act+load", "pack", "store"]
 gang_names = {0: "phase A (kin, composites)", 1: "mass matrix", 3: "cholesky+solve", 10: "stage to LDS", 4: "detect",
               11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 8: "pack", 9: "store"}
+AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
 for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]))]:
-    env = VecEnv(env_id, n, seed=1, autoreset=True)
+    env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET)
     env.reset()
     acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
     for i in range(10): env.step(acts[i])
