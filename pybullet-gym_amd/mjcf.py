@@ -13,10 +13,18 @@ unpinned by anything in this container):
   them massless dummies named ``<body>_dummy<i>``; a body with no joint becomes a
   ``jointfix_*`` fixed link.  Links are numbered in MJCF depth-first order, which is
   the order ``addToScene`` enumerates them (``robot_bases.py:60``).
-* B3 mass: geom volume x density (default 1000, capsule volume includes both
-  hemispheres), exact solid-capsule/sphere inertia about the body COM,
-  ``<inertial mass=..>`` overrides the body mass (inertia scaled), ``settotalmass``
-  rescales every body.  Joint ``armature`` is added to the joint-space inertia.
+* B3 mass: geom volume x 1000 (capsule volume includes both hemispheres; the geom
+  ``density`` attribute is not read: Ant's density="5" would leave a 0.9 kg ant on
+  250 N m motors), ``<inertial mass=..>`` overrides the body mass, ``settotalmass`` is not
+  read.  Inertia is Bullet's compound-shape approximation, not the solid's: the mass
+  times the box inertia of the link's collision AABB in the link frame
+  (btCompoundShape::calculateLocalInertia, applied by URDF2Bullet when loadMJCF is not
+  given URDF_USE_INERTIA_FROM_FILE -- robot_bases.py:108,116 pass only self-collision
+  flags), diagonal in the link axes.  Joint ``armature`` is not modelled (btMultiBody has
+  none).  These four choices are backed by the reference's pretrained roboschool
+  policies (tests/test_policies.py): each one raises or holds every policy's score on the
+  oracle (Hopper 60 -> 1130 mean return, Ant -119 -> 734, InvertedDoublePendulum
+  3125 -> 4368) against the exact-solid / armature / density / settotalmass rules.
 * B4 collision: every robot geom whose contype or conaffinity is non-zero collides
   with the floor; robot-robot pairs follow MuJoCo's contype/conaffinity rule and
   exclude every ancestor pair (URDF_USE_SELF_COLLISION_EXCLUDE_ALL_PARENTS,
@@ -213,6 +221,55 @@ def combine_mass(parts):
     return M, com, inertia
 
 
+PYBULLET_MJCF_DENSITY = 1000.0
+APPLY_SETTOTALMASS = False
+
+
+def _shortest_arc(u: np.ndarray) -> np.ndarray:
+    """Rotation taking +z to unit vector u (Bullet's shortestArcQuat, as the MJCF importer
+    orients a fromto capsule: a btCapsuleShapeZ in a child transform)."""
+    z = np.array([0.0, 0.0, 1.0])
+    v = np.cross(z, u)
+    s = float(np.linalg.norm(v))
+    c = float(np.dot(z, u))
+    if s < 1e-12:
+        return np.eye(3) if c > 0 else np.diag([1.0, -1.0, -1.0])
+    k = v / s
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    ang = math.atan2(s, c)
+    return np.eye(3) + math.sin(ang) * K + (1 - math.cos(ang)) * (K @ K)
+
+
+def collision_aabb(geoms) -> Tuple[np.ndarray, np.ndarray]:
+    """AABB (link frame) of a link's collision shapes as Bullet computes it: each capsule is
+    a Z capsule with half extents (r, r, r + h/2) whose box is rotated into the link frame
+    (btCapsuleShape::getAabb: |R| he), a sphere is +-r; the compound takes the union."""
+    lo = np.full(3, np.inf)
+    hi = np.full(3, -np.inf)
+    for g in geoms:
+        c = 0.5 * (g.p0 + g.p1)
+        if g.kind == GEOM_SPHERE:
+            ext = np.full(3, g.radius)
+        else:
+            seg = g.p1 - g.p0
+            L = float(np.linalg.norm(seg))
+            u = seg / L if L > 1e-12 else np.array([0.0, 0.0, 1.0])
+            ext = np.abs(_shortest_arc(u)) @ np.array([g.radius, g.radius, g.radius + 0.5 * L])
+        lo = np.minimum(lo, c - ext)
+        hi = np.maximum(hi, c + ext)
+    return lo, hi
+
+
+def bullet_compound_inertia(geoms, mass: float) -> np.ndarray:
+    """btCompoundShape::calculateLocalInertia: "approximation: take the inertia from the
+    aabb" -- the solid box of the compound's AABB, I = m/12 (l_y^2 + l_z^2, ...), diagonal in
+    the link axes (the inertial frame of an MJCF body without <inertial> is unrotated)."""
+    lo, hi = collision_aabb(geoms)
+    l = hi - lo
+    return np.diag([mass / 12.0 * (l[1] ** 2 + l[2] ** 2), mass / 12.0 * (l[0] ** 2 + l[2] ** 2),
+                    mass / 12.0 * (l[0] ** 2 + l[1] ** 2)])
+
+
 # ----------------------------------------------------------------------------- parser
 def _floats(s: Optional[str], n: Optional[int] = None) -> Optional[np.ndarray]:
     if s is None:
@@ -272,7 +329,7 @@ def _frame_of(ctx: _Ctx, el) -> Tuple[np.ndarray, np.ndarray]:
 def _parse_geom(ctx: _Ctx, g) -> Tuple[Geom, float]:
     kind_s = ctx.gattr(g, "type", "sphere")
     size = _floats(ctx.gattr(g, "size"))
-    density = float(ctx.gattr(g, "density", "1000"))
+    density = PYBULLET_MJCF_DENSITY  # B3: the geom density attribute is not read
     fr = _floats(ctx.gattr(g, "friction", "1 0.005 0.0001"))
     contype = int(ctx.gattr(g, "contype", "1"))
     conaff = int(ctx.gattr(g, "conaffinity", "1"))
@@ -326,6 +383,8 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
             m_new = float(inert.get("mass"))
             scale = m_new / M if M > 0 else 0.0
             M, inertia = m_new, inertia * scale
+        if geoms:
+            inertia = bullet_compound_inertia(geoms, M)
         return M, com, inertia, geoms
 
     def joint_info(j, rot_body_to_link=np.eye(3)):
@@ -354,7 +413,7 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
         return dict(jtype=jtype, axis=axis, anchor=anchor, lower=lo if limited else 0.0,
                     upper=hi if limited else -1.0, limited=limited,
                     damping=float(ctx.jattr(j, "damping", "0")),
-                    armature=float(ctx.jattr(j, "armature", "0")),
+                    armature=0.0,  # B3: btMultiBody has no armature
                     joint_name=j.get("name"))
 
     def add_body(b, parent_link: int, parent_pos_shift: np.ndarray):
@@ -407,7 +466,7 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
         add_body(rb, -1, np.zeros(3))
 
     model = RobotModel(name=robot_name, links=links, **base)
-    if ctx.settotalmass is not None:
+    if ctx.settotalmass is not None and APPLY_SETTOTALMASS:
         s = ctx.settotalmass / model.total_mass()
         model.base_mass *= s
         model.base_inertia = model.base_inertia * s

@@ -49,9 +49,32 @@ def test_ant_topology():
 
 
 def test_halfcheetah_mass_and_gains():
+    """settotalmass="14" is not read (mjcf.py B3); the feet's <inertial mass="10"/> is."""
     t = codegen.load_tables("halfcheetah")
-    assert abs(sum(t["link_mass"]) + t["base_mass"] - 14.0) < 1e-9  # settotalmass="14"
+    names = t["link_name"]
+    assert t["link_mass"][names.index("bfoot")] == 10.0 and t["link_mass"][names.index("ffoot")] == 10.0
+    assert sum(t["link_mass"]) + t["base_mass"] > 14.0
     assert t["act_gain"] == pytest.approx([0.9 * c for c in (120, 90, 60, 140, 60, 30)])
+
+
+def test_pybullet_importer_mass_rules():
+    """mjcf.py B3: density 1000 whatever the geom says (Ant's density="5"), no armature,
+    inertia = mass x box inertia of the link's collision AABB (btCompoundShape)."""
+    ant = codegen.load_tables("ant")
+    assert ant["base_mass"] == pytest.approx(1000 * 4 / 3 * np.pi * 0.25 ** 3)  # torso sphere r 0.25
+    # the sphere's AABB is a 0.5 m cube: I = m/12 (0.25 + 0.25)
+    assert ant["base_inertia"][:3] == pytest.approx([ant["base_mass"] / 12 * 0.5] * 3)
+    for t in (ant, codegen.load_tables("humanoid"), codegen.load_tables("hopper")):
+        assert all(a == 0.0 for a in t["dof_armature"])
+        for I in t["link_inertia"]:
+            assert I[3:] == [0.0, 0.0, 0.0]  # diagonal in the link axes
+    # pendulum pole: fromto capsule r 0.049 from (0,0,0) to (0.001,0,0.6)
+    pend = codegen.load_tables("pendulum")
+    g = mjcf.Geom("cpole", mjcf.GEOM_CAPSULE, 0.049, np.zeros(3), np.array([0.001, 0, 0.6]), 1.0, 0, 1)
+    m = pend["link_mass"][1]
+    assert np.diag(mjcf.bullet_compound_inertia([g], m)) == pytest.approx(pend["link_inertia"][1][:3])
+    lo, hi = mjcf.collision_aabb([g])
+    assert hi[2] - lo[2] == pytest.approx(np.hypot(0.001, 0.6) + 2 * 0.049, rel=1e-3)
 
 
 def test_humanoid_dummies_and_pairs():

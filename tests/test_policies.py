@@ -1,0 +1,57 @@
+"""Pretrained-policy behavioural regression (tests/policies.py).
+
+The reference's roboschool policies were trained on pybullet physics; on this simulator
+they are scored against a random policy on the same episodes.  The bands below are what the
+current physics achieves (DESIGN.md section 6 has the full table): they catch a physics
+regression, and they are the evidence behind the importer rules in mjcf.py B3 (armature,
+density, settotalmass, AABB inertia).  They are not a pybullet pin -- on pybullet these
+policies walk for the full 1,000 steps, which the Ant, Walker2D and Humanoid policies do
+not do here (physics parity is unpinned).
+"""
+import numpy as np
+import pytest
+import torch
+
+import policies
+
+# env id -> (envs, minimum mean return, minimum ratio to the random policy's mean)
+BANDS = {
+    "InvertedPendulumPyBulletEnv-v0": (8, 999.0, 10.0),
+    "InvertedDoublePendulumPyBulletEnv-v0": (8, 1500.0, 5.0),
+    "HopperPyBulletEnv-v0": (8, 500.0, 10.0),
+    "HalfCheetahPyBulletEnv-v0": (8, 300.0, 10.0),
+}
+
+
+@pytest.mark.parametrize("env_id", list(BANDS))
+def test_pretrained_policy_oracle(env_id):
+    n, floor, ratio = BANDS[env_id]
+    ret, length = policies.episode_returns_oracle(env_id, n, seed=0)
+    rnd = policies.random_returns_oracle(env_id, n, seed=0)
+    assert np.isfinite(ret).all()
+    assert ret.mean() >= floor, (ret.mean(), length)
+    assert ret.mean() >= ratio * max(rnd.mean(), 1.0), (ret.mean(), rnd.mean())
+
+
+def test_policy_weights_fixture_shapes():
+    """The extracted weights keep the reference's layer shapes (enjoy_TF_*.py:21-23)."""
+    for env_id in policies.POLICY_FILES:
+        w = policies.Policy(env_id).w
+        assert w[0].shape[1] == w[2].shape[0] and w[2].shape[1] == w[4].shape[0]
+        assert w[1].shape == (w[0].shape[1],) and w[5].shape == (w[4].shape[1],)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env_id", list(BANDS))
+def test_pretrained_policy_device(env_id):
+    """Same bands through the HIP step kernel, 64 episodes (trajectories diverge from the
+    oracle's chaotically after contact events; the score distribution must not)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pybulletgym_amd  # noqa: F401
+    _, floor, ratio = BANDS[env_id]
+    ret, length = policies.episode_returns_device(env_id, 64, seed=0)
+    rnd = policies.random_returns_oracle(env_id, 8, seed=0)
+    assert np.isfinite(ret).all()
+    assert ret.mean() >= floor, (ret.mean(), length.mean())
+    assert ret.mean() >= ratio * max(rnd.mean(), 1.0)
