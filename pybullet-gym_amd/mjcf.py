@@ -31,7 +31,11 @@ unpinned by anything in this container):
   ``robot_bases.py:116``).
 * B5 friction: geom friction[0] times the floor's lateral friction 0.8
   (``scene_stadium.py:33``); restitution 0 x 0.5 = 0.
-* B6 damping: MJCF joint damping, applied as -d*qdot once per env step.
+* B6 damping: the joint element's own ``damping`` attribute, applied as -d*qdot once per
+  env step; a ``<default><joint damping=..>`` is not inherited (pybullet's importer takes
+  only ``limited`` from joint defaults).  Evidence: with inherited damping 1 the
+  pretrained swing-up policy never swings the pole up (mean return -666); without it,
+  878 -- and InvertedDoublePendulum 4368 -> 6491 (tests/test_policies.py).
 * The base frame is the base's centre of mass (pybullet reports base and link
   positions of the inertial frame); link frames are MJCF body frames and keep a COM
   offset.  Inertial frames are not rotated to principal axes.
@@ -412,7 +416,7 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
             limited = False
         return dict(jtype=jtype, axis=axis, anchor=anchor, lower=lo if limited else 0.0,
                     upper=hi if limited else -1.0, limited=limited,
-                    damping=float(ctx.jattr(j, "damping", "0")),
+                    damping=float(j.get("damping", "0")),  # B6: the joint's own attribute only
                     armature=0.0,  # B3: btMultiBody has no armature
                     joint_name=j.get("name"))
 

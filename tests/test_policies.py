@@ -4,7 +4,7 @@ The reference's roboschool policies were trained on pybullet physics; on this si
 they are scored against a random policy on the same episodes.  The bands below are what the
 current physics achieves (DESIGN.md section 6 has the full table): they catch a physics
 regression, and they are the evidence behind the importer rules in mjcf.py B3 (armature,
-density, settotalmass, AABB inertia).  They are not a pybullet pin -- on pybullet these
+density, settotalmass, AABB inertia) and B6 (damping).  They are not a pybullet pin -- on pybullet these
 policies walk for the full 1,000 steps, which the Ant, Walker2D and Humanoid policies do
 not do here (physics parity is unpinned).
 """
@@ -17,7 +17,8 @@ import policies
 # env id -> (envs, minimum mean return, minimum ratio to the random policy's mean)
 BANDS = {
     "InvertedPendulumPyBulletEnv-v0": (8, 999.0, 10.0),
-    "InvertedDoublePendulumPyBulletEnv-v0": (8, 1500.0, 5.0),
+    "InvertedPendulumSwingupPyBulletEnv-v0": (8, 700.0, None),  # swings up and balances (random: -920)
+    "InvertedDoublePendulumPyBulletEnv-v0": (8, 3000.0, 10.0),
     "HopperPyBulletEnv-v0": (8, 500.0, 10.0),
     "HalfCheetahPyBulletEnv-v0": (8, 300.0, 10.0),
 }
@@ -30,7 +31,8 @@ def test_pretrained_policy_oracle(env_id):
     rnd = policies.random_returns_oracle(env_id, n, seed=0)
     assert np.isfinite(ret).all()
     assert ret.mean() >= floor, (ret.mean(), length)
-    assert ret.mean() >= ratio * max(rnd.mean(), 1.0), (ret.mean(), rnd.mean())
+    if ratio is not None:
+        assert ret.mean() >= ratio * max(rnd.mean(), 1.0), (ret.mean(), rnd.mean())
 
 
 def test_policy_weights_fixture_shapes():
@@ -54,4 +56,5 @@ def test_pretrained_policy_device(env_id):
     rnd = policies.random_returns_oracle(env_id, 8, seed=0)
     assert np.isfinite(ret).all()
     assert ret.mean() >= floor, (ret.mean(), length.mean())
-    assert ret.mean() >= ratio * max(rnd.mean(), 1.0)
+    if ratio is not None:
+        assert ret.mean() >= ratio * max(rnd.mean(), 1.0)
