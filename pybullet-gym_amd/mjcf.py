@@ -31,8 +31,9 @@ unpinned by anything in this container):
   ``robot_bases.py:116``).
 * B5 friction: geom friction[0] times the floor's lateral friction 0.8
   (``scene_stadium.py:33``); restitution 0 x 0.5 = 0.
-* B6 damping: the joint element's own ``damping`` attribute, applied as -d*qdot once per
-  env step; a ``<default><joint damping=..>`` is not inherited (pybullet's importer takes
+* B6 damping: the joint element's own ``damping`` attribute, applied as -d*qdot from each
+  sub-step's velocity (pybullet applies it per stepSimulation; per sub-step is the stable
+  choice at dt/4); a ``<default><joint damping=..>`` is not inherited (pybullet's importer takes
   only ``limited`` from joint defaults).  Evidence: with inherited damping 1 the
   pretrained swing-up policy never swings the pole up (mean return -666); without it,
   878 -- and InvertedDoublePendulum 4368 -> 6491 (tests/test_policies.py).
