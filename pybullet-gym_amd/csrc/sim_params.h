@@ -7,7 +7,9 @@
 #pragma once
 
 #define PBG_GRAVITY 9.8                 // gym_locomotion_envs.py:19, gym_pendulum_envs.py:14
-#define PBG_CONTACT_ERP 0.9             // scene_bases.py:62 setDefaultContactERP(0.9)
+#define PBG_CONTACT_ERP 0.2             // [EXT] btContactSolverInfo::m_erp: the multibody contact rows use m_erp;
+                                        // setDefaultContactERP(0.9) (scene_bases.py:62) sets m_erp2, used only
+                                        // for split-impulse penetrations deeper than 4 cm
 #define PBG_SOLVER_ITERATIONS 5         // scene_bases.py:65 numSolverIterations=5
 #define PBG_LIMIT_ERP 0.2               // [EXT] btContactSolverInfo::m_erp default
 #define PBG_LIMIT_MAX_IMPULSE 100.0     // [EXT] btMultiBodyJointLimitConstraint max impulse

@@ -19,7 +19,7 @@ BANDS = {
     "InvertedPendulumPyBulletEnv-v0": (8, 999.0, 10.0),
     "InvertedPendulumSwingupPyBulletEnv-v0": (8, 700.0, None),  # swings up and balances (random: -920)
     "InvertedDoublePendulumPyBulletEnv-v0": (8, 3000.0, 10.0),
-    "HopperPyBulletEnv-v0": (8, 500.0, 10.0),
+    "HopperPyBulletEnv-v0": (8, 1000.0, 30.0),
     "HalfCheetahPyBulletEnv-v0": (8, 300.0, 10.0),
 }
 
