@@ -201,14 +201,20 @@ struct Gang {
   static constexpr int PERC = DW + 1 + 3 * CRW;
   static constexpr int NJ1 = R::NJ > 0 ? R::NJ : 1;
   static constexpr int BW = 27;                // body record: Rm 9 | x 3 | c 3 | w 3 | v 3 | al 3 | ac 3
+  static constexpr int FW = 12;                // its frame part (Rm | x) lives at O_FR, stride FW; the
+  static constexpr int KW = BW - FW;           // kinematic part (c | w | v | al | ac) at O_KV, stride KW
   static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
   static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
   static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
-  static constexpr int O_FR = O_JO + 3 * NJ1, O_LP = O_FR + BW * NB, O_LR = O_LP + 2 * NLIM;
+  static constexpr int O_FR = O_JO + 3 * NJ1, O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
   static constexpr int LRSZ = NLIM * LRW > NB * CW ? NLIM * LRW : NB * CW;
   static constexpr int FIXED = O_LR + LRSZ;
+  // the kinematic parts are dead once M and the bias are built, before any contact is
+  // written: they share the start of the contact area (the env region holds >= KW*NB words)
+  static constexpr int O_KV = FIXED;
+  static constexpr int MIN_CONTACT_WORDS = KW * NB;
   static constexpr int GWORDS = (MAXC > 0 ? MAXC : 1) * PERC;  // device workspace per env
   static constexpr int ROUNDS_S = (R::NS + T - 1) / T;
 };
@@ -222,6 +228,12 @@ struct GangCtx {
   int t;         // lane in the gang
   int le;        // gang in the wave
 };
+// word w (0..26) of body b's record: frame part (w < 12) or kinematic part
+template <class R, int T>
+PBG_DEV lds_float* body_word(const lds_float* l, int b, int w) {
+  using G = Gang<R, T>;
+  return (lds_float*)l + (w < G::FW ? G::O_FR + G::FW * b + w : G::O_KV + G::KW * b + (w - G::FW));
+}
 // model tables, copied once per workgroup into LDS (vector-memory loads of a __constant__
 // table indexed by lane cost hundreds of cycles each; the level loops chain several)
 template <class R>
@@ -303,7 +315,7 @@ template <class R, int T>
 PBG_DEV f3 gang_O(const GangCtx& X) {
   using G = Gang<R, T>;
   constexpr int rb = Dims<R>::REF_BODY;
-  const lds_float* p = X.l + G::O_FR + G::BW * rb + 12;
+  const lds_float* p = body_word<R, T>(X.l, rb, 12);
   return mk3(p[0], p[1], p[2]);
 }
 template <class R, int T>
@@ -317,14 +329,13 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
   // base record and joint state (replicated registers -> LDS)
   if (w0) {
     const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
-    lds_float* p = X.l + G::O_FR;
     const float rec[G::BW] = {Rb.m[0], Rb.m[1], Rb.m[2], Rb.m[3], Rb.m[4], Rb.m[5], Rb.m[6], Rb.m[7], Rb.m[8],
                               s.bp[0], s.bp[1], s.bp[2], s.bp[0], s.bp[1], s.bp[2],
                               R::floating ? s.bw[0] : 0.f, R::floating ? s.bw[1] : 0.f, R::floating ? s.bw[2] : 0.f,
                               R::floating ? s.bv[0] : 0.f, R::floating ? s.bv[1] : 0.f, R::floating ? s.bv[2] : 0.f,
                               0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < G::BW; i++) p[i] = rec[i];
+    for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, 0, i) = rec[i];
 #pragma unroll
     for (int d = 0; d < R::NJ; d++) { X.l[G::O_Q + d] = s.q[d]; X.l[G::O_QD + d] = s.qd[d]; }
   }
@@ -335,12 +346,13 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
 #pragma unroll 1
     for (int idx = TD.lev_start[lv] + X.t; idx < TD.lev_start[lv + 1]; idx += T) {
       const int b = TD.lev_body[idx], p = TD.parent[b], jt = TD.jt[b], d = TD.dof[b];
-      const lds_float* P = X.l + G::O_FR + G::BW * p;
+      const lds_float* P = body_word<R, T>(X.l, p, 0);
+      const lds_float* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
       m3 Rp, Ro;
 #pragma unroll
       for (int i = 0; i < 9; i++) { Rp.m[i] = P[i]; Ro.m[i] = TD.ro[b][i]; }
-      const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(P[12], P[13], P[14]), wp = mk3(P[15], P[16], P[17]);
-      const f3 vp = mk3(P[18], P[19], P[20]), alp = mk3(P[21], P[22], P[23]), acp = mk3(P[24], P[25], P[26]);
+      const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(PK[12], PK[13], PK[14]), wp = mk3(PK[15], PK[16], PK[17]);
+      const f3 vp = mk3(PK[18], PK[19], PK[20]), alp = mk3(PK[21], PK[22], PK[23]), acp = mk3(PK[24], PK[25], PK[26]);
       const m3 R0 = mul(Rp, Ro);
       const f3 x0 = xp + mul(Rp, mk3(TD.opos[b][0], TD.opos[b][1], TD.opos[b][2]));
       const f3 axl = mk3(TD.axis[b][0], TD.axis[b][1], TD.axis[b][2]);
@@ -388,9 +400,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
       }
       const float rec[G::BW] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
                                 x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z};
-      lds_float* Q = X.l + G::O_FR + G::BW * b;
 #pragma unroll
-      for (int i = 0; i < G::BW; i++) Q[i] = rec[i];
+      for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, b, i) = rec[i];
     }
     PBG_GANG_SYNC
   });
@@ -398,12 +409,13 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
   // per-body inertia and wrench about O; motion vectors about O
 #pragma unroll 1
   for (int b = X.t; b < NB; b += T) {
-    const lds_float* P = X.l + G::O_FR + G::BW * b;
+    const lds_float* P = body_word<R, T>(X.l, b, 0);
+    const lds_float* PK = body_word<R, T>(X.l, b, G::FW) - G::FW;
     m3 Rm;
 #pragma unroll
     for (int i = 0; i < 9; i++) Rm.m[i] = P[i];
-    const f3 c = mk3(P[12], P[13], P[14]), w = mk3(P[15], P[16], P[17]), v = mk3(P[18], P[19], P[20]);
-    const f3 al = mk3(P[21], P[22], P[23]), ac = mk3(P[24], P[25], P[26]);
+    const f3 c = mk3(PK[12], PK[13], PK[14]), w = mk3(PK[15], PK[16], PK[17]), v = mk3(PK[18], PK[19], PK[20]);
+    const f3 al = mk3(PK[21], PK[22], PK[23]), ac = mk3(PK[24], PK[25], PK[26]);
     const float m = TD.mass[b];
     float I6[6];
 #pragma unroll
@@ -552,11 +564,12 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       }
 #pragma unroll
       for (int b = 0; b < D::NB; b++) {
-        lds_float* p = X.l + G::O_FR + G::BW * b;
+        lds_float* p = body_word<R, T>(X.l, b, 0);
 #pragma unroll
         for (int i = 0; i < 9; i++) p[i] = k.Rm[b].m[i];
         p[9] = k.x[b].x; p[10] = k.x[b].y; p[11] = k.x[b].z;
-        p[12] = k.c[b].x; p[13] = k.c[b].y; p[14] = k.c[b].z;
+        lds_float* pk = body_word<R, T>(X.l, b, G::FW);
+        pk[0] = k.c[b].x; pk[1] = k.c[b].y; pk[2] = k.c[b].z;
       }
     }
   }
@@ -565,7 +578,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   PBG_GANG_SYNC
   STAMP(10)
   auto frame = [&](int b, m3& Rm, f3& x) {
-    const lds_float* p = X.l + G::O_FR + G::BW * b;
+    const lds_float* p = body_word<R, T>(X.l, b, 0);
 #pragma unroll
     for (int i = 0; i < 9; i++) Rm.m[i] = p[i];
     x = mk3(p[9], p[10], p[11]);

@@ -90,7 +90,7 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     g->team = 16;
     g->block = PBG_GANG_BLOCK;
     g->lds_rows = cap;
-    g->env_words = G::FIXED + cap * G::PERC;
+    g->env_words = G::FIXED + (cap * G::PERC > G::MIN_CONTACT_WORDS ? cap * G::PERC : G::MIN_CONTACT_WORDS);
     g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
     g->scratch_words_per_env = G::GWORDS;
     const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;

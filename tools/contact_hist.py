@@ -1,0 +1,17 @@
+"""Contact-count histogram per env-step under random actions (dev tool: LDS capacity sizing)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import pybulletgym_amd  # noqa: F401
+from pybulletgym_amd.vec_env import VecEnv
+for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["HumanoidPyBulletEnv-v0:4096"]))]:
+    env = VecEnv(env_id, n, seed=3, autoreset=True)
+    env.reset()
+    h = torch.zeros(64, dtype=torch.int64, device="cuda")
+    for i in range(200):
+        env.step(torch.rand((n, env.info.action_dim), device="cuda") * 2 - 1, want_contacts=True)
+        if i >= 50:
+            h += torch.bincount(env.ncontact.clamp(max=63).long(), minlength=64)
+    h = h.cpu().tolist()
+    tot = sum(h)
+    print(env_id, "contacts per env-step:", {k: round(v / tot, 3) for k, v in enumerate(h) if v}, flush=True)
