@@ -114,41 +114,33 @@ def timed_rollout(VecEnv, env_id, n, steps, warmup, dev, rank, world, no_graph):
     if not no_graph:
         G = max(d for d in range(1, min(64, steps) + 1) if steps % d == 0)
         graph = env.capture([acts[j % pool] for j in range(G)])
-    # per-launch kernel time (roofline.kernel_ms), HIP events on the launch stream: around
-    # graph replays (back-to-back kernels) or, with --no-graph, around single launches
+    # per-launch kernel time (roofline.kernel_ms): HIP events on the launch stream around the
+    # timed region itself (graph replays are back-to-back kernels), so it describes the same
+    # launches as `value`; with --no-graph, events around each single launch
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if no_graph:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(100)]
-        for i in range(100):
-            ev[i][0].record(stream)
-            env.step(acts[(warmup + i) % pool])
-            ev[i][1].record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / 100
-    else:
-        reps = max(1, 200 // G)
-        e0.record(stream)
-        for _ in range(reps):
-            graph.replay()
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = e0.elapsed_time(e1) / (reps * G)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)] \
+        if no_graph else None
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    e0.record(stream)
     if no_graph:
         for i in range(steps):
+            ev[i][0].record(stream)
             env.step(acts[(warmup + i) % pool])
+            ev[i][1].record(stream)
     else:
         for _ in range(steps // G):
             graph.replay()
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) if no_graph else e0.elapsed_time(e1)) / steps
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -11,7 +11,8 @@ mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
+# the bench command itself (same steps / warmup), without the CPU leg
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
 for W in ant humanoid; do
   if [ $W = ant ]; then A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384"; else A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096"; fi
   B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline --second-env none $A"
