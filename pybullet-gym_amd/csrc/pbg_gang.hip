@@ -767,13 +767,14 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   {
     // joint-limit rows stay in registers for the whole solve
     constexpr int NL1 = NLIM > 0 ? NLIM : 1;
-    float ly[NL1][NSL], lm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
+    float ly[NL1][NSL], lm[NL1], lrm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
 #pragma unroll
     for (int li = 0; li < NLIM; li++) {
       const lds_float* p = X.l + G::O_LR + li * G::LRW;
 #pragma unroll
       for (int m = 0; m < NSL; m++) ly[li][m] = p[X.t + m * T];
       lm[li] = p[YS]; ltl[li] = p[YS + 1]; lth[li] = p[YS + 2];
+      lrm[li] = lm[li] > 0.f ? fast_rcp(lm[li]) : 0.f;  // off the sweeps' dependency chain
       llo[li] = 0.f; lhi[li] = 0.f;
     }
     for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
@@ -787,7 +788,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         const float nlo = fminf(fmaxf(llo[li] + meff * (ltl[li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo[li];
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
+        const float yu2 = meff > 0.f ? yu + dlo * lrm[li] : yu;
         const float nhi = fminf(fmaxf(lhi[li] + meff * (lth[li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi[li];
         llo[li] = nlo;

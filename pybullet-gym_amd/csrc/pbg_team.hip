@@ -813,7 +813,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     }
   });
   // every lane needs each branch's base part, m_eff and targets (replicated PGS math)
-  float BY[4][NLB_][6], Bm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
+  float BY[4][NLB_][6], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
   static_for<0, 4>([&](auto k_c) {
     constexpr int kk = decltype(k_c)::value;
     static_for<0, NLIMB>([&](auto l_c) {
@@ -821,6 +821,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) BY[kk][li][gg] = quad_bcast<kk>(LyB[li][gg]);
       Bm[kk][li] = quad_bcast<kk>(Lm[li]);
+      Brm[kk][li] = Bm[kk][li] > 0.f ? fast_rcp(Bm[kk][li]) : 0.f;  // off the sweeps' dependency chain
       Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
       Bth[kk][li] = quad_bcast<kk>(Lth[li]);
       Blo[kk][li] = 0.f;
@@ -947,7 +948,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         const float nlo = fminf(fmaxf(llo + meff * (Btl[kk][li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo;
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
+        const float yu2 = meff > 0.f ? yu + dlo * Brm[kk][li] : yu;
         const float nhi = fminf(fmaxf(lhi + meff * (Bth[kk][li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi;
         Blo[kk][li] = nlo;
