@@ -155,7 +155,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs-per-gpu", type=int, default=ENVS_PER_GPU)
     ap.add_argument("--env", default=ENV_ID)
-    ap.add_argument("--gather", action="store_true", help="also time the RCCL obs all-gather (separately)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip timing the RCCL obs all-gather (timed separately, outside `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
     ap.add_argument("--second-env", default="HumanoidPyBulletEnv-v0", help="second workload of the metric ('none' = off)")
@@ -203,7 +204,7 @@ def main():
         env2.close()
 
     gather_ms = None
-    if args.gather and world > 1:
+    if not args.no_gather and world > 1:
         for _ in range(3):
             gather_flat(env.obs)
         torch.cuda.synchronize(dev)
@@ -250,7 +251,10 @@ def main():
         if second is not None:
             out["humanoid" if "Humanoid" in second["env"] else "second"] = second
         if gather_ms is not None:
+            # the learner's optional flat batch: one all_gather_into_tensor of
+            # [envs_per_gpu, obs_dim] float32 per rank over RCCL, timed after the rollout
             out["allgather_obs_ms"] = gather_ms
+            out["allgather_obs_bytes"] = world * n * env.info.obs_dim * 4
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
