@@ -21,6 +21,8 @@ BANDS = {
     "InvertedDoublePendulumPyBulletEnv-v0": (8, 3000.0, 10.0),
     "HopperPyBulletEnv-v0": (8, 1000.0, 30.0),
     "HalfCheetahPyBulletEnv-v0": (8, 300.0, 10.0),
+    "Walker2DPyBulletEnv-v0": (8, 120.0, 5.0),
+    "AntPyBulletEnv-v0": (8, 650.0, 1.15),  # walks forward at ~0.7 m/s; random actions mostly stand (alive +1)
 }
 
 
