@@ -86,6 +86,20 @@ def valu_roofline(pmc, kernel_ms, n):
             "source": "profiles/" + os.path.basename(pmc.get("_path", "pmc"))}
 
 
+def occupancy(env):
+    """Step-kernel occupancy (Humanoid row): lanes per env, workgroup, LDS per
+    workgroup, registers per lane; waves per SIMD = min(register limit, LDS limit, waves the
+    env count provides / (256 CUs x 4 SIMDs))."""
+    i = env.info
+    waves = -(-env.num_envs * i.lanes_per_env // 64)
+    reg_limit = 512 // max(8 * -(-i.vgprs // 8), 1) if i.vgprs > 0 else 8
+    wgs_per_cu = (160 * 1024) // i.lds_bytes if i.lds_bytes > 0 else 32
+    lds_limit = max(1, wgs_per_cu * max(i.block // 64, 1) // 4)
+    return {"lanes_per_env": i.lanes_per_env, "block": i.block, "lds_bytes_per_workgroup": i.lds_bytes,
+            "vgprs": i.vgprs, "scratch_bytes": i.scratch_bytes, "lds_rows": i.lds_rows,
+            "waves_per_simd": min(reg_limit, lds_limit, max(1, waves // 1024))}
+
+
 def kernel_name(env):
     lpe = env.info.lanes_per_env
     k = {1: "pbg::step_kernel", 4: "pbg::team_step_kernel", 16: "pbg::gang_step_kernel"}.get(lpe, "pbg::step_kernel")
@@ -192,6 +206,7 @@ def main():
         second = {"env": args.second_env, "envs_per_gpu": n2, "global_envs": world * n2, "steps": steps2,
                   "value": world * n2 * steps2 / el2, "unit": "env-steps/s", "ms_per_step": el2 / steps2 * 1e3,
                   "kernel": kernel_name(env2), "kernel_ms": km2, "lanes_per_env": env2.info.lanes_per_env,
+                  "occupancy": occupancy(env2),
                   "obs_finite": bool(torch.isfinite(env2.obs).all())}
         alg2 = alg_bytes_per_env_step(env2.info)
         ach2 = alg2 * n2 / (km2 * 1e-3) / 1e9
@@ -245,6 +260,7 @@ def main():
                          "kernel": kernel_name(env), "kernel_ms": kernel_ms,
                          "alg_bytes_per_env_step": alg},
             "obs_finite": finite,
+            "occupancy": occupancy(env),
         }
         if pmc and pmc.get("valu_insts_per_launch"):
             out["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)

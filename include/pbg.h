@@ -48,7 +48,12 @@ typedef struct {
   int max_episode_steps; /* gym TimeLimit (envs/__init__.py) */
   int reset_dofs;        /* joints randomised by reset (robot_locomotors.py:18-19) */
   int floating;
-  int lanes_per_env;     /* step kernel geometry: 1 (lane per env) or 4 (quad per env) */
+  int lanes_per_env;     /* step kernel geometry: 1 (lane per env), 4 (quad) or 16 (gang) */
+  int block;             /* step kernel workgroup size (lanes) */
+  int lds_bytes;         /* dynamic LDS per step workgroup */
+  int vgprs;             /* step kernel registers per lane (hipFuncGetAttributes numRegs) */
+  int scratch_bytes;     /* step kernel private segment per lane (0: no spills to memory) */
+  int lds_rows;          /* contact rows (gang: contacts) resident in LDS per env */
 } pbg_info_t;
 
 typedef struct {

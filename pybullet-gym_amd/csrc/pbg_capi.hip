@@ -187,6 +187,11 @@ int pbg_info(const pbg_handle* h, pbg_info_t* out) {
   if (!h || !out) return fail(PBG_E_ARG, "pbg_info: NULL argument%s%ld");
   *out = h->info;
   out->lanes_per_env = h->geo.team;
+  out->block = h->geo.block;
+  out->lds_bytes = (int)h->geo.lds_bytes;
+  out->vgprs = h->geo.vgprs;
+  out->scratch_bytes = h->geo.scratch_bytes;
+  out->lds_rows = h->geo.lds_rows;
   return PBG_OK;
 }
 

@@ -20,6 +20,8 @@ struct Geometry {
   int gang_dist;     // gang: distributed (1) or replicated (0) unconstrained dynamics
   size_t lds_bytes;  // dynamic LDS per step workgroup
   size_t scratch_words_per_env;
+  int vgprs;          // the selected step kernel's registers per lane (hipFuncGetAttributes)
+  int scratch_bytes;  // and its private segment per lane
 };
 
 #define PBG_DECLARE_ROBOT(NAME)                                                                            \

@@ -20,6 +20,15 @@ using R = pbg_models::PBG_ROBOT;
 
 static inline unsigned blocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
 
+// registers / private segment of the step kernel a plan selected (pbg_info occupancy)
+static int kernel_attrs(const void* fn, Geometry* g) {
+  hipFuncAttributes a{};
+  const hipError_t e = hipFuncGetAttributes(&a, fn);
+  g->vgprs = e == hipSuccess ? a.numRegs : -1;
+  g->scratch_bytes = e == hipSuccess ? (int)a.localSizeBytes : -1;
+  return (int)e;
+}
+
 // Geometry: one env per lane, one wave per workgroup.  With fewer than 64 envs per CU
 // the workgroup shrinks to 32 or 16 active lanes so every CU gets a wave (the step is
 // issue/latency bound: a wave's time barely depends on its active lanes).  All resident
@@ -47,8 +56,9 @@ static int plan_team(int n_envs, int cus, Geometry* g) {
     g->lds_rows = cap;
     g->lds_bytes = (size_t)ES * sizeof(float) * per_env;
     g->scratch_words_per_env = RW::WORDS;
-    return (int)hipFuncSetAttribute((const void*)team_step_kernel<RR, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)g->lds_bytes);
+    const void* fn = (const void*)team_step_kernel<RR, 16>;
+    const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+    return e ? e : kernel_attrs(fn, g);
   } else {
     (void)n_envs; (void)cus; (void)g;
     return (int)hipErrorInvalidValue;
@@ -94,7 +104,8 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
     g->scratch_words_per_env = G::GWORDS;
     const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;
-    return (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+    const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+    return e ? e : kernel_attrs(fn, g);
   } else {
     (void)n_envs; (void)cus; (void)g;
     return (int)hipErrorInvalidValue;
@@ -138,11 +149,9 @@ int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   g->lds_rows = cap;
   g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
   g->scratch_words_per_env = RW::WORDS;
-  hipError_t e = hipSuccess;
-  if (b == 64) e = hipFuncSetAttribute((const void*)step_kernel<R, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
-  else if (b == 32) e = hipFuncSetAttribute((const void*)step_kernel<R, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
-  else e = hipFuncSetAttribute((const void*)step_kernel<R, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
-  return (int)e;
+  const void* fn = b == 64 ? (const void*)step_kernel<R, 64> : (b == 32 ? (const void*)step_kernel<R, 32> : (const void*)step_kernel<R, 16>);
+  const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+  return e ? e : kernel_attrs(fn, g);
 }
 
 int PBG_FN(launch_step_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {

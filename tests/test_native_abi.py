@@ -40,6 +40,14 @@ def test_pack_record_sizes_without_gpu():
     assert b"unknown env id" in lib.pbg_last_error()
 
 
+def test_info_struct_matches_header():
+    """_native.Info mirrors pbg_info_t field for field (all int)."""
+    src = open(HEADER).read()
+    body = src[src.index("typedef struct {", src.index("pbg_handle;")):src.index("} pbg_info_t;")]
+    fields = re.findall(r"\bint\s+([a-z_]+);", body)
+    assert fields == [f[0] for f in _native.Info._fields_]
+
+
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "_lib", None)
     monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
