@@ -7,10 +7,19 @@ envs per GPU (weak scaling: each rank owns 16,384 envs, no per-step collective).
 One "step" = one batched env step of every env on every GPU: apply_action, 4 physics
 sub-steps (Featherstone dynamics, contacts, 5-sweep PGS, integration), the
 observation/reward/done pack, TimeLimit + auto-reset -- one kernel launch per GPU.
-Actions are pre-generated U(-1, 1) float32 tensors already resident in HBM.
+
+Protocol: actions U(-1, 1) from Philox4x32-10 keyed by 0x5EED, counter
+(step, global env) -- pbg_sample_actions, generated into HBM before the timed region, one
+distinct batch per step; an untimed pre-roll (--preroll, 200 steps) ages the episodes past
+their first steps so the timed window sees steady-state contact counts and auto-resets, then
+W warm-up steps, then EXACTLY K timed steps (one HIP graph of the K launches) bracketed by a
+barrier + device sync on both sides, max over ranks.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  python -m torch.distributed.run --nproc-per-node 2 ... bench.py --gpus 2 --dry-run-cpu
+      (CI: the N > 1 control flow -- gloo process group, barriers, max over ranks, the flat
+       gather, the JSON line -- on CPU with a no-physics stand-in env; value meaningless)
 """
 import argparse
 import json
@@ -24,10 +33,14 @@ sys.path.insert(0, REPO)
 METRIC = "env steps/sec (whole node) at N parallel envs, Ant + Humanoid, 1/2/4/8 MI355X"  # BASELINE.json
 ENV_ID = "AntPyBulletEnv-v0"
 ENVS_PER_GPU = 16384
+ACTION_SEED = 0x5EED
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (non-matrix) peak
 SHORT = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
          "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
          "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d"}
+# BASELINE.json configs timed beside the headline (per-GPU env counts)
+EXTRA_LEGS = "HumanoidPyBulletEnv-v0:4096,HopperPyBulletEnv-v0:4096,HalfCheetahPyBulletEnv-v0:8192"
 
 
 def alg_bytes_per_env_step(info):
@@ -37,28 +50,52 @@ def alg_bytes_per_env_step(info):
     return 4 * (2 * S + info.action_dim + info.obs_dim + 2)
 
 
+def host_threads():
+    """Threads for the CPU leg: the CPUs this process may run on (sched_getaffinity), capped by
+    OMP_NUM_THREADS when the launcher sets it (the GPU box sets it to its CPU share, 16)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(avail, omp) if omp > 0 else avail), avail
+
+
 def cpu_baseline(seconds=12.0):
-    """The CPU oracle (float64 restatement of the same step) on the host's cores, on a
-    bounded sample: 4,096 Ant envs stepped until ~`seconds` of wall time."""
+    """The CPU oracle (float64 restatement of the same step, OpenMP over envs) on the host's
+    cores, on a bounded sample of the same workload: 4,096 Ant envs, Philox 0x5EED actions,
+    auto-reset on done or after 1,000 steps (reset noise from the host Philox mirror), stepped
+    until ~`seconds` of wall time."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    import pybulletgym_amd  # noqa: F401
+    from pybulletgym_amd import rng
+    threads, avail = host_threads()
     n = 4096
-    e = oracle.OracleEnvs(ENV_ID, n, nthreads=threads)
-    rng = np.random.default_rng(0)
-    e.reset(rng.uniform(-0.1, 0.1, (n, e.info.NR)))
-    acts = rng.uniform(-1, 1, (8, n, e.info.NA)).astype(np.float32)
-    e.step(acts[0])
-    steps = 0
+    e = oracle.OracleEnvs(ENV_ID, n, nthreads=threads, seed=ACTION_SEED)
+    ids = np.arange(n)
+    epi = np.zeros(n, np.int64)
+    obs = e.reset(rng.reset_noise(ACTION_SEED, ids, 0, e.info.NR).astype(np.float64))
+    acts = rng.sample_actions(e.info.NA, ids, np.arange(16), seed=ACTION_SEED)  # cycled (host Philox is slow)
+    steps = resets = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        e.step(acts[steps % 8])
+        obs, _, done, _ = e.step(acts[steps % 16])
         steps += 1
+        finished = done | (e.aux[:, 2] >= 1000)
+        if finished.any():
+            epi[finished] += 1
+            q = np.zeros((n, e.info.NR))
+            for k in np.flatnonzero(finished):
+                q[k] = rng.reset_noise(ACTION_SEED, [k], int(epi[k]), e.info.NR)[0]
+            e.reset(q, mask=finished, obs=obs)
+            resets += int(finished.sum())
     dt = time.perf_counter() - t0
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/pbg_oracle.cpp (float64) on {n} Ant envs x {steps} steps, "
-                      f"{threads} OpenMP threads, {dt:.1f} s; no auto-reset"}
+            "sample": f"oracle/pbg_oracle.cpp (float64) on {n} Ant envs x {steps} steps with auto-reset "
+                      f"({resets} resets), {threads} OpenMP threads of {avail} CPUs available "
+                      f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), {dt:.1f} s"}
 
 
 def load_pmc(env_id, n):
@@ -75,10 +112,20 @@ def load_pmc(env_id, n):
     return d if d.get("envs") == n else None
 
 
+def load_flops():
+    """Counted FP32 flops per env-step per robot (profiles/flops_per_env_step.json, written by
+    tools/count_flops.py from the op-counting build of the oracle)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "flops_per_env_step.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def valu_roofline(pmc, kernel_ms, n):
-    """VALU issue roofline (the binding one): wave64 VALU instructions per
-    launch (PMC SQ_INSTS_VALU) / the kernel's HIP-event time, against the chip's issue
-    peak: 256 CUs x 4 SIMDs x one wave64 VALU op per 2 cycles at 2.4 GHz."""
+    """VALU issue roofline: wave64 VALU instructions per launch (PMC SQ_INSTS_VALU) / the
+    kernel's HIP-event time, against the chip's issue peak: 256 CUs x 4 SIMDs x one wave64
+    VALU op per 2 cycles at 2.4 GHz."""
     peak = 256 * 4 * 2.4e9 / 2 / 1e12
     ach = pmc["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e12
     return {"achieved": ach, "peak": peak, "unit": "T wave-instr/s", "frac": ach / peak,
@@ -87,9 +134,8 @@ def valu_roofline(pmc, kernel_ms, n):
 
 
 def occupancy(env):
-    """Step-kernel occupancy (Humanoid row): lanes per env, workgroup, LDS per
-    workgroup, registers per lane; waves per SIMD = min(register limit, LDS limit, waves the
-    env count provides / (256 CUs x 4 SIMDs))."""
+    """Step-kernel occupancy: lanes per env, workgroup, LDS per workgroup, registers per lane;
+    waves per SIMD = min(register limit, LDS limit, waves the env count provides / 1024 SIMDs)."""
     i = env.info
     waves = -(-env.num_envs * i.lanes_per_env // 64)
     reg_limit = 512 // max(8 * -(-i.vgprs // 8), 1) if i.vgprs > 0 else 8
@@ -106,55 +152,97 @@ def kernel_name(env):
     return f"{k}<{env.env_id}>"
 
 
-def timed_rollout(VecEnv, env_id, n, steps, warmup, dev, rank, world, no_graph):
-    """Random-action rollout of n envs on this GPU: warmup steps, per-launch kernel time
-    (HIP events on the launch stream), then exactly `steps` steps bracketed by a barrier +
-    device sync on both sides; returns (env, elapsed_s max over ranks, kernel_ms, G)."""
+class DryRunEnv:
+    """--dry-run-cpu stand-in: VecEnv's buffers and call shape, no physics (CI of the N > 1
+    control flow only)."""
+
+    def __init__(self, env_id, n, device, seed, env_offset, autoreset):
+        import torch
+
+        class _I:  # pbg_info_t fields bench reads
+            floating, n_joints, action_dim, obs_dim, substeps = 1, 14, 8, 28, 4
+            lanes_per_env, block, lds_bytes, vgprs, scratch_bytes, lds_rows = 1, 64, 0, 0, 0, 0
+        self.info, self.env_id, self.num_envs = _I(), env_id, n
+        self.obs = torch.zeros((n, 28))
+        self.reward = torch.zeros(n)
+        self.done = torch.zeros(n, dtype=torch.uint8)
+
+    def reset(self):
+        return self.obs
+
+    def step(self, a):
+        self.obs[:, :8] = a
+        return self.obs
+
+    def close(self):
+        pass
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed_rollout(make_env, env_id, n, steps, warmup, preroll, dev, rank, world, no_graph):
+    """Rollout of n envs on this device: preroll + warmup untimed steps, then exactly `steps`
+    timed steps bracketed by a barrier + device sync on both sides.  Returns (env, elapsed_s
+    max over ranks, kernel_ms per launch, launches per graph)."""
     import torch
     import torch.distributed as dist
-    env = VecEnv(env_id, n, device=dev, seed=0x5EED, env_offset=rank * n, autoreset=True)
+    env = make_env(env_id, n, dev, ACTION_SEED, rank * n, True)
     env.reset()
     na = env.info.action_dim
-    total = warmup + steps
-    pool = min(total, 256)  # distinct pre-generated action batches, cycled
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    acts = torch.rand((pool, n, na), device=dev, generator=g, dtype=torch.float32) * 2 - 1
-
-    for i in range(warmup):
-        env.step(acts[i % pool])
-    stream = torch.cuda.current_stream(dev)
-    # timed region: the K steps as HIP-graph replays of G captured steps (G divides K)
-    G = 1
-    if not no_graph:
-        G = max(d for d in range(1, min(64, steps) + 1) if steps % d == 0)
-        graph = env.capture([acts[j % pool] for j in range(G)])
-    # per-launch kernel time (roofline.kernel_ms): HIP events on the launch stream around the
-    # timed region itself (graph replays are back-to-back kernels), so it describes the same
-    # launches as `value`; with --no-graph, events around each single launch
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)] \
-        if no_graph else None
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    if no_graph:
-        for i in range(steps):
-            ev[i][0].record(stream)
-            env.step(acts[(warmup + i) % pool])
-            ev[i][1].record(stream)
+    total = preroll + warmup + steps
+    if dev.type == "cuda":
+        from pybulletgym_amd.vec_env import sample_actions
+        # one distinct Philox batch per step, resident in HBM before the timed region
+        acts = sample_actions(na, n, total, seed=ACTION_SEED, step0=0, env_offset=rank * n, device=dev)
     else:
-        for _ in range(steps // G):
-            graph.replay()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
+        acts = torch.rand((total, n, na)) * 2 - 1
+    for i in range(preroll + warmup):
+        env.step(acts[i])
+    t_first = preroll + warmup
+    graph, G = None, 1
+    if dev.type == "cuda" and not no_graph:
+        # the timed steps as HIP-graph replays (G launches per graph, G divides K)
+        G = max(d for d in range(1, min(1000, steps) + 1) if steps % d == 0)
+        graphs = [env.capture([acts[t_first + r * G + j] for j in range(G)]) for r in range(steps // G)] \
+            if G < steps else [env.capture([acts[t_first + j] for j in range(G)])]
+    timing = dev.type == "cuda"
+    if timing:
+        stream = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)] \
+            if no_graph else None
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
+    t0 = time.perf_counter()
+    if timing:
+        e0.record(stream)
+    if dev.type == "cuda" and not no_graph:
+        for g in graphs:
+            g.replay()
+    else:
+        for i in range(steps):
+            if timing:
+                ev[i][0].record(stream)
+            env.step(acts[t_first + i])
+            if timing:
+                ev[i][1].record(stream)
+    if timing:
+        e1.record(stream)
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) if no_graph else e0.elapsed_time(e1)) / steps
+    if timing:
+        kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) if no_graph else e0.elapsed_time(e1)) / steps
+    else:
+        kernel_ms = elapsed / steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -162,20 +250,51 @@ def timed_rollout(VecEnv, env_id, n, steps, warmup, dev, rank, world, no_graph):
     return env, elapsed, kernel_ms, G
 
 
+def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
+    """value / roofline block of one workload (HBM line from the algorithmic bytes; FP32 line
+    from the counted flops when profiles/flops_per_env_step.json has the robot)."""
+    import torch
+    alg = alg_bytes_per_env_step(env.info)
+    achieved = alg * n / (kernel_ms * 1e-3) / 1e9
+    pmc = load_pmc(env.env_id, n)
+    d = {"env": env.env_id, "envs_per_gpu": n, "global_envs": world * n, "steps": steps,
+         "value": world * n * steps / elapsed, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
+         "kernel": kernel_name(env), "kernel_ms": kernel_ms, "occupancy": occupancy(env),
+         "obs_finite": bool(torch.isfinite(env.obs).all()),
+         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                      "kernel": kernel_name(env), "kernel_ms": kernel_ms, "alg_bytes_per_env_step": alg}}
+    f = flops.get(SHORT.get(env.env_id, env.env_id))
+    if f:
+        tf = f["flops_per_env_step"] * n / (kernel_ms * 1e-3) / 1e12
+        d["flop_roofline"] = {"bound": "valu-fp32", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": tf / FP32_PEAK_TFLOPS, "flops_per_env_step": f["flops_per_env_step"],
+                              "source": "profiles/flops_per_env_step.json (counted, tools/count_flops.py)"}
+    if pmc and pmc.get("valu_insts_per_launch"):
+        d["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--preroll", type=int, default=200, help="untimed steps before the warm-up (episode aging)")
     ap.add_argument("--envs-per-gpu", type=int, default=ENVS_PER_GPU)
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip timing the RCCL obs all-gather (timed separately, outside `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
-    ap.add_argument("--second-env", default="HumanoidPyBulletEnv-v0", help="second workload of the metric ('none' = off)")
-    ap.add_argument("--second-envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--legs", default=EXTRA_LEGS,
+                    help="extra workloads env:envs_per_gpu,... timed beside `value` ('none' = off)")
+    ap.add_argument("--second-env", default=None, help="(compat) 'none' disables the extra legs")
+    ap.add_argument("--leg-steps", type=int, default=200)
+    ap.add_argument("--dry-run-cpu", action="store_true", help="CI: N > 1 control flow on CPU/gloo, no physics")
     args = ap.parse_args()
+    if args.second_env == "none":
+        args.legs = "none"
 
     import torch
     import torch.distributed as dist
@@ -183,63 +302,57 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if args.dry_run_cpu:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        make_env = DryRunEnv
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
     import pybulletgym_amd  # noqa: F401
     from pybulletgym_amd.distributed import gather_flat
-    from pybulletgym_amd.vec_env import VecEnv
+    if not args.dry_run_cpu:
+        from pybulletgym_amd.vec_env import VecEnv
 
+        def make_env(env_id, n, dev, seed, env_offset, autoreset):
+            return VecEnv(env_id, n, device=dev, seed=seed, env_offset=env_offset, autoreset=autoreset)
+
+    flops = load_flops()
     n = args.envs_per_gpu
-    env, elapsed, kernel_ms, G = timed_rollout(VecEnv, args.env, n, args.steps, args.warmup, dev, rank, world,
-                                               args.no_graph)
-    second = None
-    if args.second_env not in ("", "none") and args.second_env != args.env:
-        # BASELINE metric names Ant + Humanoid: the Humanoid config (32,768 envs on 8 GPUs =
-        # 4,096 per GPU, BASELINE.json configs[4]) timed the same way, reported beside `value`
-        n2 = args.second_envs_per_gpu
-        steps2 = max(1, min(args.steps, 200))
-        env2, el2, km2, G2 = timed_rollout(VecEnv, args.second_env, n2, steps2, min(args.warmup, 20), dev, rank,
-                                           world, args.no_graph)
-        second = {"env": args.second_env, "envs_per_gpu": n2, "global_envs": world * n2, "steps": steps2,
-                  "value": world * n2 * steps2 / el2, "unit": "env-steps/s", "ms_per_step": el2 / steps2 * 1e3,
-                  "kernel": kernel_name(env2), "kernel_ms": km2, "lanes_per_env": env2.info.lanes_per_env,
-                  "occupancy": occupancy(env2),
-                  "obs_finite": bool(torch.isfinite(env2.obs).all())}
-        alg2 = alg_bytes_per_env_step(env2.info)
-        ach2 = alg2 * n2 / (km2 * 1e-3) / 1e9
-        pmc2 = load_pmc(args.second_env, n2)
-        second["roofline"] = {"bound": "hbm", "achieved": ach2, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": ach2 / HBM_PEAK_GBS, "traffic": pmc2.get("hbm_bytes_per_launch") if pmc2 else None,
-                              "alg_bytes_per_env_step": alg2}
-        if pmc2 and pmc2.get("valu_insts_per_launch"):
-            second["valu_roofline"] = valu_roofline(pmc2, km2, n2)
-        env2.close()
+    env, elapsed, kernel_ms, G = timed_rollout(make_env, args.env, n, args.steps, args.warmup, args.preroll, dev,
+                                               rank, world, args.no_graph)
+    head = leg_summary(env, world, n, args.steps, elapsed, kernel_ms, flops)
 
     gather_ms = None
     if not args.no_gather and world > 1:
         for _ in range(3):
             gather_flat(env.obs)
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         t1 = time.perf_counter()
         for _ in range(20):
             gather_flat(env.obs)
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         gather_ms = (time.perf_counter() - t1) / 20 * 1e3
 
-    finite = bool(torch.isfinite(env.obs).all())
+    legs = {}
+    if args.legs not in ("", "none"):
+        for spec in args.legs.split(","):
+            eid, cnt = spec.split(":")
+            if eid == args.env:
+                continue
+            e2, el2, km2, _ = timed_rollout(make_env, eid, int(cnt), args.leg_steps, min(args.warmup, 20),
+                                            args.preroll, dev, rank, world, args.no_graph)
+            legs[SHORT.get(eid, eid)] = leg_summary(e2, world, int(cnt), args.leg_steps, el2, km2, flops)
+            e2.close()
+
     if rank == 0:
-        steps_total = world * n * args.steps
-        value = steps_total / elapsed
-        alg = alg_bytes_per_env_step(env.info)
-        achieved = alg * n / (kernel_ms * 1e-3) / 1e9
-        pmc = load_pmc(args.env, n)
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
         out = {
             "metric": METRIC,
-            "value": value,
+            "value": head["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -249,29 +362,31 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: U(-1,1) float32 actions pre-generated in HBM; robot compiled from the reference MJCF",
+            "data": "synthetic: Philox4x32-10 U(-1,1) float32 actions (key 0x5EED, counter (step, global env)) "
+                    "generated in HBM before the timed region; robot compiled from the reference MJCF",
             "config": {"workload": f"{args.env} random-action rollout, auto-reset (TimeLimit 1000)",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps": env.info.substeps,
                        "solver_iterations": 5, "parallelism": f"env-sharded x{world}, no per-step collective",
-                       "launch": "host loop" if args.no_graph else f"hipGraph replay of {G} captured steps",
+                       "preroll_steps": args.preroll,
+                       "launch": "host loop" if args.no_graph or args.dry_run_cpu else
+                       f"hipGraph replay, {G} captured launches per graph",
                        "lanes_per_env": env.info.lanes_per_env},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel_name(env), "kernel_ms": kernel_ms,
-                         "alg_bytes_per_env_step": alg},
-            "obs_finite": finite,
-            "occupancy": occupancy(env),
+            "roofline": head["roofline"],
+            "obs_finite": head["obs_finite"],
+            "occupancy": head["occupancy"],
         }
-        if pmc and pmc.get("valu_insts_per_launch"):
-            out["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)
-        if second is not None:
-            out["humanoid" if "Humanoid" in second["env"] else "second"] = second
+        for k in ("flop_roofline", "valu_roofline"):
+            if k in head:
+                out[k] = head[k]
+        out.update(legs)
         if gather_ms is not None:
             # the learner's optional flat batch: one all_gather_into_tensor of
-            # [envs_per_gpu, obs_dim] float32 per rank over RCCL, timed after the rollout
+            # [envs_per_gpu, obs_dim] float32 per rank, timed after the rollout
             out["allgather_obs_ms"] = gather_ms
             out["allgather_obs_bytes"] = world * n * env.info.obs_dim * 4
-        if world == 1 and not args.no_cpu_baseline:
+        if args.dry_run_cpu:
+            out["dry_run"] = "cpu/gloo stand-in env: control-flow check only, value is not a measurement"
+        if world == 1 and not args.no_cpu_baseline and not args.dry_run_cpu:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -34,7 +34,10 @@ extern "C" {
 typedef struct pbg_handle pbg_handle;
 
 typedef struct {
-  int robot_id;          /* 0 pendulum, 1 hopper, 2 halfcheetah, 3 ant, 4 humanoid */
+  int robot_id;          /* 0 pendulum, 1 hopper, 2 halfcheetah, 3 ant, 4 humanoid, 5 walker2d,
+                            6 pendulum_swingup, 7 double_pendulum, 8 humanoid_flagrun,
+                            9 hopper_mujoco, 10 walker2d_mujoco, 11 halfcheetah_mujoco,
+                            12 ant_mujoco, 13 humanoid_mujoco, 14 double_pendulum_mujoco */
   int n_envs;
   int action_dim;        /* action_space.shape[0]   (robot_bases.py:24-25) */
   int obs_dim;           /* observation_space.shape[0] (robot_bases.py:26-27) */
@@ -66,14 +69,39 @@ typedef struct {
   float* term_obs;    /* nullable [n, obs_dim] observation before an auto-reset */
   int32_t* ncontact;  /* nullable [n] contact points in the last sub-step */
   int autoreset;      /* reset envs that finished, inside the same launch */
+  double* rew_terms;  /* nullable [n, 5] float64: the terms the reward sums, in the order of the
+                         reference's self.rewards list, zero-padded -- walkers: alive, progress,
+                         electricity, joints_at_limit, feet_collision (gym_locomotion_envs.py:99-105);
+                         MuJoCo Ant/Humanoid: alive, progress, joints_at_limit, feet_collision
+                         (mujoco/gym_locomotion_envs.py:98-103); MuJoCo planar: potential,
+                         [alive,] power_cost; pendulums: their rewards list */
+  uint32_t* csig;     /* nullable [n] contact-set signature of the env step: the sum mod 2^32 of
+                         fmix32((substep << 16) + candidate + 0x9E3779B9) over every active collision
+                         candidate (floor slots 0..NS-1, self pairs NS + p) of every sub-step
+                         (sim_params.h pbg_contact_hash; for parity tests) */
 } pbg_step_io_t;
+
+/* Test / diagnostic launch options (pbg_create_debug).  -1 = the default everywhere. */
+typedef struct {
+  int kernel;     /* 0: one-lane-per-env kernel for every robot; 2: the 16-lane gang kernel for
+                     every walker (Ant included); -1 / 1: default (quad for Ant, gang otherwise) */
+  int lds_rows;   /* k >= 0: at most k contact rows (gang: contacts) per env resident in LDS,
+                     the rest in the device workspace (bitwise-equality tests of that path) */
+  int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics */
+} pbg_debug_opts_t;
 
 /* gym.make(env_id) for n envs (envs/__init__.py:4-103 registry entries; the env's
  * physics client is created here instead of lazily in BaseBulletEnv._reset,
- * env_bases.py:46-56).  env_id: "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0",
- * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "InvertedPendulumPyBulletEnv-v0",
- * "Walker2DPyBulletEnv-v0". */
+ * env_bases.py:46-56).  env_id (robot_id order): "InvertedPendulumPyBulletEnv-v0",
+ * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "AntPyBulletEnv-v0",
+ * "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "InvertedPendulumSwingupPyBulletEnv-v0",
+ * "InvertedDoublePendulumPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0",
+ * "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0",
+ * "InvertedDoublePendulumMuJoCoEnv-v0" (the short robot names are accepted too). */
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out);
+/* pbg_create with test / diagnostic launch options (opts NULL = pbg_create). */
+int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                     const pbg_debug_opts_t* opts, pbg_handle** out);
 /* BaseBulletEnv._close (env_bases.py:103-107) */
 void pbg_destroy(pbg_handle* h);
 /* action_space / observation_space / model sizes (robot_bases.py:24-27) */
@@ -94,11 +122,12 @@ int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* d
 int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
 
 /* pybullet saveState/restoreState (gym_locomotion_envs.py:25,36) generalised to trace
- * replay / teacher forcing.  phys: [n, state_words] float64 records
+ * replay / teacher forcing / checkpoints.  phys: [n, state_words] float64 records
  *   [0..2] base COM pos, [3..6] base quat (x,y,z,w), [7..9] base COM lin vel (world),
  *   [10..12] base ang vel (world), then q[n_joints], qd[n_joints];
  * aux: [n, aux_words] float64 = [potential, initial_z, elapsed_steps, floor_in_parts,
- *   feet_contact[n_feet]]  (aux may be NULL in set_state). */
+ *   feet_contact[n_feet], (HumanoidFlagrun: walk target x, y, flag_timeout, flag draws),
+ *   episodes started (the reset-noise RNG counter)]  (aux may be NULL in set_state). */
 int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream);
 int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream);
 
@@ -106,6 +135,13 @@ int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* st
  * explicit inputs, for golden-vector parity; layouts in pbg_pack_record_sizes. */
 int pbg_pack_record_sizes(const char* env_id, int* in_words, int* out_words);
 int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, void* stream);
+
+/* Batched action_space.sample() (robot_bases.py:24-25 Box(-1, 1)): out[s, e, i] = U(-1, 1)
+ * float32 for s < n_steps, e < n_envs, i < action_dim; Philox4x32-10, key = seed, counter =
+ * (step0 + s, env_offset + e, i / 4, 0xAC7) -- the bench's random-action protocol
+ * (BASELINE.md section 2), independent of the sharding.  out: device [n_steps, n_envs, action_dim]. */
+int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, uint32_t step0, int env_offset,
+                       float* out, void* stream);
 
 const char* pbg_last_error(void);
 

@@ -43,7 +43,12 @@ def lib():
         P = ctypes.c_void_p
         L.pbg_oracle_info.argtypes = [ctypes.c_int, P]
         L.pbg_oracle_reset.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
-        L.pbg_oracle_step.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int]
+        L.pbg_oracle_reset_mask.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P]
+        L.pbg_oracle_step.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P]
+        L.pbg_oracle_step_ex.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P,
+                                         ctypes.c_int]
+        L.pbg_oracle_count_flops.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
+        L.pbg_oracle_set_physics.argtypes = [P, ctypes.c_int]
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
         L.pbg_oracle_pack_flag.argtypes = [ctypes.c_int, P, P, P, P]
         L.pbg_oracle_set_rng.argtypes = [ctypes.c_uint64, ctypes.c_int]
@@ -75,8 +80,10 @@ class Info:
 class OracleEnvs:
     """Batch of n envs stepped by the CPU oracle (float64 physics)."""
 
-    def __init__(self, name: str, n: int, nthreads: int = 1, seed: int = 0, env_offset: int = 0):
-        """seed / env_offset key the Philox draws of HumanoidFlagrun's flag (as the kernels')."""
+    def __init__(self, name: str, n: int, nthreads: int = 1, seed: int = 0, env_offset: int = 0, precision: int = 64):
+        """seed / env_offset key the Philox draws of HumanoidFlagrun's flag (as the kernels').
+        precision 32: the physics in IEEE float32 (the conditioning probe of the parity tests)."""
+        self.precision = precision
         lib().pbg_oracle_set_rng(seed, env_offset)
         self.rid = robot_id(name)
         self.info = Info(self.rid)
@@ -84,11 +91,17 @@ class OracleEnvs:
         self.nthreads = nthreads
         self.state = np.zeros((n, self.info.SD), dtype=np.float64)
         self.aux = np.zeros((n, self.info.AD), dtype=np.float64)
+        self.csig = np.zeros(n, dtype=np.uint32)      # last step's contact-set signatures
+        self.terms = np.zeros((n, 5), dtype=np.float64)  # last step's reward terms
 
-    def reset(self, qinit: np.ndarray) -> np.ndarray:
+    def reset(self, qinit: np.ndarray, mask: np.ndarray = None, obs: np.ndarray = None) -> np.ndarray:
+        """Reset all envs (or those with mask != 0, writing their rows of `obs`)."""
         qinit = np.ascontiguousarray(qinit, dtype=np.float64).reshape(self.n, self.info.NR)
-        obs = np.zeros((self.n, self.info.OBS), dtype=np.float32)
-        assert lib().pbg_oracle_reset(self.rid, self.n, _p(self.state), _p(self.aux), _p(qinit), _p(obs)) == 0
+        if obs is None:
+            obs = np.zeros((self.n, self.info.OBS), dtype=np.float32)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        assert lib().pbg_oracle_reset_mask(self.rid, self.n, _p(self.state), _p(self.aux), _p(qinit), _p(obs),
+                                           _p(m)) == 0
         return obs
 
     def step(self, act: np.ndarray):
@@ -97,8 +110,9 @@ class OracleEnvs:
         rew = np.zeros(self.n, dtype=np.float64)
         done = np.zeros(self.n, dtype=np.uint8)
         nc = np.zeros(self.n, dtype=np.int32)
-        assert lib().pbg_oracle_step(self.rid, self.n, _p(self.state), _p(self.aux), _p(act), _p(obs),
-                                     _p(rew), _p(done), _p(nc), self.nthreads) == 0
+        assert lib().pbg_oracle_step_ex(self.rid, self.n, _p(self.state), _p(self.aux), _p(act), _p(obs),
+                                        _p(rew), _p(done), _p(nc), self.nthreads, _p(self.csig), _p(self.terms),
+                                        self.precision) == 0
         return obs, rew, done.astype(bool), nc
 
 

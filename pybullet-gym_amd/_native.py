@@ -33,7 +33,13 @@ class Info(ctypes.Structure):
 class StepIO(ctypes.Structure):
     _fields_ = [("act", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("rew", ctypes.c_void_p),
                 ("done", ctypes.c_void_p), ("rew64", ctypes.c_void_p), ("trunc", ctypes.c_void_p),
-                ("term_obs", ctypes.c_void_p), ("ncontact", ctypes.c_void_p), ("autoreset", ctypes.c_int)]
+                ("term_obs", ctypes.c_void_p), ("ncontact", ctypes.c_void_p), ("autoreset", ctypes.c_int),
+                ("rew_terms", ctypes.c_void_p), ("csig", ctypes.c_void_p)]
+
+
+class DebugOpts(ctypes.Structure):
+    """pbg_debug_opts_t: test / diagnostic launch options (-1 = default)."""
+    _fields_ = [("kernel", ctypes.c_int), ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int)]
 
 
 _lib = None
@@ -51,6 +57,9 @@ def lib():
     P, I, H = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
     L.pbg_create.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(H)]
     L.pbg_create.restype = I
+    L.pbg_create_debug.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(DebugOpts),
+                                   ctypes.POINTER(H)]
+    L.pbg_sample_actions.argtypes = [I, I, I, ctypes.c_uint64, ctypes.c_uint32, I, P, P]
     L.pbg_destroy.argtypes = [H]
     L.pbg_destroy.restype = None
     L.pbg_info.argtypes = [H, ctypes.POINTER(Info)]
@@ -63,14 +72,15 @@ def lib():
     L.pbg_pack.argtypes = [ctypes.c_char_p, I, P, P, P]
     L.pbg_last_error.restype = ctypes.c_char_p
     for f in ("pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state", "pbg_set_state",
-              "pbg_pack_record_sizes", "pbg_pack"):
+              "pbg_pack_record_sizes", "pbg_pack", "pbg_create_debug", "pbg_sample_actions"):
         getattr(L, f).restype = I
     _lib = L
     return L
 
 
-EXPORTED = ("pbg_create", "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state",
-            "pbg_set_state", "pbg_pack_record_sizes", "pbg_pack", "pbg_last_error")
+EXPORTED = ("pbg_create", "pbg_create_debug", "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex",
+            "pbg_get_state", "pbg_set_state", "pbg_pack_record_sizes", "pbg_pack", "pbg_sample_actions",
+            "pbg_last_error")
 
 
 def check(rc: int, what: str):

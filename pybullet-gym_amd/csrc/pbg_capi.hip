@@ -11,6 +11,7 @@
 #include "models_gen.h"
 #include "pbg_launch.h"
 #include "pbg_records.h"
+#include "pbg_math.h"
 #include "pbg_types.h"
 #include "sim_params.h"
 
@@ -113,6 +114,11 @@ extern "C" {
 const char* pbg_last_error(void) { return g_err; }
 
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out) {
+  return pbg_create_debug(env_id, n_envs, device, seed, env_offset, nullptr, out);
+}
+
+int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                     const pbg_debug_opts_t* opts, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
   *out = nullptr;
   const int rid = env_robot_id(env_id);
@@ -138,14 +144,13 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
   const size_t n = (size_t)n_envs;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  // PBG_TEAM=0 selects the one-lane-per-env kernel for every robot, PBG_TEAM=2 the gang
-  // kernel for every walker (Ant included); default: quad for Ant, gang for the others
-  const char* team_env = getenv("PBG_TEAM");
-  const int mode = (team_env && team_env[0] == '0') ? 0 : ((team_env && team_env[0] == '2') ? 2 : 1);
+  // kernel variant: 1 = default (quad for Ant, gang for the other walkers), 0 = the
+  // one-lane-per-env kernel for every robot, 2 = the gang kernel for every walker
+  const int mode = (opts && (opts->kernel == 0 || opts->kernel == 2)) ? opts->kernel : 1;
+  h->geo.force_dist = opts ? opts->gang_dist : -1;
   int e = hip_check(o->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
-  // PBG_LDS_ROWS=k caps the LDS-resident contact rows (tests of the workspace path)
-  const char* rows_env = getenv("PBG_LDS_ROWS");
-  if (rows_env && atoi(rows_env) >= 0 && atoi(rows_env) < h->geo.lds_rows) h->geo.lds_rows = atoi(rows_env);
+  // cap on the LDS-resident contact rows (tests of the device-workspace path)
+  if (opts && opts->lds_rows >= 0 && opts->lds_rows < h->geo.lds_rows) h->geo.lds_rows = opts->lds_rows;
   e |= hip_check(hipMalloc(&B.st, sizeof(float) * n * h->info.state_words), "hipMalloc state");
   e |= hip_check(hipMalloc(&B.pot, sizeof(double) * n), "hipMalloc potential");
   e |= hip_check(hipMalloc(&B.z0, sizeof(float) * n), "hipMalloc z0");
@@ -206,7 +211,8 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
   if (!h || !io || !io->act || !io->obs || !io->rew || !io->done)
     return fail(PBG_E_ARG, "pbg_step: NULL handle or required buffer%s%ld");
   DeviceGuard dg(h->device);
-  pbg::StepIO s{io->act, io->obs, io->rew, io->rew64, io->done, io->trunc, io->term_obs, io->ncontact, io->autoreset};
+  pbg::StepIO s{io->act, io->obs, io->rew, io->rew64, io->done, io->trunc, io->term_obs, io->ncontact, io->autoreset,
+                io->rew_terms, io->csig};
   return hip_check(h->ops->step(h->B, s, h->scratch, h->geo, (hipStream_t)stream), "step_kernel launch");
 }
 
@@ -254,6 +260,35 @@ int pbg_debug_stamps(int rid, unsigned long long* host_out) {
   return PBG_E_ENV;
 }
 #endif
+
+// Batched action_space.sample(): out[s][e][i] = U(-1, 1) float32, Philox4x32-10 keyed by the
+// seed, counter (step0 + s, env_offset + e, 4-wide block of i, 0xAC7), u = (r >> 8) / 2^24.
+__global__ __launch_bounds__(256) void sample_actions_kernel(int na, int n, int steps, uint32_t k0, uint32_t k1,
+                                                             uint32_t step0, int env_offset, float* __restrict__ out) {
+  const int nb = (na + 3) / 4;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one (step, env, block) per lane
+  if (idx >= (long)steps * n * nb) return;
+  const int blk = (int)(idx % nb);
+  const long se = idx / nb;
+  const int e = (int)(se % n), st = (int)(se / n);
+  u4 ctr = {step0 + (uint32_t)st, (uint32_t)(env_offset + e), (uint32_t)blk, 0xAC7u};
+  const u4 r = philox4x32_10(ctr, k0, k1);
+  const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+  float* o = out + ((size_t)st * n + e) * na;
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+    if (4 * blk + t < na) o[4 * blk + t] = fmaf(2.f, u01(rr[t]), -1.f);
+}
+
+int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, uint32_t step0, int env_offset,
+                       float* out, void* stream) {
+  if (action_dim <= 0 || n_envs <= 0 || n_steps <= 0 || !out)
+    return fail(PBG_E_ARG, "pbg_sample_actions: bad arguments%s%ld");
+  const long lanes = (long)n_steps * n_envs * ((action_dim + 3) / 4);
+  hipLaunchKernelGGL(sample_actions_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     action_dim, n_envs, n_steps, (uint32_t)seed, (uint32_t)(seed >> 32), step0, env_offset, out);
+  return hip_check((int)hipGetLastError(), "sample_actions launch");
+}
 
 int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, void* stream) {
   const int rid = env_robot_id(env_id);

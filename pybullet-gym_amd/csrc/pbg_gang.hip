@@ -52,6 +52,19 @@ PBG_DEV float gang_sum(float x) {
   return x;
 }
 PBG_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
+template <int CTRL>
+PBG_DEV uint32_t dpp_u(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+// integer sum over the T lanes of a DPP row segment (mod 2^32), same in every lane
+template <int T>
+PBG_DEV uint32_t gang_sum_u32(uint32_t x) {
+  x += dpp_u<0xB1>(x);
+  x += dpp_u<0x4E>(x);
+  if constexpr (T >= 8) x += dpp_u<0x141>(x);
+  if constexpr (T >= 16) x += dpp_u<0x140>(x);
+  return x;
+}
 
 // ------------------------------------------------------------------ constant tables
 template <class R>
@@ -510,7 +523,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
 
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int T, bool DIST>
-PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits SUB_STAMP_ARGS) {
+PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits, uint32_t sub,
+                         uint32_t& csig SUB_STAMP_ARGS) {
   using D = Dims<R>;
   using G = Gang<R, T>;
   auto& TB = GangTabs<R>::tab(X.tabs);
@@ -612,6 +626,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     const uint64_t mine = bal & gang_mask;
     sb |= (mine >> (X.le * T)) << (r * T);
     if (act) {
+      csig += pbg_contact_hash(sub, (uint32_t)sl);  // this lane's share of the signature
       const int c = nc + __popcll(bal & gang_mask & below);
       const f3 P = mk3(cc.x, cc.y, cc.z - rad);
       put_desc(c, P - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[TB.slot_body[sl]], 0u, 1.f, TB.slot_mu[sl]);
@@ -670,6 +685,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       }
       const uint64_t bal = __ballot(act);
       if (act) {
+        csig += pbg_contact_hash(sub, (uint32_t)(R::NS + pp));
         const int c = nc + __popcll(bal & gang_mask & below);
         put_desc(c, PA - O, PB - O, nrm, dist, 1.f, TB.chain[TB.geom_body[ga]], TB.chain[TB.geom_body[gb]], 0.f, TB.pmu[pp]);
       }
@@ -728,7 +744,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     }
     // y = L^-1 J (forward substitution over the compile-time pattern of L)
     float y[N];
-    float D2 = 0.f, vJ = 0.f;
+    float D2 = 0.f;
 #pragma unroll
     for (int i = 0; i < N; i++) {
       float tt = J[i];
@@ -737,7 +753,6 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         if (D::coupled(i, kk)) tt -= X.l[G::O_L + D::lidx(i, kk)] * y[kk];
       y[i] = tt * X.l[G::O_LD + i];
       D2 += y[i] * y[i];
-      vJ += y[i] * X.l[G::O_U + i];
     }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
     if (is_lim) {
@@ -746,15 +761,15 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
       const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
       p[YS] = meff;
-      p[YS + 1] = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
-      p[YS + 2] = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
+      p[YS + 1] = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
+      p[YS + 2] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
     } else {
       const int w0r = G::DW + 1 + dir * G::CRW;
 #pragma unroll
       for (int i = 0; i < YS; i++) cput<R, T>(X, c, w0r + i, i < N ? y[i] : 0.f);
       cput<R, T>(X, c, w0r + YS, meff);
       cput<R, T>(X, c, w0r + YS + 1,
-                 dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+                 dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
       cput<R, T>(X, c, w0r + YS + 2, 0.f);
     }
   }
@@ -907,9 +922,15 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   }
   uint64_t slot_bits = 0;
   int nc = 0;
+  uint32_t csig = 0;  // per-lane share; gang-summed below
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits SUB_STAMP_PASS);
+  for (int sub = 0; sub < R::substeps; sub++)
+    nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits, (uint32_t)sub, csig SUB_STAMP_PASS);
   if (io.ncontact && w0) io.ncontact[e] = nc;
+  if (io.csig) {
+    const uint32_t sig = gang_sum_u32<T>(csig);
+    if (w0) io.csig[e] = sig;
+  }
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   float obs[R::OBS];
@@ -948,6 +969,10 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   if (w0) {
     io.rew[e] = (float)po.reward;
     if (io.rew64) io.rew64[e] = po.reward;
+    if (io.rew_terms) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) io.rew_terms[(size_t)e * 5 + i] = po.terms[i];
+    }
     io.done[e] = term || trunc;
     if (io.trunc) io.trunc[e] = trunc && !term;
   }

@@ -18,6 +18,7 @@ struct Geometry {
   int lds_rows;      // contact-constraint rows (gang: contacts) resident in LDS per env
   int env_words;     // gang: LDS words per env
   int gang_dist;     // gang: distributed (1) or replicated (0) unconstrained dynamics
+  int force_dist;    // in: -1 = plan's choice, 0 / 1 = force gang_dist (pbg_create_debug)
   size_t lds_bytes;  // dynamic LDS per step workgroup
   size_t scratch_words_per_env;
   int vgprs;          // the selected step kernel's registers per lane (hipFuncGetAttributes)

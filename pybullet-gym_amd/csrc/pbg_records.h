@@ -19,6 +19,6 @@ struct PackRec {
 template <class R>
 struct Records {
   static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;                       // physical state words
-  static constexpr int AD = PBG_AUX_WORDS + R::NF + (R::flagrun ? 4 : 0);     // bookkeeping words
+  static constexpr int AD = PBG_AUX_RECORD_WORDS(R::NF, R::flagrun);        // bookkeeping words
 };
 }  // namespace pbg

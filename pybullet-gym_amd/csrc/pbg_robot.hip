@@ -1,7 +1,6 @@
 // pbg_robot.hip -- per-robot kernel instantiations + launchers.  Compiled once per robot
 // with -DPBG_ROBOT=<Pendulum|Hopper|HalfCheetah|Ant|Humanoid>.
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 
 #include "pbg_launch.h"
 #include "pbg_step.hip"
@@ -87,16 +86,17 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     constexpr int EPB = PBG_GANG_BLOCK / 16;  // envs per workgroup
     const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
-    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1) - sizeof(float) * GangTabs<RR>::WORDS;
-    long words = (long)(budget / ((size_t)EPB * sizeof(float))) - G::FIXED;
+    // signed: with many workgroups per CU the share can be smaller than the model tables
+    long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - (long)sizeof(float) * (long)GangTabs<RR>::WORDS;
+    if (budget < 0) budget = 0;
+    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED;
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
     // distributed dynamics for deep trees (Humanoid) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
     g->gang_dist = RR::NDOF >= 16 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
-    const char* dist_env = getenv("PBG_GANG_DIST");  // tests: force either variant
-    if (dist_env && (dist_env[0] == '0' || dist_env[0] == '1')) g->gang_dist = dist_env[0] == '1';
+    if (g->force_dist == 0 || g->force_dist == 1) g->gang_dist = g->force_dist;  // pbg_create_debug
     g->team = 16;
     g->block = PBG_GANG_BLOCK;
     g->lds_rows = cap;

@@ -416,6 +416,13 @@ struct Rows {
 };
 
 // ------------------------------------------------------------------ one physics sub-step
+// Target of J nu_new for a positional row (contact normal, joint limit), Bullet's rhs
+// (btMultiBodyConstraintSolver::setupMultiBodyContactConstraint; velocityError = -rel_vel,
+// minus pos/dt when separated, positionalError = -erp pos/dt when penetrating) in absolute form:
+// a separated row admits an approach of at most pos/dt (speculative contact), a penetrating
+// one pushes out at erp * pos / dt.  Continuous at pos = 0.
+PBG_DEV float pos_target(float pos, float erp, float inv_dt) { return -(pos > 0.f ? 1.f : erp) * inv_dt * pos; }
+
 // tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
 // of this sub-step's collision pass (feet contacts come from the last sub-step).
 // dof motion vectors (angular, linear-at-O) in generalized order
@@ -744,7 +751,8 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
 }
 
 template <class R, int LS>
-PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw SUB_STAMP_ARGS) {
+PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw, uint32_t sub,
+                    uint32_t& csig SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
   constexpr float dt = (float)R::dt_sub;
@@ -770,14 +778,14 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         if (D::coupled(i, kk) && D::coupled(kk, gd)) t -= L[D::lidx(i, kk)] * y[kk];
       y[i] = t * Ld[i];
     }
-    float D2 = 0.f, vJ = 0.f;
+    float D2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
+    for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
     // lower row J = +e_d (pos = q - lo), upper row J = -e_d (pos = hi - q)
     const float plo = s.q[d] - (float)R::dof_lower[d], phi = (float)R::dof_upper[d] - s.q[d];
-    const float tlo = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
-    const float thi = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
+    const float tlo = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
+    const float thi = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
 #pragma unroll
     for (int i = 0; i < N; i++)
       if (D::LIMPOS.v[li][i] >= 0) rw.lim(off + D::LIMPOS.v[li][i]) = y[i];
@@ -807,6 +815,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     const bool act = dist < (float)PBG_CONTACT_THRESHOLD;
     slot_active[sl] = act;
     if (!act) return;
+    csig += pbg_contact_hash(sub, (uint32_t)sl);
     const f3 P = mk3(cc.x, cc.y, cc.z - rad);
     const f3 rP = P - O;
     const int lnk = R::slot_link[sl];
@@ -828,11 +837,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
           if (D::coupled(i, kk) && D::in_chain(kk, lnk)) t -= L[D::lidx(i, kk)] * y[kk];
         y[i] = t * Ld[i];
       }
-      float D2 = 0.f, vJ = 0.f;
+      float D2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; vJ += y[i] * u[i]; }
+      for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
       rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
@@ -878,6 +887,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       const float ra = (float)R::geom_r[ga], rb = (float)R::geom_r[gb];
       const float dist = dd - ra - rb;
       if (!(dist < (float)PBG_CONTACT_THRESHOLD)) continue;
+      csig += pbg_contact_hash(sub, (uint32_t)(R::NS + pp));
       const f3 nrm = dd > 1e-9f ? fast_rcp(dd) * dv : mk3(0, 0, 1);
       const f3 PA = ca - ra * nrm, PB = cb + rb * nrm;
       f3 t1, t2;  // btPlaneSpace1(nrm)
@@ -897,7 +907,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
         const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
         float y[N];
-        float D2 = 0.f, vJ = 0.f;
+        float D2 = 0.f;
 #pragma unroll
         for (int i = 0; i < N; i++) {
           const int di = D::dof_of(i);
@@ -910,10 +920,10 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
             if (D::coupled(i, kk)) t -= L[D::lidx(i, kk)] * y[kk];
           y[i] = t * Ld[i];
           D2 += y[i] * y[i];
-          vJ += y[i] * u[i];
+         
         }
         rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-               dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+               dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;
@@ -1026,6 +1036,7 @@ struct PackIn {
 };
 struct PackOut {
   double reward, potential, initial_z, dist;  // dist: walk_target_dist
+  double terms[5];  // the reference's self.rewards list (the terms `reward` sums), zero-padded
   double pitch;                               // body_rpy[1]
   int at_limit;                               // joints_at_limit
   uint32_t feet_out;  // bitmask
@@ -1098,6 +1109,8 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
 #pragma unroll
   for (int i = 0; i < R::NF; i++) fb |= (in.feet_prev[i] != 0.f ? 1u : 0u) << i;
   out.feet_out = fb;
+#pragma unroll
+  for (int i = 0; i < 5; i++) out.terms[i] = 0.0;
   if (!act) { out.reward = 0.0; out.done = false; return; }
   const float s0 = obs[0];
   double alive;
@@ -1128,6 +1141,8 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   elec += R::stall_torque_cost * (double)mean_s;
   const double jal = R::joints_at_limit_cost * (double)at_limit;
   out.reward = ((((0.0 + alive) + progress) + elec) + jal) + 0.0;
+  // gym_locomotion_envs.py:99-105 [alive, progress, electricity, joints_at_limit, feet_collision]
+  out.terms[0] = alive; out.terms[1] = progress; out.terms[2] = elec; out.terms[3] = jal;
 }
 
 // HumanoidFlagrun walk target (robot_locomotors.py:195-226).
@@ -1197,6 +1212,8 @@ PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_af
     obs[o++] = c > 0.f ? (v < -c ? -c : (v > c ? c : v)) : v;  // np.clip keeps NaN
   }
   out.potential = x_after; out.initial_z = 0.0; out.dist = 0.0; out.feet_out = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) out.terms[i] = 0.0;
   if (!act) { out.reward = 0.0; out.done = false; return; }
   const double potential = (x_after - x_before) / (R::dt_sub * R::substeps);
   float sq[R::NA];
@@ -1210,11 +1227,13 @@ PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_af
     if (i >= 2) small &= fabsf(obs[i]) < 100.f;
   }
   const float height = obs[0], ang = obs[1];
-  if constexpr (R::alive == 12) {  // HalfCheetah: never done
+  if constexpr (R::alive == 12) {  // HalfCheetah: never done; rewards [potential, power_cost]
     out.reward = (0.0 + potential) + (double)power_cost;
     out.done = false;
-  } else {
+    out.terms[0] = potential; out.terms[1] = (double)power_cost;
+  } else {  // rewards [potential, alive_bonus, power_cost] (mujoco gym_locomotion_envs.py:150-154)
     out.reward = ((0.0 + potential) + 1.0) + (double)power_cost;
+    out.terms[0] = potential; out.terms[1] = 1.0; out.terms[2] = (double)power_cost;
     if constexpr (R::alive == 10)  // Hopper
       out.done = !(finite && small && height > -0.3f && fabsf(ang) < 0.2f);
     else  // Walker2D
@@ -1268,6 +1287,8 @@ PBG_DEV void mujoco3d_pack(const PackIn<R>& in, const float* act, float* obs, Pa
   const double progress = out.potential - in.potential_old;
   const double jal = -0.1 * (double)out.at_limit;
   out.reward = (((0.0 + alive) + progress) + jal) + 0.0;
+  // mujoco gym_locomotion_envs.py:98-103 [alive, progress, joints_at_limit, feet_collision]
+  out.terms[0] = alive; out.terms[1] = progress; out.terms[2] = jal; out.terms[3] = 0.0; out.terms[4] = 0.0;
 }
 
 // Pendulum packs (obs float64 in the reference, float32 through the C-ABI).
@@ -1277,6 +1298,8 @@ PBG_DEV void mujoco3d_pack(const PackIn<R>& in, const float* act, float* obs, Pa
 template <class R>
 PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip, float* obs, PackOut& out) {
   out.potential = 0.0; out.initial_z = 0.0; out.feet_out = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) out.terms[i] = 0.0;
   if constexpr (R::alive == 7) {
     // InvertedDoublePendulumMuJoCo: mujoco/robot_pendula.py:75-89 obs [x, sin th, sin g, cos th,
     // cos g, clip(vx, th', g', +-10), qfrc_constraint zeros (3)]; mujoco/gym_pendulum_envs.py:60-72
@@ -1290,6 +1313,7 @@ PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip
     const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
     const double vel_penalty = 1e-3 * (thd * thd) + 5e-3 * (gd * gd);
     out.reward = ((0.0 + 10.0) + -dist_penalty) + -vel_penalty;
+    out.terms[0] = 10.0; out.terms[1] = -dist_penalty; out.terms[2] = -vel_penalty;
     out.done = py + 0.3 <= 1;
   } else if constexpr (R::alive == 6) {
     // InvertedDoublePendulum: robot_pendula.py:76-88, gym_pendulum_envs.py:69-80
@@ -1300,6 +1324,7 @@ PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip
     for (int i = 0; i < 9; i++) obs[i] = (float)o[i];
     const double dist_penalty = 0.01 * (px * px) + ((py + 0.3) - 2) * ((py + 0.3) - 2);
     out.reward = ((0.0 + 10.0) + -dist_penalty) + 0.0;  // sum([alive 10, -dist, -vel 0])
+    out.terms[0] = 10.0; out.terms[1] = -dist_penalty; out.terms[2] = -0.0;
     out.done = py + 0.3 <= 1;
   } else {
     double theta = jq[0], theta_dot = jqd[0], x = jq[1], vx = jqd[1];
@@ -1309,6 +1334,7 @@ PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip
     obs[0] = (float)x; obs[1] = (float)vx; obs[2] = (float)cos(theta); obs[3] = (float)sin(theta);
     obs[4] = (float)theta_dot;
     out.reward = R::alive == 5 ? cos(theta) : 1.0;
+    out.terms[0] = out.reward;  // rewards [float(reward)]
     out.done = R::alive == 5 ? false : fabs(theta) > 0.2;
   }
 }
@@ -1522,9 +1548,11 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   rw.n = B.n;
   rw.cap = lds_rows;
   int nc = 0;
+  uint32_t csig = 0;
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R, LS>(s, tau, slot_active, rw SUB_STAMP_PASS);
+  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R, LS>(s, tau, slot_active, rw, (uint32_t)sub, csig SUB_STAMP_PASS);
   if (io.ncontact) io.ncontact[e] = nc;
+  if (io.csig) io.csig[e] = csig;
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   float obs[R::OBS];
@@ -1563,6 +1591,10 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   const bool trunc = el >= R::max_episode_steps;  // gym TimeLimit (envs/__init__.py max_episode_steps)
   io.rew[e] = (float)po.reward;
   if (io.rew64) io.rew64[e] = po.reward;
+  if (io.rew_terms) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) io.rew_terms[(size_t)e * 5 + i] = po.terms[i];
+  }
   io.done[e] = term || trunc;
   if (io.trunc) io.trunc[e] = trunc && !term;
   if (io.autoreset && (term || trunc)) {
@@ -1681,6 +1713,7 @@ __global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __rest
     const Flag fl = load_flag<R>(B, e);
     a[4 + R::NF] = fl.tx; a[5 + R::NF] = fl.ty; a[6 + R::NF] = fl.timeout; a[7 + R::NF] = fl.count;
   }
+  a[AD - 1] = (double)B.episode[e];  // the reset-noise Philox counter
 }
 template <class R>
 __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* __restrict__ phys, const double* __restrict__ aux) {
@@ -1698,6 +1731,7 @@ __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* 
     B.flags[e] = fl;
     if constexpr (R::flagrun)
       store_flag<R>(B, e, Flag{a[4 + R::NF], a[5 + R::NF], (int)a[6 + R::NF], (int)a[7 + R::NF]});
+    B.episode[e] = (uint32_t)a[AD - 1];
   }
 }
 

@@ -796,15 +796,15 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         t6[gg] = -c;
       }
       fwd6(Lbb, Ldb, t6);
-      float D2 = 0.f, vJ = 0.f;
+      float D2 = 0.f;
 #pragma unroll
-      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; vJ += y[a] * ub[a]; }
+      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
 #pragma unroll
-      for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; vJ += t6[gg] * uB[gg]; }
+      for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; }
       const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
       const float plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
-      Ltl[li] = plo > 0.f ? vJ - plo * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * plo;
-      Lth[li] = phi > 0.f ? -vJ - phi * inv_dt : -(float)PBG_LIMIT_ERP * inv_dt * phi;
+      Ltl[li] = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
+      Lth[li] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
       Lm[li] = meff;
 #pragma unroll
       for (int a = 0; a < NDB; a++) Lyb[li][a] = y[a];
@@ -847,14 +847,14 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       const f3 mm = cross3(rP, nd);
       float y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
       fwd6(Lbb, Ldb, y6);
-      float D2 = 0.f, vJ = 0.f;
+      float D2 = 0.f;
 #pragma unroll
-      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; vJ += y6[gg] * uB[gg]; }
+      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
       float z[NDB];
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
       rw.put(3 * n0 + dir, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
     }
     rw.mu(n0) = (float)R::slot_mu[sl];
     rw.own(n0) = -1.f;
@@ -909,13 +909,13 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         for (int b = 0; b < NDB; b++) y6[gg] -= Lgb[gg][b] * y[b];
       }
       fwd6(Lbb, Ldb, y6);
-      float D2 = 0.f, vJ = 0.f;
+      float D2 = 0.f;
 #pragma unroll
-      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; vJ += y[a] * ub[a]; }
+      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
 #pragma unroll
-      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; vJ += y6[gg] * uB[gg]; }
+      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
       rw.put(3 * ci + dir, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (dist > 0.f ? vJ - dist * inv_dt : -(float)PBG_CONTACT_ERP * inv_dt * dist) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
     }
     rw.mu(ci) = pk<T::SMU, sl>(L);
     rw.own(ci) = (float)kb;
@@ -1153,8 +1153,24 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   uint32_t slot_bits = 0, base_bits = 0;
   int nc = 0;
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw SUB_STAMP_PASS);
+  uint32_t csig = 0;  // this lane's share of the contact-set signature
+  for (int sub = 0; sub < R::substeps; sub++) {
+    nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw SUB_STAMP_PASS);
+    if (io.csig) {  // base slots counted by lane 0, branch k's slots (global NS0 + k NSB + sl) by lane k
+      if (kb == 0)
+        for (int sl = 0; sl < T::NS0; sl++)
+          if ((base_bits >> sl) & 1u) csig += pbg_contact_hash((uint32_t)sub, (uint32_t)sl);
+      for (int sl = 0; sl < T::NSB; sl++)
+        if ((slot_bits >> sl) & 1u) csig += pbg_contact_hash((uint32_t)sub, (uint32_t)(T::NS0 + kb * T::NSB + sl));
+    }
+  }
   if (io.ncontact && kb == 0) io.ncontact[e] = nc;
+  if (io.csig) {
+    uint32_t sig = csig;  // quad sum mod 2^32
+    sig += (uint32_t)qperm_i<0xB1>((int)sig);
+    sig += (uint32_t)qperm_i<0x4E>((int)sig);
+    if (kb == 0) io.csig[e] = sig;
+  }
   // feet contact flags of the last sub-step: this branch's feet, OR-ed over the quad
   uint32_t fb = 0;
   static_for<0, T::NSB>([&](auto sl_c) {
@@ -1186,6 +1202,10 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   if (kb == 0) {
     io.rew[e] = (float)po.reward;
     if (io.rew64) io.rew64[e] = po.reward;
+    if (io.rew_terms) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) io.rew_terms[(size_t)e * 5 + i] = po.terms[i];
+    }
     io.done[e] = term || trunc;
     if (io.trunc) io.trunc[e] = trunc && !term;
   }

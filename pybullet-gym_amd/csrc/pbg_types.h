@@ -27,6 +27,8 @@ struct StepIO {
   float* term_obs;         // [n][OBS] nullable: obs before an auto-reset
   int32_t* ncontact;       // [n] nullable: contacts in the last sub-step
   int autoreset;
+  double* rew_terms;       // [n][5] nullable: the terms the reward sums (reference self.rewards)
+  uint32_t* csig;          // [n] nullable: contact-set signature (sim_params.h pbg_contact_hash)
 };
 
 struct ResetIO {

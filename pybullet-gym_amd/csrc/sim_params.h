@@ -5,10 +5,11 @@
 // which live in the third-party pybullet wheel (absent here): they are [EXT] and
 // unpinned by anything in this container.
 #pragma once
+#include <stdint.h>
 
 #define PBG_GRAVITY 9.8                 // gym_locomotion_envs.py:19, gym_pendulum_envs.py:14
 #define PBG_CONTACT_ERP 0.2             // [EXT] btContactSolverInfo::m_erp: the multibody contact rows use m_erp;
-                                        // setDefaultContactERP(0.9) (scene_bases.py:62) sets m_erp2, used only
+                                        // setDefaultContactERP(0.9) (scene_bases.py:69) sets m_erp2, used only
                                         // for split-impulse penetrations deeper than 4 cm
 #define PBG_SOLVER_ITERATIONS 5         // scene_bases.py:65 numSolverIterations=5
 #define PBG_LIMIT_ERP 0.2               // [EXT] btContactSolverInfo::m_erp default
@@ -40,4 +41,23 @@
 //   [0] potential  [1] initial_z  [2] elapsed steps  [3] floor-in-parts flag
 //   [4 .. 4+NF) feet_contact (as written into the observation)
 //   HumanoidFlagrun only: [4+NF .. 4+NF+4) walk target x, y, flag_timeout, flag draws so far
+//   last word: episodes started so far (the Philox counter of the next reset's noise), so a
+//   checkpoint restored into a fresh handle continues the same reset stream
 #define PBG_AUX_WORDS 4
+#define PBG_AUX_RECORD_WORDS(NF, flagrun) (PBG_AUX_WORDS + (NF) + ((flagrun) ? 4 : 0) + 1)
+
+// Contact-set signature (parity tests): the term of active collision candidate `id` (floor
+// slots 0..NS-1, self-collision pairs NS + p) in sub-step `sub` is murmur3's fmix32 of
+// (sub << 16) + id + golden ratio; an env step's signature is the sum mod 2^32 of the terms
+// of every active candidate of every sub-step (order-free, so distributed kernels reduce it
+// with a plain integer sum).  Equal signatures <=> the same active contact sets (up to 2^-32).
+#ifdef __HIP__
+#define PBG_HD __host__ __device__ inline
+#else
+#define PBG_HD inline
+#endif
+PBG_HD uint32_t pbg_contact_hash(uint32_t sub, uint32_t id) {
+  uint32_t h = (sub << 16) + id + 0x9E3779B9u;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}

@@ -10,7 +10,7 @@ all-gather of observations/rewards/dones for a learner that wants one flat batch
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -24,23 +24,52 @@ def shard_range(num_global: int, rank: int, world: int) -> Tuple[int, int]:
     return offset, count
 
 
-def gather_flat(local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather equal-size per-rank tensors [n_local, ...] into [world * n_local, ...]
-    in rank order (= global env order for equal shards)."""
+def gather_flat(local: torch.Tensor, num_global: Optional[int] = None, group=None) -> torch.Tensor:
+    """All-gather per-rank tensors [n_rank, ...] into [num_global, ...] in rank order (= global
+    env order).  Shards may differ by one row (shard_range): every rank pads its share to
+    ceil(num_global / world) rows, one all_gather_into_tensor moves the padded blocks, and the
+    pad rows are dropped.  num_global=None assumes equal shards (world * n_local)."""
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    return out
+    n_local = local.shape[0]
+    if num_global is None:
+        num_global = world * n_local
+    rows = -(-num_global // world)
+    rank = dist.get_rank(group)
+    off, cnt = shard_range(num_global, rank, world)
+    if cnt != n_local:
+        raise ValueError(f"rank {rank} holds {n_local} rows, shard_range says {cnt} of {num_global}")
+    tail = tuple(local.shape[1:])
+    if n_local == rows:
+        send = local.contiguous()
+    else:
+        send = torch.zeros((rows,) + tail, dtype=local.dtype, device=local.device)
+        send[:n_local] = local
+    out = torch.empty((world * rows,) + tail, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, send, group=group)
+    if num_global == world * rows:
+        return out
+    keep = torch.cat([torch.arange(r * rows, r * rows + shard_range(num_global, r, world)[1], device=out.device)
+                      for r in range(world)])
+    return out.index_select(0, keep)
 
 
 class ShardedVecEnv:
-    """This rank's share of a global batch of envs, plus the optional flat gather."""
+    """This rank's share of a global batch of envs, plus the optional flat gather.
+
+    env_factory(env_id, count, device, seed, env_offset, autoreset) builds the per-rank env
+    (default: the HIP VecEnv); anything with ``obs`` / ``reward`` / ``done`` tensors and
+    ``reset`` / ``step`` works (the CPU tests drive the oracle through it)."""
 
     def __init__(self, env_id: str, num_global: int, rank: int, world: int, device, seed: int = 0,
-                 autoreset: bool = True):
-        from .vec_env import VecEnv
+                 autoreset: bool = True, env_factory: Optional[Callable] = None):
+        self.num_global = num_global
         self.offset, self.count = shard_range(num_global, rank, world)
-        self.env = VecEnv(env_id, self.count, device=device, seed=seed, env_offset=self.offset, autoreset=autoreset)
+        if env_factory is None:
+            from .vec_env import VecEnv
+
+            def env_factory(env_id, count, device, seed, env_offset, autoreset):
+                return VecEnv(env_id, count, device=device, seed=seed, env_offset=env_offset, autoreset=autoreset)
+        self.env = env_factory(env_id, self.count, device, seed, self.offset, autoreset)
 
     def reset(self, **kw):
         return self.env.reset(**kw)
@@ -49,6 +78,7 @@ class ShardedVecEnv:
         return self.env.step(actions)
 
     def gather(self):
-        """(obs, reward, done) of every env of every rank, flat, on every rank."""
+        """(obs, reward, done) of every env of every rank, flat in global env order, on every rank."""
         e = self.env
-        return gather_flat(e.obs), gather_flat(e.reward), gather_flat(e.done)
+        n = self.num_global
+        return gather_flat(e.obs, n), gather_flat(e.reward, n), gather_flat(e.done, n)

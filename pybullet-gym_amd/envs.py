@@ -188,7 +188,9 @@ class BaseBulletEnv:
         assert np.isfinite(a).all()  # robot_locomotors.py:27
         res = self._vec.step(torch.from_numpy(a), want_reward64=True)
         r = float(self._vec.reward64[0])
-        done = bool(res.done[0])
+        # termination only (gym_locomotion_envs.py:61-65): the kernel's own TimeLimit marks a
+        # 1000th step done + truncated; the time limit belongs to the TimeLimit wrapper
+        done = bool(res.done[0]) and not bool(res.truncated[0])
         self.frame += 1
         self.reward += r
         return self._obs_out(res.obs), r, done, {}
@@ -429,7 +431,8 @@ REWARD_THRESHOLD = {"InvertedPendulumPyBulletEnv-v0": 950.0, "HopperPyBulletEnv-
                     "InvertedDoublePendulumMuJoCoEnv-v0": 9100.0,
                     "Walker2DPyBulletEnv-v0": 2500.0, "Walker2DMuJoCoEnv-v0": 2500.0,
                     "HalfCheetahMuJoCoEnv-v0": 3000.0, "HopperMuJoCoEnv-v0": 2500.0, "AntMuJoCoEnv-v0": 2500.0,
-                    "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0}
+                    "HalfCheetahPyBulletEnv-v0": 3000.0, "AntPyBulletEnv-v0": 2500.0,
+                    "HumanoidFlagrunPyBulletEnv-v0": 2000.0}  # envs/__init__.py:90
 
 
 class TimeLimit:

@@ -46,3 +46,23 @@ def reset_noise(seed: int, global_ids, episode, n_reset_dofs: int) -> np.ndarray
             if j < n_reset_dofs:
                 out[:, j] = v[:, t]
     return out
+
+
+def sample_actions(action_dim: int, global_ids, steps, seed: int = 0x5EED) -> np.ndarray:
+    """float32 [len(steps), len(global_ids), action_dim] = pbg_sample_actions' U(-1, 1) draws
+    (Philox4x32-10, key = seed, counter = (step, global env id, block of 4 actions, 0xAC7))."""
+    gid = np.asarray(global_ids, dtype=np.uint32)
+    st = np.asarray(steps, dtype=np.uint32)
+    key = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    out = np.zeros((st.size, gid.size, action_dim), dtype=np.float32)
+    S, G = np.meshgrid(st, gid, indexing="ij")
+    for blk in range((action_dim + 3) // 4):
+        ctr = np.stack([S, G, np.full_like(S, blk), np.full_like(S, 0xAC7)], axis=-1)
+        r = philox4x32_10(ctr, key)
+        u = (r >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        v = (2.0 * u.astype(np.float64) - 1.0).astype(np.float32)  # fmaf(2, u, -1): exact, one rounding
+        for t in range(4):
+            j = 4 * blk + t
+            if j < action_dim:
+                out[..., j] = v[..., t]
+    return out

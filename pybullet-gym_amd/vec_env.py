@@ -37,8 +37,20 @@ class StepResult:
 
 
 class VecEnv:
+    """``num_envs`` copies of ``env_id`` on one GPU.
+
+    ``step`` returns views of the env's own output buffers (``obs``, ``reward``, ``done``,
+    ``truncated``, ``terminal_obs``): the next ``step`` or ``reset`` overwrites them in place,
+    so a learner that keeps a batch across steps must ``clone()`` it (the buffers are never
+    reallocated, which is what lets a step be captured into a HIP graph).
+
+    ``kernel`` / ``lds_rows`` / ``gang_dist`` are test and diagnostic launch options
+    (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
+    a cap on LDS-resident contact rows, forced replicated (0) / distributed (1) gang dynamics.
+    """
+
     def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
-                 autoreset: bool = True):
+                 autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1):
         if not torch.cuda.is_available():
             raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.env_id = env_id
@@ -48,8 +60,9 @@ class VecEnv:
         L = _native.lib()
         h = ctypes.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        _native.check(L.pbg_create(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
-                                   ctypes.byref(h)), "pbg_create")
+        opts = _native.DebugOpts(int(kernel), int(lds_rows), int(gang_dist))
+        _native.check(L.pbg_create_debug(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
+                                         ctypes.byref(opts), ctypes.byref(h)), "pbg_create")
         self._h = h
         info = _native.Info()
         _native.check(L.pbg_info(h, ctypes.byref(info)), "pbg_info")
@@ -66,6 +79,8 @@ class VecEnv:
         self.terminal_obs = torch.zeros((n, info.obs_dim), dtype=torch.float32, **kw)
         self.reward64 = None
         self.ncontact = None
+        self.reward_terms = None
+        self.contact_sig = None
         self._io = _native.StepIO()
 
     # ---------------------------------------------------------------- lifecycle
@@ -93,7 +108,12 @@ class VecEnv:
                                               _stream(self.device)), "pbg_reset")
         return self.obs
 
-    def step(self, actions: torch.Tensor, want_reward64: bool = False, want_contacts: bool = False) -> StepResult:
+    def step(self, actions: torch.Tensor, want_reward64: bool = False, want_contacts: bool = False,
+             want_terms: bool = False) -> StepResult:
+        """One env step of every env.  Optional outputs (kept on the object): ``reward64``
+        (float64 reward), ``ncontact`` / ``contact_sig`` (contacts of the last sub-step and the
+        step's contact-set signature, want_contacts), ``reward_terms`` ([n, 5] float64: the
+        reference's per-term ``self.rewards``, gym_locomotion_envs.py:99-105; want_terms)."""
         a = actions
         if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
@@ -109,8 +129,13 @@ class VecEnv:
             self.reward64 = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         if want_contacts and self.ncontact is None:
             self.ncontact = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+            self.contact_sig = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)  # uint32 bits
+        if want_terms and self.reward_terms is None:
+            self.reward_terms = torch.zeros((self.num_envs, 5), dtype=torch.float64, device=self.device)
         io.rew64 = self.reward64.data_ptr() if want_reward64 else None
         io.ncontact = self.ncontact.data_ptr() if want_contacts else None
+        io.csig = self.contact_sig.data_ptr() if want_contacts else None
+        io.rew_terms = self.reward_terms.data_ptr() if want_terms else None
         io.autoreset = 1 if self.autoreset else 0
         _native.check(_native.lib().pbg_step_ex(self._h, ctypes.byref(io), _stream(self.device)), "pbg_step")
         return StepResult(self.obs, self.reward, self.done, self.truncated, self.terminal_obs)
@@ -147,6 +172,16 @@ class VecEnv:
             assert aux.shape == (self.num_envs, self.info.aux_words)
         _native.check(_native.lib().pbg_set_state(self._h, _ptr(phys), _ptr(aux), _stream(self.device)),
                       "pbg_set_state")
+
+
+def sample_actions(action_dim: int, num_envs: int, steps: int, seed: int = 0x5EED, step0: int = 0,
+                   env_offset: int = 0, device="cuda:0") -> torch.Tensor:
+    """[steps, num_envs, action_dim] float32 U(-1, 1) on the device (pbg_sample_actions: Philox,
+    counter (step0 + s, env_offset + e, ...), so a shard draws the same actions as a full batch)."""
+    out = torch.empty((steps, num_envs, action_dim), dtype=torch.float32, device=device)
+    _native.check(_native.lib().pbg_sample_actions(action_dim, num_envs, steps, seed, step0, env_offset,
+                                                    _ptr(out), _stream(out.device)), "pbg_sample_actions")
+    return out
 
 
 def pack(env_id: str, in_rec: torch.Tensor) -> torch.Tensor:

@@ -1,8 +1,9 @@
 """Multi-process sharding on CPU (gloo, world_size 2): each rank steps its contiguous env
-range with reset noise keyed by global env id, and the flat all-gather reproduces a
-single-process run over all envs bit-for-bit.  The per-rank stepping uses the CPU oracle
-(the HIP path needs a GPU); the sharding arithmetic and gather glue are the product's
-(pybulletgym_amd.distributed)."""
+range with reset noise keyed by global env id, and the product's flat all-gather
+(pybulletgym_amd.distributed.ShardedVecEnv.gather -> gather_flat, padded for uneven shards)
+reproduces a single-process run over all envs bit-for-bit -- obs float32, reward float32 and
+the uint8 done flags.  The per-rank env is the CPU oracle behind VecEnv's buffer interface
+(the HIP path needs a GPU); shard arithmetic, env factory and gather are the product's."""
 import os
 import socket
 
@@ -16,37 +17,49 @@ import pybulletgym_amd  # noqa: F401
 from pybulletgym_amd import distributed as pd, rng
 
 ENV = "AntPyBulletEnv-v0"
-N_GLOBAL, STEPS, SEED = 10, 4, 11
+N_GLOBAL, STEPS, SEED = 7, 4, 11  # 7 envs on 2 ranks: shards of 4 and 3
+
+
+class OracleShard:
+    """VecEnv-shaped CPU stand-in (obs / reward / done tensors, reset / step) over the oracle,
+    for the gloo tests only."""
+
+    def __init__(self, env_id, count, device, seed, env_offset, autoreset):
+        import oracle
+        self.e = oracle.OracleEnvs(env_id, count)
+        self.ids = np.arange(env_offset, env_offset + count)
+        self.seed = seed
+        self.obs = torch.zeros((count, self.e.info.OBS), dtype=torch.float32)
+        self.reward = torch.zeros(count, dtype=torch.float32)
+        self.done = torch.zeros(count, dtype=torch.uint8)
+
+    def reset(self):
+        q = rng.reset_noise(self.seed, self.ids, 0, self.e.info.NR).astype(np.float64)
+        self.obs[:] = torch.from_numpy(self.e.reset(q))
+        return self.obs
+
+    def step(self, actions):
+        o, r, d, _ = self.e.step(np.asarray(actions))
+        self.obs[:] = torch.from_numpy(o)
+        self.reward[:] = torch.from_numpy(r.astype(np.float32))
+        self.done[:] = torch.from_numpy(d.astype(np.uint8))
+        return self.obs
 
 
 def actions_for(global_ids, step, na):
-    out = np.zeros((len(global_ids), na), np.float32)
-    for i, g in enumerate(global_ids):
-        out[i] = np.random.default_rng(1000 * step + int(g)).uniform(-1, 1, na)
-    return out
-
-
-def rollout(global_ids):
-    import oracle
-    e = oracle.OracleEnvs(ENV, len(global_ids))
-    obs = [e.reset(rng.reset_noise(SEED, global_ids, 0, e.info.NR).astype(np.float64))]
-    rews = []
-    for t in range(STEPS):
-        o, r, d, _ = e.step(actions_for(global_ids, t, e.info.NA))
-        obs.append(o)
-        rews.append(r)
-    return np.stack(obs), np.stack(rews)
+    return rng.sample_actions(na, global_ids, [step], seed=SEED)[0]
 
 
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    off, cnt = pd.shard_range(N_GLOBAL, rank, world)
-    obs, rew = rollout(np.arange(off, off + cnt))
-    flat = pd.gather_flat(torch.from_numpy(obs[-1]))
-    flat_r = pd.gather_flat(torch.from_numpy(rew[-1]))
+    env = pd.ShardedVecEnv(ENV, N_GLOBAL, rank, world, device="cpu", seed=SEED, env_factory=OracleShard)
+    env.reset()
+    for t in range(STEPS):
+        env.step(actions_for(np.arange(env.offset, env.offset + env.count), t, 8))
+    obs, rew, done = env.gather()
     if rank == 0:
-        q.put((flat.numpy(), flat_r.numpy()))
+        q.put((env.count, obs.numpy(), rew.numpy(), done.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,7 +73,7 @@ def _free_port():
 
 
 def test_shard_range_covers_all():
-    for n in (1, 7, 16384, 65536):
+    for n in (1, 7, 16384, 65536, 65537):
         for w in (1, 2, 3, 8):
             spans = [pd.shard_range(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and sum(c for _, c in spans) == n
@@ -68,17 +81,22 @@ def test_shard_range_covers_all():
                 assert o1 + c1 == o2
 
 
-def test_two_rank_gather_matches_single_process():
+def test_two_rank_sharded_vecenv_gather_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    flat_obs, flat_rew = q.get(timeout=120)
+    count0, flat_obs, flat_rew, flat_done = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref_obs, ref_rew = rollout(np.arange(N_GLOBAL))
-    np.testing.assert_array_equal(flat_obs, ref_obs[-1])
-    np.testing.assert_array_equal(flat_rew, ref_rew[-1])
+    assert count0 == 4 and flat_obs.shape == (N_GLOBAL, 28) and flat_done.dtype == np.uint8
+    ref = OracleShard(ENV, N_GLOBAL, "cpu", SEED, 0, True)
+    ref.reset()
+    for t in range(STEPS):
+        ref.step(actions_for(np.arange(N_GLOBAL), t, 8))
+    np.testing.assert_array_equal(flat_obs, ref.obs.numpy())
+    np.testing.assert_array_equal(flat_rew, ref.reward.numpy())
+    np.testing.assert_array_equal(flat_done, ref.done.numpy())
