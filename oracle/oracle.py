@@ -46,7 +46,7 @@ def lib():
         L.pbg_oracle_reset_mask.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P]
         L.pbg_oracle_step.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P]
         L.pbg_oracle_step_ex.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P,
-                                         ctypes.c_int]
+                                         ctypes.c_int, P]
         L.pbg_oracle_count_flops.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
         L.pbg_oracle_set_physics.argtypes = [P, ctypes.c_int]
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
@@ -92,6 +92,7 @@ class OracleEnvs:
         self.state = np.zeros((n, self.info.SD), dtype=np.float64)
         self.aux = np.zeros((n, self.info.AD), dtype=np.float64)
         self.csig = np.zeros(n, dtype=np.uint32)      # last step's contact-set signatures
+        self.asig = np.zeros(n, dtype=np.uint32)      # last step's solver active-set signatures
         self.terms = np.zeros((n, 5), dtype=np.float64)  # last step's reward terms
 
     def reset(self, qinit: np.ndarray, mask: np.ndarray = None, obs: np.ndarray = None) -> np.ndarray:
@@ -112,7 +113,7 @@ class OracleEnvs:
         nc = np.zeros(self.n, dtype=np.int32)
         assert lib().pbg_oracle_step_ex(self.rid, self.n, _p(self.state), _p(self.aux), _p(act), _p(obs),
                                         _p(rew), _p(done), _p(nc), self.nthreads, _p(self.csig), _p(self.terms),
-                                        self.precision) == 0
+                                        self.precision, _p(self.asig)) == 0
         return obs, rew, done.astype(bool), nc
 
 

@@ -58,7 +58,7 @@ enum { OPT_CONTACT_ERP, OPT_DEEP_ERP, OPT_DEEP_THR, OPT_DEEP_MODE, OPT_LIMIT_MOD
        OPT_COUNT };
 double g_opt[OPT_COUNT];
 const double g_opt_default[OPT_COUNT] = {
-    PBG_CONTACT_ERP,  // contact ERP (penetrating contact normal rows)
+    -1.0,             // contact ERP of penetrating contact normal rows (-1: the model's, models_gen.h)
     -1.0,             // ERP for penetrations deeper than OPT_DEEP_THR (-1: same as contact ERP)
     -0.04,            // split-impulse penetration threshold (btContactSolverInfo m_splitImpulsePenetrationThreshold)
     0.0,              // deep mode: 0 = OPT_DEEP_ERP, 1 = no positional term (split impulse absent for multibodies)
@@ -84,7 +84,7 @@ size_t g_cache_n = 0;
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
       floor, max_steps, robot_body, tip_link, flagrun;
-  double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip;
+  double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip, contact_erp;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
   const double (*off_pos)[3], (*axis)[3], (*anchor)[3], (*com)[3], (*off_quat)[4], (*inertia)[6];
@@ -109,7 +109,7 @@ MV view() {
   m.flagrun = R::flagrun;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
-  m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
+  m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.contact_erp = R::contact_erp; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
   m.base_quat = R::base_quat; m.link_parent = R::link_parent; m.link_jtype = R::link_jtype;
   m.link_dof = R::link_dof; m.off_pos = R::link_offset_pos; m.axis = R::link_axis;
   m.anchor = R::link_anchor; m.com = R::link_com; m.off_quat = R::link_offset_quat;
@@ -705,9 +705,10 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
 // rew_terms (nullable): [n][5] the terms the reward sums (the reference's self.rewards).
 // precision: 64 = the float64 oracle; 32 = the same physics in IEEE float32 (the pack stays
 // float64, as in the kernels) -- the parity tests' conditioning probe.
+// asig (nullable): per env the solver active-set signature (sim_params.h pbg_solver_event).
 int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float* act, float* obs, double* rew,
                        uint8_t* done, int32_t* ncontact, int nthreads, uint32_t* csig, double* rew_terms,
-                       int precision) {
+                       int precision, uint32_t* asig) {
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
@@ -725,8 +726,10 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     uint8_t slot_active[MAXS];
     uint32_t sig = 0;
     double* cache = g_cache && (size_t)e < g_cache_n ? g_cache + (size_t)e * 4 * (MAXS + MAXPAIR) : nullptr;
-    const int nc = precision == 32 ? physics_step<float>(m, s, ac, slot_active, &sig, nullptr)
-                                   : physics_step<double>(m, s, ac, slot_active, &sig, cache);
+    uint32_t as = 0;
+    const int nc = precision == 32 ? physics_step<float>(m, s, ac, slot_active, &sig, nullptr, &as)
+                                   : physics_step<double>(m, s, ac, slot_active, &sig, cache, &as);
+    if (asig) asig[e] = as;
     if (ncontact) ncontact[e] = nc;
     if (csig) csig[e] = sig;
     double* terms = rew_terms ? rew_terms + (size_t)e * 5 : nullptr;
@@ -764,7 +767,8 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
 
 int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* act, float* obs, double* rew,
                     uint8_t* done, int32_t* ncontact, int nthreads, uint32_t* csig, double* rew_terms) {
-  return pbg_oracle_step_ex(robot, n, state, aux, act, obs, rew, done, ncontact, nthreads, csig, rew_terms, 64);
+  return pbg_oracle_step_ex(robot, n, state, aux, act, obs, rew, done, ncontact, nthreads, csig, rew_terms, 64,
+                            nullptr);
 }
 
 // Algorithmic FP32 work of the physics (apply_action + the sub-steps) of one env step from

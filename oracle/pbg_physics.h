@@ -378,14 +378,17 @@ void setup_row(int n, const T L[MAXD][MAXD], const T* nu, RowT<T>& r, T pos, int
   r.lambda = T(0);
 }
 
-template <class T> inline void solve_row(int n, RowT<T>& r, T* nu) {
+// returns the clamp code of the update (sim_params.h pbg_clamp_code)
+template <class T> inline uint32_t solve_row(int n, RowT<T>& r, T* nu) {
   T delta = r.meff * (r.target - dotn(n, r.J, nu));
   T nl = r.lambda + delta;
+  const uint32_t code = pbg_clamp_code(nl, r.lo, r.hi);
   if (nl < r.lo) nl = r.lo;
   if (nl > r.hi) nl = r.hi;
   delta = nl - r.lambda;
   r.lambda = nl;
   for (int i = 0; i < n; i++) nu[i] = nu[i] + r.W[i] * delta;
+  return code;
 }
 
 template <class T> inline T clampv(T v) {
@@ -398,9 +401,10 @@ template <class T> inline T clampv(T v) {
 // (robot_locomotors.py:26-29).  qd_step: joint velocities at the start of the env step
 // (rule study: damping once per step).  cache (nullable, T = double only): warm-start store.
 // Returns the number of contacts; slot_active receives the floor-slot flags.
+// asig (nullable): adds the solver active-set events (sim_params.h pbg_solver_event).
 template <class T>
 int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint32_t* sig, double* cache,
-            const T* qd_step) {
+            const T* qd_step, uint32_t* asig) {
   const T dt(m.dt_sub);
   const int n = m.NDOF;
   static thread_local KinT<T> k;
@@ -454,7 +458,7 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     nc = w;
   }
   int first_normal = nr;
-  const double erp = g_opt[OPT_CONTACT_ERP];
+  const double erp = g_opt[OPT_CONTACT_ERP] < 0 ? m.contact_erp : g_opt[OPT_CONTACT_ERP];
   const double deep_erp = g_opt[OPT_DEEP_ERP] < 0 ? erp : g_opt[OPT_DEEP_ERP];
   for (int c = 0; c < nc; c++) {
     RowT<T>& r = rows[nr++];
@@ -498,10 +502,21 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   }
   const int iters = (int)g_opt[OPT_ITERS];
   const bool cone = g_opt[OPT_FRIC_MODE] == 1.0;
+  // solver-event row ids: limits 2 li + side (first_normal rows), contact c 2 NLIM + 3 c + dir
+  auto event = [&](int it, int row, uint32_t code) {
+    if (asig && code) *asig += pbg_solver_event((uint32_t)sub, (uint32_t)it, (uint32_t)row, code);
+  };
+  auto crow = [&](int i) {  // the event row id of constraint row i
+    if (i < first_normal) return i;
+    if (i < first_friction) return first_normal + 3 * (i - first_normal);
+    const int c = (i - first_friction) / fric_dirs;
+    return first_normal + 3 * c + 1 + (i - first_friction - fric_dirs * c);
+  };
   for (int it = 0; it < iters; it++) {
-    for (int i = 0; i < first_friction; i++) solve_row(n, rows[i], nu);
+    for (int i = 0; i < first_friction; i++) event(it, crow(i), solve_row(n, rows[i], nu));
     for (int i = first_friction; i < nr; i += (cone ? 2 : 1)) {
       T ln = rows[rows[i].normal].lambda;
+      if (!(ln > T(0)) && (i - first_friction) % fric_dirs == 0) event(it, crow(i), 3u);
       if (ln > T(0)) {  // [EXT] Bullet solves a friction row only under a positive normal impulse
         if (cone) {  // btMultiBodyConstraintSolver::resolveConeFrictionConstraintRows
           RowT<T>& a = rows[i];
@@ -518,7 +533,7 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
         } else {
           rows[i].lo = T(0) - rows[i].mu * ln;
           rows[i].hi = rows[i].mu * ln;
-          solve_row(n, rows[i], nu);
+          event(it, crow(i), solve_row(n, rows[i], nu));
         }
       }
     }
@@ -569,7 +584,8 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
 // kernels: act_gain * clip(a) in double, rounded to T), `substeps` sub-steps.  state: the
 // env's float64 record, read into T and written back (T = double: in place).
 template <class T>
-int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_active, uint32_t* sig, double* cache) {
+int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_active, uint32_t* sig, double* cache,
+                 uint32_t* asig = nullptr) {
   T s[PBG_BASE_WORDS + 2 * MAXD], tau[MAXD], qd_step[MAXD];
   const int SD = PBG_BASE_WORDS + 2 * m.NJ;
   for (int i = 0; i < SD; i++) s[i] = T(state[i]);
@@ -580,7 +596,7 @@ int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_acti
   }
   for (int d = 0; d < m.NJ; d++) qd_step[d] = s[PBG_BASE_WORDS + m.NJ + d];
   int nc = 0;
-  for (int sub = 0; sub < m.substeps; sub++) nc = substep<T>(m, s, tau, slot_active, sub, sig, cache, qd_step);
+  for (int sub = 0; sub < m.substeps; sub++) nc = substep<T>(m, s, tau, slot_active, sub, sig, cache, qd_step, asig);
   for (int i = 0; i < SD; i++) state[i] = (double)s[i];
   return nc;
 }

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
       const int nopt = pbg_oracle_set_physics(nullptr, 0);
       pbg_oracle_set_physics(nullptr, 0);
       if (var[0] >= 0) {
-        const double def[] = {0.2, -1.0, -0.04, 0, 0, 0, 0, 0, 0, 0.2, 5, 0, 0, 1, 1};
+        const double def[] = {-1.0, -1.0, -0.04, 0, 0, 0, 0, 0, 0, 0.2, 5, 0, 0, 1, 1};
         memcpy(opt, def, sizeof(def));
         opt[(int)var[0]] = var[1];
         pbg_oracle_set_physics(opt, nopt);

@@ -20,6 +20,57 @@ from . import mjcf, robots
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(HERE, "csrc", "models_gen.h")
 MODEL_DIR = os.path.join(HERE, "models")
+# Importer-rule overrides: a pybullet dump, when one exists, replaces the
+# mjcf.py rules B3-B6 per robot without code changes.  Format (every key optional):
+#   {"<robot key>": {"contact_erp": e, "floor_lateral_friction": mu_floor,
+#      "links":  {"<link or base name>": {"mass": m, "local_inertia_diagonal": [ix, iy, iz],
+#                                         "lateral_friction": mu}},      # getDynamicsInfo fields
+#      "joints": {"<joint name>": {"damping": d, "lower": lo, "upper": hi}}}}  # getJointInfo fields
+OVERRIDES = os.path.join(MODEL_DIR, "importer_overrides.json")
+CONTACT_ERP_DEFAULT = 0.2  # sim_params.h PBG_CONTACT_ERP (Bullet btContactSolverInfo::m_erp)
+
+
+def load_overrides(path: str = None) -> Dict:
+    path = path or OVERRIDES
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        ov = json.load(f)
+    return {k: v for k, v in ov.items() if not k.startswith("_")}
+
+
+def apply_overrides(model: mjcf.RobotModel, ov: Dict) -> None:
+    """Replace the imported mass / inertia / friction / joint damping and limits by the values
+    a pybullet dump reports (getDynamicsInfo / getJointInfo), in place."""
+    floor_mu = ov.get("floor_lateral_friction")
+    for name, d in ov.get("links", {}).items():
+        if name == model.base_name:
+            if "mass" in d:
+                model.base_mass = float(d["mass"])
+            if "local_inertia_diagonal" in d:
+                model.base_inertia = np.diag([float(x) for x in d["local_inertia_diagonal"]])
+            geoms = model.base_geoms
+        else:
+            link = model.links[model.link_index(name)]
+            if "mass" in d:
+                link.mass = float(d["mass"])
+            if "local_inertia_diagonal" in d:
+                link.inertia = np.diag([float(x) for x in d["local_inertia_diagonal"]])
+            geoms = link.geoms
+        if "lateral_friction" in d:
+            for g in geoms:
+                g.friction = float(d["lateral_friction"])
+    for name, d in ov.get("joints", {}).items():
+        hits = [l for l in model.links if l.joint_name == name]
+        if not hits:
+            raise KeyError(f"override for unknown joint {name!r}")
+        for l in hits:
+            if "damping" in d:
+                l.damping = float(d["damping"])
+            if "lower" in d and "upper" in d:
+                l.lower, l.upper = float(d["lower"]), float(d["upper"])
+                l.limited = l.lower <= l.upper
+    return floor_mu
 
 
 def _chain_links(model: mjcf.RobotModel, li: int) -> List[int]:
@@ -29,7 +80,10 @@ def _chain_links(model: mjcf.RobotModel, li: int) -> List[int]:
     return out[::-1]
 
 
-def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
+def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None) -> Dict:
+    ov = ov or {}
+    floor_mu = apply_overrides(model, ov)
+    floor_mu = mjcf.FLOOR_FRICTION if floor_mu is None else float(floor_mu)
     parts, ordered, robot_body = robots.add_to_scene_order(model, spec.robot_name)
     L = model.n_links
     NJ = model.n_joint_dofs
@@ -107,7 +161,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
             for g in geoms:
                 if g.contype == 0 and g.conaffinity == 0:
                     continue
-                mu = g.friction * mjcf.FLOOR_FRICTION
+                mu = g.friction * floor_mu
                 if g.kind == mjcf.GEOM_SPHERE:
                     slots.append((li, g.p0, g.radius, mu))
                 else:
@@ -182,16 +236,19 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel) -> Dict:
         NG=len(pgeoms), geom_link=[g[0] for g in pgeoms], geom_p0=[list(g[1].p0) for g in pgeoms],
         geom_p1=[list(g[1].p1) for g in pgeoms], geom_r=[g[1].radius for g in pgeoms],
         pair_ga=pair_ga, pair_gb=pair_gb,
+        contact_erp=float(ov.get("contact_erp", CONTACT_ERP_DEFAULT)),
     )
     return t
 
 
-def compile_all(asset_dir: str = None) -> Dict[str, Dict]:
+def compile_all(asset_dir: str = None, overrides: Dict = None) -> Dict[str, Dict]:
+    """overrides: {robot key: override dict} (default: models/importer_overrides.json if present)."""
     asset_dir = asset_dir or robots.reference_asset_dir()
+    overrides = load_overrides() if overrides is None else overrides
     out = {}
     for key, spec in robots.SPECS.items():
         model = mjcf.compile_mjcf(os.path.join(asset_dir, spec.mjcf), key)
-        out[key] = build_tables(spec, model)
+        out[key] = build_tables(spec, model, overrides.get(key))
     return out
 
 
@@ -235,7 +292,7 @@ def emit_struct(t: Dict) -> str:
               "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
-              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip"):
+              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp"):
         L.append(f"  static constexpr double {k} = {_num(t[k])};")
     L.append(_arr1("base_inertia", "double", t["base_inertia"]))
     L.append(_arr1("base_pos", "double", t["base_pos"]))

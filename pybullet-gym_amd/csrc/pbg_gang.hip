@@ -769,7 +769,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       for (int i = 0; i < YS; i++) cput<R, T>(X, c, w0r + i, i < N ? y[i] : 0.f);
       cput<R, T>(X, c, w0r + YS, meff);
       cput<R, T>(X, c, w0r + YS + 1,
-                 dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
+                 dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
       cput<R, T>(X, c, w0r + YS + 2, 0.f);
     }
   }

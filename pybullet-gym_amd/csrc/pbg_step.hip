@@ -841,7 +841,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
       rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
@@ -923,7 +923,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
          
         }
         rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-               dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
+               dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;

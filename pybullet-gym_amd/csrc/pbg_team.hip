@@ -854,7 +854,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
       rw.put(3 * n0 + dir, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
     }
     rw.mu(n0) = (float)R::slot_mu[sl];
     rw.own(n0) = -1.f;
@@ -915,7 +915,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
       rw.put(3 * ci + dir, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)PBG_CONTACT_ERP, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
     }
     rw.mu(ci) = pk<T::SMU, sl>(L);
     rw.own(ci) = (float)kb;

@@ -8,7 +8,7 @@
 #include <stdint.h>
 
 #define PBG_GRAVITY 9.8                 // gym_locomotion_envs.py:19, gym_pendulum_envs.py:14
-#define PBG_CONTACT_ERP 0.2             // [EXT] btContactSolverInfo::m_erp: the multibody contact rows use m_erp;
+#define PBG_CONTACT_ERP 0.2             // default of models_gen.h contact_erp (per robot; codegen overrides) [EXT] btContactSolverInfo::m_erp: the multibody contact rows use m_erp;
                                         // setDefaultContactERP(0.9) (scene_bases.py:69) sets m_erp2, used only
                                         // for split-impulse penetrations deeper than 4 cm
 #define PBG_SOLVER_ITERATIONS 5         // scene_bases.py:65 numSolverIterations=5
@@ -61,3 +61,16 @@ PBG_HD uint32_t pbg_contact_hash(uint32_t sub, uint32_t id) {
   h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
   return h;
 }
+
+// Solver active-set signature (parity tests): a PGS row update that ends clamped at its lower
+// bound (code 1) or its upper bound (code 2), and a friction pair skipped under a non-positive
+// normal impulse (code 3, on the pair's first row), add the term of (sub-step, sweep, row,
+// code); rows: joint limit li (limited dofs in dof order) side s -> 2 li + s, contact c ->
+// 2 NLIM + 3 c + {0 normal, 1 and 2 friction}.  With the same contact set and the same
+// signature, GPU and oracle took the same branch at every update of the 5-sweep PGS, which is
+// then a smooth function of the state.
+PBG_HD uint32_t pbg_solver_event(uint32_t sub, uint32_t sweep, uint32_t row, uint32_t code) {
+  return pbg_contact_hash(0x8000u | (sub << 4) | sweep, (row << 2) | code);
+}
+template <class F>
+PBG_HD uint32_t pbg_clamp_code(F v, F lo, F hi) { return v < lo ? 1u : (v > hi ? 2u : 0u); }

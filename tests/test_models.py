@@ -102,3 +102,37 @@ def test_walker2d_topology_and_gains():
                                     "thigh_left_joint", "leg_left_joint", "foot_left_joint"]
     assert t["act_gain"] == pytest.approx([40.0, 40.0, 12.0, 40.0, 40.0, 12.0])
     assert [t["link_name"][l] for l in t["foot_link"]] == ["foot", "foot_left"]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_ASSETS), reason="reference assets only in the build container")
+def test_importer_overrides_change_the_generated_tables():
+    """A getDynamicsInfo / getJointInfo-shaped override (models/importer_overrides.json format)
+    replaces the mjcf.py rules: mass, inertia diagonal, lateral friction, joint damping and
+    limits, contact ERP and the floor friction all land in the emitted header."""
+    spec = robots.spec_for("ant")
+    base = codegen.build_tables(spec, mjcf.compile_mjcf(os.path.join(REF_ASSETS, spec.mjcf), "ant"))
+    ov = {"contact_erp": 0.9, "floor_lateral_friction": 1.0,
+          "links": {"torso": {"mass": 12.5, "local_inertia_diagonal": [0.3, 0.4, 0.5], "lateral_friction": 0.5},
+                    "front_left_foot": {"mass": 0.75}},
+          "joints": {"hip_1": {"damping": 2.5, "lower": -0.5, "upper": 0.25}}}
+    t = codegen.build_tables(spec, mjcf.compile_mjcf(os.path.join(REF_ASSETS, spec.mjcf), "ant"), ov)
+    assert t["contact_erp"] == 0.9 and base["contact_erp"] == 0.2
+    assert t["base_mass"] == 12.5 and t["base_inertia"][:3] == [0.3, 0.4, 0.5]
+    foot = t["link_name"].index("front_left_foot")
+    assert t["link_mass"][foot] == 0.75 != base["link_mass"][foot]
+    d = t["link_dof"][t["link_name"].index("aux_1")]  # hip_1 moves aux_1
+    assert t["dof_damping"][d] == 2.5 and (t["dof_lower"][d], t["dof_upper"][d]) == (-0.5, 0.25)
+    base_slots = [i for i, l in enumerate(t["slot_link"]) if l == -1]
+    assert all(abs(t["slot_mu"][i] - 0.5 * 1.0) < 1e-12 for i in base_slots)
+    other = [i for i, l in enumerate(t["slot_link"]) if l != -1]
+    assert all(abs(t["slot_mu"][i] - base["slot_mu"][i] / 0.8) < 1e-12 for i in other)  # floor 0.8 -> 1.0
+    hdr = codegen.emit_struct(t)
+    assert "contact_erp = 0.9;" in hdr and "base_mass = 12.5;" in hdr
+    assert codegen.emit_struct(base) != hdr
+
+
+def test_committed_override_file_is_well_formed():
+    ov = codegen.load_overrides()
+    assert isinstance(ov, dict)
+    for key in ov:
+        assert key in robots.SPECS, key
