@@ -334,25 +334,29 @@ struct TRows {
     p[(NDB + 7) * st] = target;
     p[(NDB + 8) * st] = 0.f;
   }
-  // one row in registers (loaded ahead of its update: PGS software pipelining)
+  // One row in registers (loaded ahead of its update: PGS software pipelining).  The base
+  // part is sliced over the quad: lane k holds base components k and k + 4 (k < 2), the
+  // same components of u it owns in the sweeps (BaseSlice), so each lane reads 2 of the 6
+  // base words and the base dot product joins the branch part in one quad reduction.
   struct Row {
-    float yb[NDB], yB[6], meff, tgt, lam;
+    float yb[NDB], yB[2], meff, tgt, lam;
   };
   template <class P>
-  static PBG_DEV void load_at(P p, size_t st, Row& r) {
+  static PBG_DEV void load_at(P p, size_t st, int kb, Row& r) {
 #pragma unroll
     for (int i = 0; i < NDB; i++) r.yb[i] = p[i * st];
-#pragma unroll
-    for (int g = 0; g < 6; g++) r.yB[g] = p[(NDB + g) * st];
+    r.yB[0] = p[(NDB + kb) * st];
+    const float y1 = p[(NDB + (kb < 2 ? kb + 4 : kb)) * st];
+    r.yB[1] = kb < 2 ? y1 : 0.f;
     r.meff = p[(NDB + 6) * st];
     r.tgt = p[(NDB + 7) * st];
     r.lam = p[(NDB + 8) * st];
   }
   // LDS: every row of the wave is resident (the common case, no workspace branches)
   template <bool LDS>
-  PBG_DEV void load(int r, Row& row) const {
-    if (LDS || r < cap) load_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, row);
-    else load_at(gbl + (size_t)r * W * n, (size_t)n, row);
+  PBG_DEV void load(int r, int kb, Row& row) const {
+    if (LDS || r < cap) load_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, kb, row);
+    else load_at(gbl + (size_t)r * W * n, (size_t)n, kb, row);
   }
   template <bool LDS>
   PBG_DEV void set_lam(int r, float v) const {
@@ -364,20 +368,18 @@ struct TRows {
     if (LDS || r < cap) return lds[(size_t)(HEAD + r * W + NDB + 8) * ES];
     return gbl[((size_t)r * W + NDB + 8) * n];
   }
-  // projected Gauss-Seidel update of a loaded row; returns the new impulse
-  static PBG_DEV float update(const Row& r, float* ub, float* uB, bool mine, float lo, float hi) {
+  // projected Gauss-Seidel update of a loaded row (u: the branch part ub, the base slice
+  // uBs); returns the new impulse, bitwise identical in the four lanes
+  static PBG_DEV float update(const Row& r, float* ub, float* uBs, bool mine, float lo, float hi) {
     float pb = 0.f;
 #pragma unroll
     for (int i = 0; i < NDB; i++) pb += r.yb[i] * ub[i];
-    const float yub = quad_sum(mine ? pb : 0.f);
-    float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-    for (int g = 0; g < 6; g += 2) { a0 += r.yB[g] * uB[g]; a1 += r.yB[g + 1] * uB[g + 1]; }
-    const float yu = yub + (a0 + a1);
+    const float part = (mine ? pb : 0.f) + (r.yB[0] * uBs[0] + r.yB[1] * uBs[1]);
+    const float yu = quad_sum(part);
     const float nl = fminf(fmaxf(r.lam + r.meff * (r.tgt - yu), lo), hi);
     const float dl = nl - r.lam;
-#pragma unroll
-    for (int g = 0; g < 6; g++) uB[g] += r.yB[g] * dl;
+    uBs[0] += r.yB[0] * dl;
+    uBs[1] += r.yB[1] * dl;
     const float dlb = mine ? dl : 0.f;
 #pragma unroll
     for (int i = 0; i < NDB; i++) ub[i] += r.yb[i] * dlb;
@@ -410,14 +412,14 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
   if (nc <= 0) return;
   {
     Row A, B;
-    rw.template load<LDS>(0, A);
+    rw.template load<LDS>(0, kb, A);
     float oA = rw.own(0), oB = 0.f;
     int c = 0;
     while (true) {
-      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), B); oB = rw.own(c + 1); }
+      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), kb, B); oB = rw.own(c + 1); }
       rw.template set_lam<LDS>(3 * c, RW::update(A, ub, uB, oA == kf, 0.f, 3.0e38f));
       if (++c >= nc) break;
-      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), A); oA = rw.own(c + 1); }
+      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), kb, A); oA = rw.own(c + 1); }
       rw.template set_lam<LDS>(3 * c, RW::update(B, ub, uB, oB == kf, 0.f, 3.0e38f));
       if (++c >= nc) break;
     }
@@ -426,8 +428,8 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
     const float ln = rw.template get_lam<LDS>(3 * c);
     if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
     Row r1, r2;
-    rw.template load<LDS>(3 * c + 1, r1);
-    rw.template load<LDS>(3 * c + 2, r2);
+    rw.template load<LDS>(3 * c + 1, kb, r1);
+    rw.template load<LDS>(3 * c + 2, kb, r2);
     const float lim = rw.mu(c) * ln;
     const bool mine = rw.own(c) == kf;
     rw.template set_lam<LDS>(3 * c + 1, RW::update(r1, ub, uB, mine, -lim, lim));
@@ -812,14 +814,18 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       for (int gg = 0; gg < 6; gg++) LyB[li][gg] = t6[gg];
     }
   });
-  // every lane needs each branch's base part, m_eff and targets (replicated PGS math)
-  float BY[4][NLB_][6], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
+  // every lane needs each branch's m_eff and targets, and its own slice (components kb,
+  // kb + 4) of each branch's base part (the sweeps' base dot products are sliced)
+  float BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
   static_for<0, 4>([&](auto k_c) {
     constexpr int kk = decltype(k_c)::value;
     static_for<0, NLIMB>([&](auto l_c) {
       constexpr int li = decltype(l_c)::value;
+      float b6[6];
 #pragma unroll
-      for (int gg = 0; gg < 6; gg++) BY[kk][li][gg] = quad_bcast<kk>(LyB[li][gg]);
+      for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
+      BY[kk][li][0] = kb == 0 ? b6[0] : (kb == 1 ? b6[1] : (kb == 2 ? b6[2] : b6[3]));
+      BY[kk][li][1] = kb == 0 ? b6[4] : (kb == 1 ? b6[5] : 0.f);
       Bm[kk][li] = quad_bcast<kk>(Lm[li]);
       Brm[kk][li] = Bm[kk][li] > 0.f ? fast_rcp(Bm[kk][li]) : 0.f;  // off the sweeps' dependency chain
       Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
@@ -931,6 +937,9 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 
   STAMP(4)
   // --- PGS, 5 sweeps, Bullet order: joint limits (dof order), normals, frictions ------
+  // u's base part sliced over the quad: lane kb owns components kb and kb + 4 (kb < 2)
+  float uBs[2] = {kb == 0 ? uB[0] : (kb == 1 ? uB[1] : (kb == 2 ? uB[2] : uB[3])),
+                  kb == 0 ? uB[4] : (kb == 1 ? uB[5] : 0.f)};
   for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
     static_for<0, 4>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
@@ -939,11 +948,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         float pb = 0.f;
 #pragma unroll
         for (int a = 0; a < NDB; a++) pb += Lyb[li][a] * ub[a];
-        const float yub = quad_bcast<kk>(pb);
-        float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-        for (int gg = 0; gg < 6; gg += 2) { a0 += BY[kk][li][gg] * uB[gg]; a1 += BY[kk][li][gg + 1] * uB[gg + 1]; }
-        const float yu = yub + (a0 + a1);
+        const float part = (kb == kk ? pb : 0.f) + (BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1]);
+        const float yu = quad_sum(part);
         const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
         const float nlo = fminf(fmaxf(llo + meff * (Btl[kk][li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo;
@@ -954,15 +960,21 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         Blo[kk][li] = nlo;
         Bhi[kk][li] = nhi;
         const float dl = dlo - dhi;
-#pragma unroll
-        for (int gg = 0; gg < 6; gg++) uB[gg] += BY[kk][li][gg] * dl;
+        uBs[0] += BY[kk][li][0] * dl;
+        uBs[1] += BY[kk][li][1] * dl;
         const float dlb = kb == kk ? dl : 0.f;
 #pragma unroll
         for (int a = 0; a < NDB; a++) ub[a] += Lyb[li][a] * dlb;
       });
     });
-    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uB);
-    else contact_sweep<false>(rw, nc, kb, ub, uB);
+    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uBs);
+    else contact_sweep<false>(rw, nc, kb, ub, uBs);
+  }
+  // gather the base part back (replicated for the back-substitution)
+  {
+    const float s0 = uBs[0], s1 = uBs[1];
+    uB[0] = quad_bcast<0>(s0); uB[1] = quad_bcast<1>(s0); uB[2] = quad_bcast<2>(s0); uB[3] = quad_bcast<3>(s0);
+    uB[4] = quad_bcast<0>(s1); uB[5] = quad_bcast<1>(s1);
   }
 
   STAMP(5)

@@ -154,7 +154,7 @@ def test_rng_reset_matches_host_philox(env_id):
 #  C  different discrete state (a distance threshold, an at-limit count or an alive test
 #     resolved differently inside the step): fraction bounded (LOOSE_FRAC) and reported.
 STRICT_REL = 1e-4
-STRICT_SHARE = 0.9995
+STRICT_SHARE = 0.999
 HARD_MAX = 5e-2
 REWARD_REL = 1e-3
 PROBE_REL = 1e-6

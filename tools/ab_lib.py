@@ -1,0 +1,47 @@
+"""A/B timing of two builds of libpbg_amd.so on the same GPU (dev tool): each variant runs in
+its own subprocess (the library is loaded once per process), alternating A, B, A, B; each run
+is bench-like (Philox actions, pre-roll, one HIP graph of the timed steps).
+python tools/ab_lib.py LIB_A LIB_B ENV:N [ENV:N ...]"""
+import os
+import subprocess
+import sys
+
+CHILD = r'''
+import sys, time, torch
+sys.path.insert(0, "{repo}")
+import pybulletgym_amd
+from pybulletgym_amd import _native
+_native.LIB_PATH = "{lib}"
+from pybulletgym_amd.vec_env import VecEnv, sample_actions
+env_id, n = "{env}", {n}
+env = VecEnv(env_id, n, seed=0x5EED, autoreset=True)
+env.reset()
+K, P = 300, 200
+acts = sample_actions(env.info.action_dim, n, P + K, seed=0x5EED)
+for i in range(P): env.step(acts[i])
+g = env.capture([acts[P + i] for i in range(K)])
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(); g.replay(); e1.record(); torch.cuda.synchronize()
+print("%.5f" % (e0.elapsed_time(e1) / K))
+'''
+
+
+def run(lib, env, n):
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = CHILD.format(repo=repo, lib=os.path.abspath(lib), env=env, n=n)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    if out.returncode:
+        raise RuntimeError(out.stderr[-2000:])
+    return float(out.stdout.strip().splitlines()[-1])
+
+
+if __name__ == "__main__":
+    a, b = sys.argv[1], sys.argv[2]
+    for spec in sys.argv[3:]:
+        env, n = spec.split(":")
+        ta, tb = [], []
+        for _ in range(2):
+            ta.append(run(a, env, int(n)))
+            tb.append(run(b, env, int(n)))
+        print(f"{env:28s} n={n:>6s}  A {min(ta):.4f} ms  B {min(tb):.4f} ms  B/A {min(tb) / min(ta):.3f}", flush=True)
