@@ -59,8 +59,13 @@ if st:
                 out["trace_avg_ns"] = float(r["AverageNs"])
                 out["trace_calls"] = int(r["Calls"])
 if "FETCH_SIZE_median" in out and "WRITE_SIZE_median" in out:
-    out["hbm_bytes_per_launch"] = (2 * out["FETCH_SIZE_median"] + out["WRITE_SIZE_median"]) * 1024
-    out["correction"] = "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); kB = 1024 B"
+    with open(os.path.join(prof, "fetch_calibration.json")) as f:
+        cal = json.load(f)
+    out["hbm_bytes_per_launch"] = (cal["fetch_factor"] * out["FETCH_SIZE_median"]
+                                   + cal["write_dword_factor"] * out["WRITE_SIZE_median"]) * 1024
+    out["correction"] = (f"FETCH_SIZE x{cal['fetch_factor']}, WRITE_SIZE x{cal['write_dword_factor']}, measured for "
+                         "4 B/lane SoA dword loads/stores by tools/fetch_calib.hip (profiles/fetch_calibration.json); "
+                         "kB = 1024 B")
 if "SQ_INSTS_VALU_median" in out:
     out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_median"]
 if "SQ_INSTS_VALU_FMA_F32_median" in out:
