@@ -17,7 +17,7 @@ import pybulletgym_amd  # noqa: F401
 from pybulletgym_amd import distributed as pd, rng
 
 ENV = "AntPyBulletEnv-v0"
-N_GLOBAL, STEPS, SEED = 7, 4, 11  # 7 envs on 2 ranks: shards of 4 and 3
+N_GLOBAL, STEPS, SEED = 7, 4, 11  # 7 envs: uneven shards on 2 and 3 ranks
 
 
 class OracleShard:
@@ -81,18 +81,22 @@ def test_shard_range_covers_all():
                 assert o1 + c1 == o2
 
 
-def test_two_rank_sharded_vecenv_gather_matches_single_process():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_vecenv_gather_matches_single_process(world):
+    """Uneven shards (7 envs over 2 ranks: 4 + 3; over 3 ranks: 3 + 2 + 2) gather back to
+    the single-process trajectory bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     count0, flat_obs, flat_rew, flat_done = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert count0 == 4 and flat_obs.shape == (N_GLOBAL, 28) and flat_done.dtype == np.uint8
+    assert count0 == pd.shard_range(N_GLOBAL, 0, world)[1]
+    assert flat_obs.shape == (N_GLOBAL, 28) and flat_done.dtype == np.uint8
     ref = OracleShard(ENV, N_GLOBAL, "cpu", SEED, 0, True)
     ref.reset()
     for t in range(STEPS):
