@@ -37,9 +37,11 @@ namespace pbg {
 
 #define PBG_GANG_BLOCK 256  // lanes per gang workgroup (4 waves)
 
+// bound_ctrl set: every permutation used here reads a valid lane, and with it the
+// compiler folds `x + mov_dpp(x)` into one v_add_f32_dpp (no mov, no DPP hazard nop).
 template <int CTRL>
 PBG_DEV float dpp_f(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
 // all-reduce over the T (4, 8 or 16) lanes of a DPP row segment; identical bits in every
 // lane (each step adds a value and its mirror image: a + b == b + a)
@@ -54,7 +56,7 @@ PBG_DEV float gang_sum(float x) {
 PBG_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
 template <int CTRL>
 PBG_DEV uint32_t dpp_u(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
 }
 // integer sum over the T lanes of a DPP row segment (mod 2^32), same in every lane
 template <int T>

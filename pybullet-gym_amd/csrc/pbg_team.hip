@@ -23,13 +23,15 @@
 namespace pbg {
 
 // ------------------------------------------------------------------ quad (DPP) helpers
+// bound_ctrl set: every permutation used here reads a valid lane, and with it the
+// compiler folds `x + mov_dpp(x)` into one v_add_f32_dpp (no mov, no DPP hazard nop).
 template <int CTRL>
 PBG_DEV float qperm(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 PBG_DEV int qperm_i(int x) {
-  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);
 }
 // sum over the quad; identical bits in all four lanes ((x0+x1)+(x2+x3), addition commutes)
 PBG_DEV float quad_sum(float x) {
@@ -82,7 +84,7 @@ struct Team {
   static constexpr int NS0 = base_slots();
   static constexpr int NSB = B > 0 ? (R::NS - NS0) / B : 0;
   static constexpr int NC = R::NS;      // contact capacity
-  static constexpr int W = NDB + 9;     // contact row: y_b | y_base(6) | meff | target | lambda
+  static constexpr int W = 4 * NDB + 11;  // contact row: y_b (4 lane slots) | y_base (6 + 2 pad) | meff | target | lambda
   static constexpr int check() {
     if (!R::floating || (R::kind != 0 && R::kind != 3) || R::NPAIR != 0 || R::robot_body != -1 || B != 4) return false;
     if (NL % B || NJ % B || (R::NS - NS0) % B || NDB < 1 || NDB > 8) return false;
@@ -308,49 +310,58 @@ PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k
 }
 
 // ------------------------------------------------------------------ contact rows
-// Per env (shared by its quad): [mu (NC) | owner lane (NC) | rows], LDS [word][env] with
-// stride = envs per workgroup; rows beyond the LDS capacity in a device workspace
-// [word][env].  Row: y_branch (NDB, the owner's branch) | y_base (6) | meff | target | lambda.
+// Per env (shared by its quad): [mu (NC) | rows], LDS [word][env] with stride = envs per
+// workgroup; rows beyond the LDS capacity in a device workspace [word][env].
+// Row: y_branch in four lane slots (NDB words each; the owner branch's slot holds its y,
+// the other three zeros) | y_base (6) + 2 zero words | meff | target | lambda.  Every lane
+// reads its own slot and its base slice (components k, k + 4; words 6 and 7 are the zero
+// pad of lanes 2 and 3), so a row update needs no owner test: the dot products and the
+// axpy of the non-owner lanes see zeros.
 template <class R, int ES>
 struct TRows {
   using T = Team<R>;
   static constexpr int NDB = T::NDB, W = T::W, NC = T::NC, MR = 3 * T::NC;
-  static constexpr int HEAD = 2 * NC;
+  static constexpr int YB = 4 * NDB;  // first base word
+  static constexpr int HEAD = NC;
+  static_assert(NC <= 32, "contact_sweep keeps one bit per contact in a 32-bit mask");
   static constexpr int WORDS = MR * W;  // device workspace words per env
   lds_float* lds;  // LDS base + env slot
   float* gbl;      // workspace base + env
   int n;
   int cap;         // rows resident in LDS
   PBG_DEV lds_float& mu(int c) const { return lds[(size_t)c * ES]; }
-  PBG_DEV lds_float& own(int c) const { return lds[(size_t)(NC + c) * ES]; }
   PBG_DEV lds_float& stage(int w) const { return lds[(size_t)w * ES]; }
+  // slot: the writing lane's branch for a branch contact, -1 for a base contact (every
+  // lane writes the same words then)
   template <class P>
-  static PBG_DEV void put_at(P p, size_t st, const float* yb, const float* yB, float meff, float target) {
+  static PBG_DEV void put_at(P p, size_t st, int slot, const float* yb, const float* yB, float meff, float target) {
 #pragma unroll
-    for (int i = 0; i < NDB; i++) p[i * st] = yb[i];
+    for (int k = 0; k < 4; k++) {
 #pragma unroll
-    for (int g = 0; g < 6; g++) p[(NDB + g) * st] = yB[g];
-    p[(NDB + 6) * st] = meff;
-    p[(NDB + 7) * st] = target;
-    p[(NDB + 8) * st] = 0.f;
+      for (int i = 0; i < NDB; i++) p[(k * NDB + i) * st] = k == slot ? yb[i] : 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < 6; g++) p[(YB + g) * st] = yB[g];
+    p[(YB + 6) * st] = 0.f;
+    p[(YB + 7) * st] = 0.f;
+    p[(YB + 8) * st] = meff;
+    p[(YB + 9) * st] = target;
+    p[(YB + 10) * st] = 0.f;
   }
-  // One row in registers (loaded ahead of its update: PGS software pipelining).  The base
-  // part is sliced over the quad: lane k holds base components k and k + 4 (k < 2), the
-  // same components of u it owns in the sweeps (BaseSlice), so each lane reads 2 of the 6
-  // base words and the base dot product joins the branch part in one quad reduction.
+  // One row in registers (loaded ahead of its update: PGS software pipelining): this
+  // lane's branch slot and base slice.
   struct Row {
     float yb[NDB], yB[2], meff, tgt, lam;
   };
   template <class P>
   static PBG_DEV void load_at(P p, size_t st, int kb, Row& r) {
 #pragma unroll
-    for (int i = 0; i < NDB; i++) r.yb[i] = p[i * st];
-    r.yB[0] = p[(NDB + kb) * st];
-    const float y1 = p[(NDB + (kb < 2 ? kb + 4 : kb)) * st];
-    r.yB[1] = kb < 2 ? y1 : 0.f;
-    r.meff = p[(NDB + 6) * st];
-    r.tgt = p[(NDB + 7) * st];
-    r.lam = p[(NDB + 8) * st];
+    for (int i = 0; i < NDB; i++) r.yb[i] = p[(kb * NDB + i) * st];
+    r.yB[0] = p[(YB + kb) * st];
+    r.yB[1] = p[(YB + 4 + kb) * st];
+    r.meff = p[(YB + 8) * st];
+    r.tgt = p[(YB + 9) * st];
+    r.lam = p[(YB + 10) * st];
   }
   // LDS: every row of the wave is resident (the common case, no workspace branches)
   template <bool LDS>
@@ -360,34 +371,32 @@ struct TRows {
   }
   template <bool LDS>
   PBG_DEV void set_lam(int r, float v) const {
-    if (LDS || r < cap) lds[(size_t)(HEAD + r * W + NDB + 8) * ES] = v;
-    else gbl[((size_t)r * W + NDB + 8) * n] = v;
+    if (LDS || r < cap) lds[(size_t)(HEAD + r * W + YB + 10) * ES] = v;
+    else gbl[((size_t)r * W + YB + 10) * n] = v;
   }
   template <bool LDS>
   PBG_DEV float get_lam(int r) const {
-    if (LDS || r < cap) return lds[(size_t)(HEAD + r * W + NDB + 8) * ES];
-    return gbl[((size_t)r * W + NDB + 8) * n];
+    if (LDS || r < cap) return lds[(size_t)(HEAD + r * W + YB + 10) * ES];
+    return gbl[((size_t)r * W + YB + 10) * n];
   }
   // projected Gauss-Seidel update of a loaded row (u: the branch part ub, the base slice
   // uBs); returns the new impulse, bitwise identical in the four lanes
-  static PBG_DEV float update(const Row& r, float* ub, float* uBs, bool mine, float lo, float hi) {
-    float pb = 0.f;
+  static PBG_DEV float update(const Row& r, float* ub, float* uBs, float lo, float hi) {
+    float part = r.yB[0] * uBs[0] + r.yB[1] * uBs[1];
 #pragma unroll
-    for (int i = 0; i < NDB; i++) pb += r.yb[i] * ub[i];
-    const float part = (mine ? pb : 0.f) + (r.yB[0] * uBs[0] + r.yB[1] * uBs[1]);
+    for (int i = 0; i < NDB; i++) part += r.yb[i] * ub[i];
     const float yu = quad_sum(part);
     const float nl = fminf(fmaxf(r.lam + r.meff * (r.tgt - yu), lo), hi);
     const float dl = nl - r.lam;
     uBs[0] += r.yB[0] * dl;
     uBs[1] += r.yB[1] * dl;
-    const float dlb = mine ? dl : 0.f;
 #pragma unroll
-    for (int i = 0; i < NDB; i++) ub[i] += r.yb[i] * dlb;
+    for (int i = 0; i < NDB; i++) ub[i] += r.yb[i] * dl;
     return nl;
   }
-  PBG_DEV void put(int r, const float* yb, const float* yB, float meff, float target) const {
-    if (r < cap) put_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, yb, yB, meff, target);
-    else put_at(gbl + (size_t)r * W * n, (size_t)n, yb, yB, meff, target);
+  PBG_DEV void put(int r, int slot, const float* yb, const float* yB, float meff, float target) const {
+    if (r < cap) put_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, slot, yb, yB, meff, target);
+    else put_at(gbl + (size_t)r * W * n, (size_t)n, slot, yb, yB, meff, target);
   }
 };
 
@@ -403,37 +412,57 @@ PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
 
 // One PGS sweep over the contact rows in Bullet's order: all normals, then the two
 // friction rows of each contact whose normal impulse is positive, box-clamped at mu*lambda_n.
-// The next normal row is loaded before the current one is updated: two register buffers
-// alternate, so LDS latency overlaps the update arithmetic.
+// Rows are loaded one step ahead of their update (two register buffers alternate, so LDS
+// latency overlaps the previous update); the normal pass records which impulses came out
+// positive, so the friction pass walks those contacts without a load-then-test round trip.
 template <bool LDS, class RW>
 PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
   using Row = typename RW::Row;
-  const float kf = (float)kb;
   if (nc <= 0) return;
+  uint32_t pos = 0;
   {
     Row A, B;
     rw.template load<LDS>(0, kb, A);
-    float oA = rw.own(0), oB = 0.f;
     int c = 0;
     while (true) {
-      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), kb, B); oB = rw.own(c + 1); }
-      rw.template set_lam<LDS>(3 * c, RW::update(A, ub, uB, oA == kf, 0.f, 3.0e38f));
+      if (c + 1 < nc) rw.template load<LDS>(3 * (c + 1), kb, B);
+      float nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
+      rw.template set_lam<LDS>(3 * c, nl);
+      pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
-      if (c + 1 < nc) { rw.template load<LDS>(3 * (c + 1), kb, A); oA = rw.own(c + 1); }
-      rw.template set_lam<LDS>(3 * c, RW::update(B, ub, uB, oB == kf, 0.f, 3.0e38f));
+      if (c + 1 < nc) rw.template load<LDS>(3 * (c + 1), kb, A);
+      nl = RW::update(B, ub, uB, 0.f, 3.0e38f);
+      rw.template set_lam<LDS>(3 * c, nl);
+      pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
     }
   }
-  for (int c = 0; c < nc; c++) {
-    const float ln = rw.template get_lam<LDS>(3 * c);
-    if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
-    Row r1, r2;
-    rw.template load<LDS>(3 * c + 1, kb, r1);
-    rw.template load<LDS>(3 * c + 2, kb, r2);
-    const float lim = rw.mu(c) * ln;
-    const bool mine = rw.own(c) == kf;
-    rw.template set_lam<LDS>(3 * c + 1, RW::update(r1, ub, uB, mine, -lim, lim));
-    rw.template set_lam<LDS>(3 * c + 2, RW::update(r2, ub, uB, mine, -lim, lim));
+  // [EXT] friction rows only under a positive normal impulse
+  if (pos == 0u) return;
+  int c = __builtin_ctz(pos);
+  pos &= pos - 1u;
+  Row A1, A2;
+  rw.template load<LDS>(3 * c + 1, kb, A1);
+  rw.template load<LDS>(3 * c + 2, kb, A2);
+  float limA = rw.mu(c) * rw.template get_lam<LDS>(3 * c);
+  while (true) {
+    const bool more = pos != 0u;
+    const int c2 = more ? __builtin_ctz(pos) : c;
+    pos &= pos - 1u;
+    Row B1, B2;
+    float limB = 0.f;
+    if (more) {
+      rw.template load<LDS>(3 * c2 + 1, kb, B1);
+      rw.template load<LDS>(3 * c2 + 2, kb, B2);
+      limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
+    }
+    rw.template set_lam<LDS>(3 * c + 1, RW::update(A1, ub, uB, -limA, limA));
+    rw.template set_lam<LDS>(3 * c + 2, RW::update(A2, ub, uB, -limA, limA));
+    if (!more) break;
+    A1 = B1;
+    A2 = B2;
+    limA = limB;
+    c = c2;
   }
 }
 
@@ -816,11 +845,16 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
   // every lane needs each branch's m_eff and targets, and its own slice (components kb,
   // kb + 4) of each branch's base part (the sweeps' base dot products are sliced)
+  // (and its own branch part, zero in the lanes of the other branches: no owner test in
+  // the sweeps)
   float BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
+  float Byb[4][NLB_][NDB];
   static_for<0, 4>([&](auto k_c) {
     constexpr int kk = decltype(k_c)::value;
     static_for<0, NLIMB>([&](auto l_c) {
       constexpr int li = decltype(l_c)::value;
+#pragma unroll
+      for (int a = 0; a < NDB; a++) Byb[kk][li][a] = kb == kk ? Lyb[li][a] : 0.f;
       float b6[6];
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
@@ -859,11 +893,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       float z[NDB];
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
-      rw.put(3 * n0 + dir, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+      rw.put(3 * n0 + dir, -1, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
              dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
     }
     rw.mu(n0) = (float)R::slot_mu[sl];
-    rw.own(n0) = -1.f;
     n0++;
   });
   // this branch's active slots, then their contact indices (exclusive quad prefix)
@@ -920,11 +953,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
-      rw.put(3 * ci + dir, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+      rw.put(3 * ci + dir, kb, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
              dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
     }
     rw.mu(ci) = pk<T::SMU, sl>(L);
-    rw.own(ci) = (float)kb;
     ci++;
   });
   if (3 * nc > rw.cap) {  // rows in the device workspace: same-CU visibility
@@ -945,10 +977,9 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       constexpr int kk = decltype(k_c)::value;
       static_for<0, NLIMB>([&](auto l_c) {
         constexpr int li = decltype(l_c)::value;
-        float pb = 0.f;
+        float part = BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1];
 #pragma unroll
-        for (int a = 0; a < NDB; a++) pb += Lyb[li][a] * ub[a];
-        const float part = (kb == kk ? pb : 0.f) + (BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1]);
+        for (int a = 0; a < NDB; a++) part += Byb[kk][li][a] * ub[a];
         const float yu = quad_sum(part);
         const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
         const float nlo = fminf(fmaxf(llo + meff * (Btl[kk][li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
@@ -962,9 +993,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         const float dl = dlo - dhi;
         uBs[0] += BY[kk][li][0] * dl;
         uBs[1] += BY[kk][li][1] * dl;
-        const float dlb = kb == kk ? dl : 0.f;
 #pragma unroll
-        for (int a = 0; a < NDB; a++) ub[a] += Lyb[li][a] * dlb;
+        for (int a = 0; a < NDB; a++) ub[a] += Byb[kk][li][a] * dl;
       });
     });
     if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uBs);
