@@ -416,27 +416,31 @@ PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
 // latency overlaps the previous update); the normal pass records which impulses came out
 // positive, so the friction pass walks those contacts without a load-then-test round trip.
 template <bool LDS, class RW>
-PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
+PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SUB_STAMP_ARGS) {
   using Row = typename RW::Row;
   if (nc <= 0) return;
+  // The look-ahead loads are unconditional (the last row re-reads itself): a prefetch under a
+  // branch makes the compiler's LDS wait at the join conservative (lgkmcnt(0)), which
+  // serialises every row behind the next row's loads.
   uint32_t pos = 0;
   {
     Row A, B;
     rw.template load<LDS>(0, kb, A);
     int c = 0;
     while (true) {
-      if (c + 1 < nc) rw.template load<LDS>(3 * (c + 1), kb, B);
+      rw.template load<LDS>(3 * min(c + 1, nc - 1), kb, B);
       float nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
       rw.template set_lam<LDS>(3 * c, nl);
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
-      if (c + 1 < nc) rw.template load<LDS>(3 * (c + 1), kb, A);
+      rw.template load<LDS>(3 * min(c + 1, nc - 1), kb, A);
       nl = RW::update(B, ub, uB, 0.f, 3.0e38f);
       rw.template set_lam<LDS>(3 * c, nl);
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
     }
   }
+  STAMP(12)
   // [EXT] friction rows only under a positive normal impulse
   if (pos == 0u) return;
   int c = __builtin_ctz(pos);
@@ -450,12 +454,9 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB) {
     const int c2 = more ? __builtin_ctz(pos) : c;
     pos &= pos - 1u;
     Row B1, B2;
-    float limB = 0.f;
-    if (more) {
-      rw.template load<LDS>(3 * c2 + 1, kb, B1);
-      rw.template load<LDS>(3 * c2 + 2, kb, B2);
-      limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
-    }
+    rw.template load<LDS>(3 * c2 + 1, kb, B1);
+    rw.template load<LDS>(3 * c2 + 2, kb, B2);
+    const float limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
     rw.template set_lam<LDS>(3 * c + 1, RW::update(A1, ub, uB, -limA, limA));
     rw.template set_lam<LDS>(3 * c + 2, RW::update(A2, ub, uB, -limA, limA));
     if (!more) break;
@@ -997,8 +998,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         for (int a = 0; a < NDB; a++) ub[a] += Byb[kk][li][a] * dl;
       });
     });
-    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uBs);
-    else contact_sweep<false>(rw, nc, kb, ub, uBs);
+    STAMP(11)
+    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
+    else contact_sweep<false>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
+    STAMP(13)
   }
   // gather the base part back (replicated for the back-substitution)
   {

@@ -9,7 +9,8 @@ _native.LIB_PATH = os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd_stamps.so"
 from pybulletgym_amd.vec_env import VecEnv
 L = _native.lib()
 L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
-names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS", "integrate", "act+load", "pack", "store"]
+names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS (rest)", "integrate", "act+load", "pack",
+         "store", "-", "PGS limit rows", "PGS normals", "PGS frictions"]
 gang_names = {0: "phase A (kin, composites)", 1: "mass matrix", 3: "cholesky+solve", 10: "stage to LDS", 4: "detect",
               11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 8: "pack", 9: "store"}
 AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
@@ -17,7 +18,7 @@ for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] o
     env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET)
     env.reset()
     acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
-    for i in range(10): env.step(acts[i])
+    for i in range(200): env.step(acts[i % 30])  # pre-roll off the reset pose, as bench.py
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
     rid = _native.ROBOT_IDS[env_id]
