@@ -362,7 +362,7 @@ template <class T> inline T dotn(int n, const T* a, const T* b) {
 // normals, joint limits) use Bullet's rhs (btMultiBodyConstraintSolver::
 // setupMultiBodyContactConstraint: velocityError = -rel_vel, minus pos/dt when separated;
 // positionalError = -erp pos/dt when penetrating), i.e. J nu_new >= -pos/dt (separated,
-// speculative) or >= -erp pos/dt (penetrating); erp < 0: no positional term.  sep_abs = false
+// speculative) or >= -erp pos/dt (penetrating); erp < 0: no positional term (J nu_new >= 0).  sep_abs = false
 // is the round-1 relative form J dnu >= -pos/dt (kept for the rule study).
 template <class T>
 void setup_row(int n, const T L[MAXD][MAXD], const T* nu, RowT<T>& r, T pos, int positional, double erp, T dt,
@@ -373,7 +373,7 @@ void setup_row(int n, const T L[MAXD][MAXD], const T* nu, RowT<T>& r, T pos, int
   T vJ = dotn(n, r.J, nu);
   if (!positional) r.target = T(0);                                       // friction
   else if (pos > T(0)) r.target = (sep_abs ? T(0) : vJ) - pos / dt;         // [EXT] separated
-  else if (erp < 0) r.target = vJ;                                        // no positional term
+  else if (erp < 0) r.target = T(0);                                      // velocity only: J nu_new >= 0
   else r.target = T(0) - T(erp) * pos / dt;                               // Baumgarte push-out
   r.lambda = T(0);
 }

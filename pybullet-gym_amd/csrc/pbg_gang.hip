@@ -334,7 +334,7 @@ PBG_DEV f3 gang_O(const GangCtx& X) {
   return mk3(p[0], p[1], p[2]);
 }
 template <class R, int T>
-PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
+PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   using D = Dims<R>;
   using G = Gang<R, T>;
   auto& TD = GangTabs<R>::dyn(X.tabs);
@@ -420,6 +420,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
     }
     PBG_GANG_SYNC
   });
+  STAMP(0)
   const f3 O = gang_O<R, T>(X);
   // per-body inertia and wrench about O; motion vectors about O
 #pragma unroll 1
@@ -470,6 +471,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
     X.l[G::O_SV + 3 * i] = sv.x; X.l[G::O_SV + 3 * i + 1] = sv.y; X.l[G::O_SV + 3 * i + 2] = sv.z;
   }
   PBG_GANG_SYNC
+  STAMP(1)
   // composites: leaf-to-root over the levels (a body adds its children's sums)
   static_for<0, NLEV - 1>([&](auto k_c) {
     constexpr int lv = NLEV - 2 - decltype(k_c)::value;
@@ -491,6 +493,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X) {
     }
     PBG_GANG_SYNC
   });
+  STAMP(2)
   // packed lower triangle of M, then the bias (C_i = s_i . (N, F) of its composite)
 #pragma unroll 1
   for (int j = X.t; j < D::NNZ + N; j += T) {
@@ -551,7 +554,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   };
   if constexpr (DIST) {
     // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
-    gang_dyn_mass<R, T>(s, X);
+    gang_dyn_mass<R, T>(s, X SUB_STAMP_PASS);
     STAMP(3)
     // --- replicated: factorisation and the unconstrained velocity, staged for the rows ---
     float L[D::NNZ], rhs[N], Ld[N], nu[N], u[N];

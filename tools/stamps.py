@@ -11,11 +11,15 @@ L = _native.lib()
 L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
 names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS (rest)", "integrate", "act+load", "pack",
          "store", "-", "PGS limit rows", "PGS normals", "PGS frictions"]
-gang_names = {0: "phase A (kin, composites)", 1: "mass matrix", 3: "cholesky+solve", 10: "stage to LDS", 4: "detect",
+gang_names = {0: "dist: forward levels", 1: "dist: inertia + motion", 2: "dist: composites", 3: "dist: M + bias",
+              10: "replicated Cholesky + stage", 4: "detect",
               11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 8: "pack", 9: "store"}
 AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
-for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]))]:
-    env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET)
+# ENV:N[:GANG_DIST]  (GANG_DIST 0/1 forces the gang kernel's replicated / distributed dynamics)
+for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
+    env_id, n, *rest = spec.split(":")
+    n = int(n)
+    env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET, gang_dist=int(rest[0]) if rest else -1)
     env.reset()
     acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
     for i in range(200): env.step(acts[i % 30])  # pre-roll off the reset pose, as bench.py
