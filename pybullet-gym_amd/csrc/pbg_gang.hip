@@ -305,7 +305,7 @@ PBG_DEV float gang_row(const GangCtx& X, int c, int dir, float* us, float lo, fl
 #pragma unroll
   for (int m = 0; m < NSL; m++) part += y[m] * us[m];
   const float yu = gang_sum<T>(part);
-  const float nl = fminf(fmaxf(lam + meff * (tgt - yu), lo), hi);
+  const float nl = clampf(lam + meff * (tgt - yu), lo, hi);
   const float dl = nl - lam;
 #pragma unroll
   for (int m = 0; m < NSL; m++) us[m] += y[m] * dl;
@@ -805,11 +805,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         for (int m = 0; m < NSL; m++) part += ly[li][m] * us[m];
         const float yu = gang_sum<T>(part);
         const float meff = lm[li];
-        const float nlo = fminf(fmaxf(llo[li] + meff * (ltl[li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float nlo = clampf(llo[li] + meff * (ltl[li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo[li];
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
         const float yu2 = meff > 0.f ? yu + dlo * lrm[li] : yu;
-        const float nhi = fminf(fmaxf(lhi[li] + meff * (lth[li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float nhi = clampf(lhi[li] + meff * (lth[li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi[li];
         llo[li] = nlo;
         lhi[li] = nhi;

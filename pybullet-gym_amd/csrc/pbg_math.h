@@ -35,6 +35,10 @@ PBG_DEV float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 PBG_DEV float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 PBG_DEV float norm3(f3 a) { return fast_sqrt(dot3(a, a)); }
+// clamp(x, lo, hi) for lo <= hi in one v_med3_f32 (fminf(fmaxf()) costs two instructions
+// plus the IEEE canonicalisations of its operands); same result for non-NaN x
+PBG_DEV float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+
 
 // sin/cos for the moderate arguments of the physics (joint angles, exp-map half angles):
 // 3-part Cody-Waite reduction by pi/2 + minimax polynomials on [-pi/4, pi/4], a few ulp

@@ -394,7 +394,7 @@ struct Rows {
 #pragma unroll
     for (int i = 0; i < N; i++) acc[i & 3] += yv[i] * u[i];
     const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    const float nl = fminf(fmaxf(lam0 + meff * (tgt - yu), lo), hi);
+    const float nl = clampf(lam0 + meff * (tgt - yu), lo, hi);
     const float dl = nl - lam0;
     p[(N + 2) * st] = nl;
 #pragma unroll
@@ -683,7 +683,7 @@ PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld,
 #pragma unroll
   for (int i = 0; i < N; i++) {
     float t = nu[i] + dt * qdd[i];
-    nu[i] = fminf(fmaxf(t, -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    nu[i] = clampf(t, -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
   }
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -718,7 +718,7 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
     nu[i] = t * Ld[i];
   }
 #pragma unroll
-  for (int i = 0; i < N; i++) nu[i] = fminf(fmaxf(nu[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+  for (int i = 0; i < N; i++) nu[i] = clampf(nu[i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
 #pragma unroll
   for (int d = 0; d < NJ; d++) {
     s.qd[d] = nu[D::gj(d)];
@@ -949,11 +949,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       const float meff = rw.lim(off + np), tlo = rw.lim(off + np + 1), thi = rw.lim(off + np + 2);
       const float llo = rw.lim(off + np + 3), lhi = rw.lim(off + np + 4);
       const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      const float nlo = fminf(fmaxf(llo + meff * (tlo - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+      const float nlo = clampf(llo + meff * (tlo - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
       const float dlo = nlo - llo;
       // upper row sees u after the lower update: (-y).u' = -(yu + (y.y) dlo) = -(yu + dlo / meff)
       const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
-      const float nhi = fminf(fmaxf(lhi + meff * (thi + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+      const float nhi = clampf(lhi + meff * (thi + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
       const float dhi = nhi - lhi;
       rw.lim(off + np + 3) = nlo;
       rw.lim(off + np + 4) = nhi;

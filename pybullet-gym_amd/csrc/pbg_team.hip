@@ -386,7 +386,7 @@ struct TRows {
 #pragma unroll
     for (int i = 0; i < NDB; i++) part += r.yb[i] * ub[i];
     const float yu = quad_sum(part);
-    const float nl = fminf(fmaxf(r.lam + r.meff * (r.tgt - yu), lo), hi);
+    const float nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
     const float dl = nl - r.lam;
     uBs[0] += r.yB[0] * dl;
     uBs[1] += r.yB[1] * dl;
@@ -443,26 +443,33 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
   STAMP(12)
   // [EXT] friction rows only under a positive normal impulse
   if (pos == 0u) return;
+  // two register sets alternate (no copies between iterations)
   int c = __builtin_ctz(pos);
   pos &= pos - 1u;
-  Row A1, A2;
+  Row A1, A2, B1, B2;
   rw.template load<LDS>(3 * c + 1, kb, A1);
   rw.template load<LDS>(3 * c + 2, kb, A2);
-  float limA = rw.mu(c) * rw.template get_lam<LDS>(3 * c);
+  float limA = rw.mu(c) * rw.template get_lam<LDS>(3 * c), limB;
   while (true) {
-    const bool more = pos != 0u;
-    const int c2 = more ? __builtin_ctz(pos) : c;
+    bool more = pos != 0u;
+    int c2 = more ? __builtin_ctz(pos) : c;
     pos &= pos - 1u;
-    Row B1, B2;
     rw.template load<LDS>(3 * c2 + 1, kb, B1);
     rw.template load<LDS>(3 * c2 + 2, kb, B2);
-    const float limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
+    limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
     rw.template set_lam<LDS>(3 * c + 1, RW::update(A1, ub, uB, -limA, limA));
     rw.template set_lam<LDS>(3 * c + 2, RW::update(A2, ub, uB, -limA, limA));
     if (!more) break;
-    A1 = B1;
-    A2 = B2;
-    limA = limB;
+    c = c2;
+    more = pos != 0u;
+    c2 = more ? __builtin_ctz(pos) : c;
+    pos &= pos - 1u;
+    rw.template load<LDS>(3 * c2 + 1, kb, A1);
+    rw.template load<LDS>(3 * c2 + 2, kb, A2);
+    limA = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
+    rw.template set_lam<LDS>(3 * c + 1, RW::update(B1, ub, uB, -limB, limB));
+    rw.template set_lam<LDS>(3 * c + 2, RW::update(B2, ub, uB, -limB, limB));
+    if (!more) break;
     c = c2;
   }
 }
@@ -761,12 +768,12 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
     constexpr int a = T::lg(j);
-    nb[a] = fminf(fmaxf(s.qd[j] + dt * xb[a], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    nb[a] = clampf(s.qd[j] + dt * xb[a], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
   });
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    nB[i] = fminf(fmaxf(s.bv[i] + dt * xB[i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
-    nB[3 + i] = fminf(fmaxf(s.bw[i] + dt * xB[3 + i], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    nB[i] = clampf(s.bv[i] + dt * xB[i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    nB[3 + i] = clampf(s.bw[i] + dt * xB[3 + i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
   }
   float ub[NDB], uB[6];
   static_for<0, NDB>([&](auto a_c) {
@@ -983,11 +990,11 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         for (int a = 0; a < NDB; a++) part += Byb[kk][li][a] * ub[a];
         const float yu = quad_sum(part);
         const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
-        const float nlo = fminf(fmaxf(llo + meff * (Btl[kk][li] - yu), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo;
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
         const float yu2 = meff > 0.f ? yu + dlo * Brm[kk][li] : yu;
-        const float nhi = fminf(fmaxf(lhi + meff * (Bth[kk][li] + yu2), 0.f), (float)PBG_LIMIT_MAX_IMPULSE);
+        const float nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi;
         Blo[kk][li] = nlo;
         Bhi[kk][li] = nhi;
@@ -1016,7 +1023,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     constexpr int gg = 5 - decltype(r_c)::value;
     float t = uB[gg];
     static_for<gg + 1, 6>([&](auto h_c) { t -= Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
-    nB[gg] = fminf(fmaxf(t * Ldb[gg], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    nB[gg] = clampf(t * Ldb[gg], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
   });
   static_for<0, NDB>([&](auto r_c) {
     constexpr int a = NDB - 1 - decltype(r_c)::value;
@@ -1031,7 +1038,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
-    s.qd[j] = fminf(fmaxf(nb[T::lg(j)], -(float)PBG_MAX_COORD_VELOCITY), (float)PBG_MAX_COORD_VELOCITY);
+    s.qd[j] = clampf(nb[T::lg(j)], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
     s.q[j] += dt * s.qd[j];
   });
 #pragma unroll
