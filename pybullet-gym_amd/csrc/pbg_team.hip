@@ -123,6 +123,18 @@ struct Team {
   static constexpr bool anc(int a, int i) { return a == i || ((R::link_anc_mask[i] >> a) & 1u); }
   static constexpr bool owner(int i) { return R::link_dof[i] >= 0; }
   static constexpr bool in_chain(int a, int i) { return moves(dof_of(a), i); }  // gen a moves link i
+  // entry a of the branch part of limit row li (li-th limited dof of the branch) is
+  // structurally nonzero: y = L^-1 e_gd vanishes above gd and off gd's coupled dofs
+  static constexpr bool lim_nz(int li, int a) {
+    int j = 0, c = 0;
+    for (int jj = 0; jj < NDB; jj++)
+      if (R::dof_limited[jj]) {
+        if (c == li) j = jj;
+        c++;
+      }
+    const int gd = lg(j);
+    return !(a < gd || !coupled(a, gd));
+  }
 
   // per-branch constants
   static constexpr BTab<NLB * 3> vec3(const double (*t)[3]) {
@@ -986,14 +998,16 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       static_for<0, NLIMB>([&](auto l_c) {
         constexpr int li = decltype(l_c)::value;
         float part = BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1];
-#pragma unroll
-        for (int a = 0; a < NDB; a++) part += Byb[kk][li][a] * ub[a];
+        static_for<0, NDB>([&](auto a_c) {  // structural zeros of the row skipped
+          constexpr int a = decltype(a_c)::value;
+          if constexpr (T::lim_nz(li, a)) part += Byb[kk][li][a] * ub[a];
+        });
         const float yu = quad_sum(part);
         const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
         const float nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo;
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const float yu2 = meff > 0.f ? yu + dlo * Brm[kk][li] : yu;
+        const float yu2 = yu + dlo * Brm[kk][li];  // Brm = 0 when meff = 0
         const float nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi;
         Blo[kk][li] = nlo;
@@ -1001,8 +1015,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         const float dl = dlo - dhi;
         uBs[0] += BY[kk][li][0] * dl;
         uBs[1] += BY[kk][li][1] * dl;
-#pragma unroll
-        for (int a = 0; a < NDB; a++) ub[a] += Byb[kk][li][a] * dl;
+        static_for<0, NDB>([&](auto a_c) {
+          constexpr int a = decltype(a_c)::value;
+          if constexpr (T::lim_nz(li, a)) ub[a] += Byb[kk][li][a] * dl;
+        });
       });
     });
     STAMP(11)
