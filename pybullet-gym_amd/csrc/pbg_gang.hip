@@ -201,6 +201,95 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
 }
 template <class R>
 __constant__ GangDynTab<R> g_gang_dyn = make_gang_dyn_tab<R>();
+// the same table as a compile-time value (level-round code indexes it with constant bodies)
+template <class R>
+struct GangDT {
+  static constexpr GangDynTab<R> v = make_gang_dyn_tab<R>();
+};
+
+// Per-lane selection of compile-time constants.  In a round of a level the lanes t < KN own
+// the compile-time bodies Src::at(t).  ksel(t, fn) is fn(body) for this lane's body -- a
+// select chain over KN compile-time constants, or the constant itself when every body of the
+// round agrees (then kmul / mulc fold it: an identity offset rotation, a zero anchor or a
+// shared joint axis costs nothing).  fn gets the body as std::integral_constant.
+template <class Src, int KN, class V, class F>
+PBG_DEV V ksel(int t, F&& fn) {
+  V v = (V)fn(std::integral_constant<int, Src::at(KN - 1)>{});
+  static_for<0, KN - 1>([&](auto i_c) {
+    constexpr int k = KN - 2 - decltype(i_c)::value;
+    const V a = (V)fn(std::integral_constant<int, Src::at(k)>{});
+    v = t == k ? a : v;
+  });
+  return v;
+}
+// bodies of the tree level starting at lev_body[K0]
+template <class R, int K0>
+struct LevSrc {
+  static constexpr int at(int k) { return GangDT<R>::v.lev_body[K0 + k]; }
+};
+template <class R, int K0, int KN, class F>
+PBG_DEV float lvsel(int t, F&& fn) { return ksel<LevSrc<R, K0>, KN, float>(t, fn); }
+template <class R, int K0, int KN, class F>
+PBG_DEV int lvsel_i(int t, F&& fn) { return ksel<LevSrc<R, K0>, KN, int>(t, fn); }
+// opaque copy of the lane index: the lane compares of the selects stay where they are used
+// (hoisted out of the sub-step loop, their masks pinned SGPRs for the whole kernel and spilled)
+PBG_DEV int opaque_lane(int t) {
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// composites pass: per level, the bodies that have children (a leaf's composite is its own)
+template <class R>
+struct GangComp {
+  static constexpr int NB = R::NL + 1;
+  struct Tab {
+    int cnt[NB + 1];
+    int body[NB + 1][NB];
+    int nch[NB];
+    int ch[NB][NB];
+  };
+  static constexpr Tab make() {
+    Tab t{};
+    for (int b = 0; b < NB; b++) {
+      for (int c = 1; c < NB; c++)
+        if (R::link_parent[c - 1] + 1 == b) t.ch[b][t.nch[b]++] = c;
+      if (t.nch[b] > 0) {
+        const int lv = body_depth<R>(b);
+        t.body[lv][t.cnt[lv]++] = b;
+      }
+    }
+    return t;
+  }
+  static constexpr Tab v = make();
+  static constexpr int maxch(int lv, int k0, int kn) {
+    int m = 0;
+    for (int k = 0; k < kn; k++) m = v.nch[v.body[lv][k0 + k]] > m ? v.nch[v.body[lv][k0 + k]] : m;
+    return m;
+  }
+};
+template <class R, int LV, int K0>
+struct CompSrc {
+  static constexpr int at(int k) { return GangComp<R>::v.body[LV][K0 + k]; }
+};
+
+// joint type shared by the round's bodies, or -1 when they differ
+template <class R>
+constexpr int lv_jt(int k0, int kn) {
+  const int j = GangDT<R>::v.jt[GangDT<R>::v.lev_body[k0]];
+  for (int k = 1; k < kn; k++)
+    if (GangDT<R>::v.jt[GangDT<R>::v.lev_body[k0 + k]] != j) return -1;
+  return j;
+}
+// A * B where B's entries may be compile-time constants (its zeros fold away)
+PBG_DEV m3 mul_kb(const m3& A, const m3& B) {
+  m3 C;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      C.m[3 * i + j] = kmul(B.m[j], A.m[3 * i]) + kmul(B.m[3 + j], A.m[3 * i + 1]) + kmul(B.m[6 + j], A.m[3 * i + 2]);
+  return C;
+}
 
 // ------------------------------------------------------------------ layout
 template <class R, int T>
@@ -333,6 +422,102 @@ PBG_DEV f3 gang_O(const GangCtx& X) {
   const lds_float* p = body_word<R, T>(X.l, rb, 12);
   return mk3(p[0], p[1], p[2]);
 }
+// Forward kinematics / velocities / bias accelerations of one round of a tree level: lane
+// t < KN owns body lev_body[K0 + t] (compile-time), reads its parent's record from LDS and
+// writes its own.  Model constants are selected per lane (lvsel), so constants shared by the
+// round's bodies fold (the lane kernel's kmul rules).
+#define PBG_LV(expr) lvsel<R, K0, KN>(t, [&](auto bc_) { constexpr int b = decltype(bc_)::value; return (expr); })
+#define PBG_LVI(expr) lvsel_i<R, K0, KN>(t, [&](auto bc_) { constexpr int b = decltype(bc_)::value; return (expr); })
+template <class R, int T, int K0, int KN>
+PBG_DEV void gang_fk_round(const GangCtx& X) {
+  using G = Gang<R, T>;
+  using DTh = GangDT<R>;
+  constexpr int JT = lv_jt<R>(K0, KN);
+  const int t = opaque_lane(X.t);
+  if (t >= KN) return;
+  const int body = PBG_LVI(b), p = PBG_LVI(DTh::v.parent[b]), d = PBG_LVI(DTh::v.dof[b]);
+  const lds_float* P = body_word<R, T>(X.l, p, 0);
+  const lds_float* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
+  m3 Rp, Ro;
+#pragma unroll
+  for (int i = 0; i < 9; i++) Rp.m[i] = P[i];
+  static_for<0, 9>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
+    Ro.m[i] = PBG_LV(DTh::v.ro[b][i]);
+  });
+  const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(PK[12], PK[13], PK[14]), wp = mk3(PK[15], PK[16], PK[17]);
+  const f3 vp = mk3(PK[18], PK[19], PK[20]), alp = mk3(PK[21], PK[22], PK[23]), acp = mk3(PK[24], PK[25], PK[26]);
+  const m3 R0 = mul_kb(Rp, Ro);
+  const f3 x0 = xp + mulc(Rp, PBG_LV(DTh::v.opos[b][0]), PBG_LV(DTh::v.opos[b][1]), PBG_LV(DTh::v.opos[b][2]));
+  const f3 axl = mk3(PBG_LV(DTh::v.axis[b][0]), PBG_LV(DTh::v.axis[b][1]), PBG_LV(DTh::v.axis[b][2]));
+  const f3 anl = mk3(PBG_LV(DTh::v.anchor[b][0]), PBG_LV(DTh::v.anchor[b][1]), PBG_LV(DTh::v.anchor[b][2]));
+  const f3 com = mk3(PBG_LV(DTh::v.com[b][0]), PBG_LV(DTh::v.com[b][1]), PBG_LV(DTh::v.com[b][2]));
+  auto kin = [&](auto jt_c) {
+    constexpr int jt = decltype(jt_c)::value;
+    const float q = jt != 4 ? X.l[G::O_Q + d] : 0.f, qd = jt != 4 ? X.l[G::O_QD + d] : 0.f;
+    m3 Rm = R0;
+    f3 x = x0, w, v, al, ac, c;
+    if constexpr (jt == 0) {
+      float sn, cs;
+      sincos_fast(q, &sn, &cs);
+      const float t1 = 1.f - cs;
+      m3 Rj;
+      const float axx = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][0]), ayy = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][1]);
+      const float azz = PBG_LV(DTh::v.axis[b][2] * DTh::v.axis[b][2]), axy = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][1]);
+      const float axz = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][2]), ayz = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][2]);
+      Rj.m[0] = kmul(axx, t1) + cs;                 Rj.m[1] = kmul(axy, t1) - kmul(axl.z, sn); Rj.m[2] = kmul(axz, t1) + kmul(axl.y, sn);
+      Rj.m[3] = kmul(axy, t1) + kmul(axl.z, sn);    Rj.m[4] = kmul(ayy, t1) + cs;              Rj.m[5] = kmul(ayz, t1) - kmul(axl.x, sn);
+      Rj.m[6] = kmul(axz, t1) - kmul(axl.y, sn);    Rj.m[7] = kmul(ayz, t1) + kmul(axl.x, sn); Rj.m[8] = kmul(azz, t1) + cs;
+      Rm = mul_kb(R0, Rj);
+      const f3 rja = mulc(Rj, anl);
+      x = x0 + mulc(R0, anl - rja);
+      c = x + mulc(Rm, com);
+      const f3 a = mulc(R0, axl);
+      const f3 o = x0 + mulc(R0, anl);
+      const f3 ro = o - cp;
+      const f3 vo = vp + cross3(wp, ro);
+      const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+      w = wp + qd * a;
+      al = alp + qd * cross3(wp, a);
+      const f3 rc = c - o;
+      v = vo + cross3(w, rc);
+      ac = ao + cross3(al, rc) + cross3(w, cross3(w, rc));
+      X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
+      X.l[G::O_JO + 3 * d] = o.x; X.l[G::O_JO + 3 * d + 1] = o.y; X.l[G::O_JO + 3 * d + 2] = o.z;
+    } else if constexpr (jt == 1) {
+      const f3 a = mulc(R0, axl);
+      x = x0 + q * a;
+      c = x + mulc(Rm, com);
+      const f3 r = c - cp;
+      w = wp;
+      al = alp;
+      v = vp + cross3(wp, r) + qd * a;
+      ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * qd) * cross3(wp, a);
+      X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
+      X.l[G::O_JO + 3 * d] = x0.x; X.l[G::O_JO + 3 * d + 1] = x0.y; X.l[G::O_JO + 3 * d + 2] = x0.z;
+    } else {
+      c = x + mulc(Rm, com);
+      const f3 r = c - cp;
+      w = wp;
+      al = alp;
+      v = vp + cross3(wp, r);
+      ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
+    }
+    const float rec[G::BW] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
+                              x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z};
+#pragma unroll
+    for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, body, i) = rec[i];
+  };
+  if constexpr (JT >= 0) {
+    kin(std::integral_constant<int, JT>{});
+  } else {
+    const int jt = PBG_LVI(DTh::v.jt[b]);
+    if (jt == 0) kin(std::integral_constant<int, 0>{});
+    else if (jt == 1) kin(std::integral_constant<int, 1>{});
+    else kin(std::integral_constant<int, 4>{});
+  }
+}
+
 template <class R, int T>
 PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   using D = Dims<R>;
@@ -358,73 +543,20 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   // forward pass, one level at a time (a body's parent is one level up)
   static_for<1, NLEV>([&](auto lv_c) {
     constexpr int lv = decltype(lv_c)::value;
-#pragma unroll 1
-    for (int idx = TD.lev_start[lv] + X.t; idx < TD.lev_start[lv + 1]; idx += T) {
-      const int b = TD.lev_body[idx], p = TD.parent[b], jt = TD.jt[b], d = TD.dof[b];
-      const lds_float* P = body_word<R, T>(X.l, p, 0);
-      const lds_float* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
-      m3 Rp, Ro;
-#pragma unroll
-      for (int i = 0; i < 9; i++) { Rp.m[i] = P[i]; Ro.m[i] = TD.ro[b][i]; }
-      const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(PK[12], PK[13], PK[14]), wp = mk3(PK[15], PK[16], PK[17]);
-      const f3 vp = mk3(PK[18], PK[19], PK[20]), alp = mk3(PK[21], PK[22], PK[23]), acp = mk3(PK[24], PK[25], PK[26]);
-      const m3 R0 = mul(Rp, Ro);
-      const f3 x0 = xp + mul(Rp, mk3(TD.opos[b][0], TD.opos[b][1], TD.opos[b][2]));
-      const f3 axl = mk3(TD.axis[b][0], TD.axis[b][1], TD.axis[b][2]);
-      const f3 anl = mk3(TD.anchor[b][0], TD.anchor[b][1], TD.anchor[b][2]);
-      const float q = d >= 0 ? X.l[G::O_Q + d] : 0.f, qd = d >= 0 ? X.l[G::O_QD + d] : 0.f;
-      m3 Rm = R0;
-      f3 x = x0;
-      if (jt == 0) {
-        const m3 Rj = axis_angle_m3(axl.x, axl.y, axl.z, q);
-        Rm = mul(R0, Rj);
-        x = x0 + mul(R0, anl - mul(Rj, anl));
-      } else if (jt == 1) {
-        x = x0 + q * mul(R0, axl);
-      }
-      const f3 c = x + mul(Rm, mk3(TD.com[b][0], TD.com[b][1], TD.com[b][2]));
-      f3 w, v, al, ac;
-      if (jt == 0) {
-        const f3 a = mul(R0, axl);
-        const f3 o = x0 + mul(R0, anl);
-        const f3 ro = o - cp;
-        const f3 vo = vp + cross3(wp, ro);
-        const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
-        w = wp + qd * a;
-        al = alp + qd * cross3(wp, a);
-        const f3 rc = c - o;
-        v = vo + cross3(w, rc);
-        ac = ao + cross3(al, rc) + cross3(w, cross3(w, rc));
-        X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
-        X.l[G::O_JO + 3 * d] = o.x; X.l[G::O_JO + 3 * d + 1] = o.y; X.l[G::O_JO + 3 * d + 2] = o.z;
-      } else if (jt == 1) {
-        const f3 a = mul(R0, axl);
-        const f3 r = c - cp;
-        w = wp;
-        al = alp;
-        v = vp + cross3(wp, r) + qd * a;
-        ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * qd) * cross3(wp, a);
-        X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
-        X.l[G::O_JO + 3 * d] = x0.x; X.l[G::O_JO + 3 * d + 1] = x0.y; X.l[G::O_JO + 3 * d + 2] = x0.z;
-      } else {
-        const f3 r = c - cp;
-        w = wp;
-        al = alp;
-        v = vp + cross3(wp, r);
-        ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
-      }
-      const float rec[G::BW] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
-                                x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z};
-#pragma unroll
-      for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, b, i) = rec[i];
-    }
+    constexpr int K0 = GangDT<R>::v.lev_start[lv], NBL = GangDT<R>::v.lev_start[lv + 1] - K0;
+    static_for<0, (NBL + T - 1) / T>([&](auto r_c) {
+      constexpr int r = decltype(r_c)::value;
+      gang_fk_round<R, T, K0 + r * T, (NBL - r * T < T ? NBL - r * T : T)>(X);
+    });
     PBG_GANG_SYNC
   });
   STAMP(0)
   const f3 O = gang_O<R, T>(X);
   // per-body inertia and wrench about O; motion vectors about O
-#pragma unroll 1
-  for (int b = X.t; b < NB; b += T) {
+#pragma unroll
+  for (int r_ = 0; r_ < (NB + T - 1) / T; r_++) {  // rounds unrolled: table loads of all rounds overlap
+    const int b = r_ * T + X.t;
+    if (b >= NB) continue;
     const lds_float* P = body_word<R, T>(X.l, b, 0);
     const lds_float* PK = body_word<R, T>(X.l, b, G::FW) - G::FW;
     m3 Rm;
@@ -451,8 +583,10 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
 #pragma unroll
     for (int i = 0; i < G::CW; i++) C[i] = massive ? cmp[i] : 0.f;
   }
-#pragma unroll 1
-  for (int i = X.t; i < N; i += T) {
+#pragma unroll
+  for (int r_ = 0; r_ < (N + T - 1) / T; r_++) {
+    const int i = r_ * T + X.t;
+    if (i >= N) continue;
     const int d = TD.g_dof[i];
     f3 sw, sv;
     if (d >= 0) {
@@ -475,28 +609,40 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   // composites: leaf-to-root over the levels (a body adds its children's sums)
   static_for<0, NLEV - 1>([&](auto k_c) {
     constexpr int lv = NLEV - 2 - decltype(k_c)::value;
-#pragma unroll 1
-    for (int idx = TD.lev_start[lv] + X.t; idx < TD.lev_start[lv + 1]; idx += T) {
-      const int b = TD.lev_body[idx];
-      lds_float* C = X.l + G::O_CP + G::CW * b;
-      float acc[G::CW];
+    using GC = GangComp<R>;
+    constexpr int NBL = GC::v.cnt[lv];
+    static_for<0, (NBL + T - 1) / T>([&](auto r_c) {
+      constexpr int K0 = decltype(r_c)::value * T, KN = NBL - K0 < T ? NBL - K0 : T;
+      constexpr int MC = GC::maxch(lv, K0, KN);
+      using S = CompSrc<R, lv, K0>;
+      const int t = opaque_lane(X.t);
+      if (t < KN) {
+        const int b = ksel<S, KN, int>(t, [&](auto bc) { return decltype(bc)::value; });
+        lds_float* C = X.l + G::O_CP + G::CW * b;
+        float acc[G::CW];
 #pragma unroll
-      for (int i = 0; i < G::CW; i++) acc[i] = C[i];
-#pragma unroll 1
-      for (int j = TD.child_start[b]; j < TD.child_start[b + 1]; j++) {
-        const lds_float* K = X.l + G::O_CP + G::CW * TD.child[j];
+        for (int i = 0; i < G::CW; i++) acc[i] = C[i];
+        static_for<0, MC>([&](auto j_c) {
+          constexpr int j = decltype(j_c)::value;
+          const int c = ksel<S, KN, int>(t, [&](auto bc) { return j < GC::v.nch[decltype(bc)::value] ? GC::v.ch[decltype(bc)::value][j] : -1; });
+          if (c >= 0) {
+            const lds_float* K = X.l + G::O_CP + G::CW * c;
 #pragma unroll
-        for (int i = 0; i < G::CW; i++) acc[i] += K[i];
+            for (int i = 0; i < G::CW; i++) acc[i] += K[i];
+          }
+        });
+#pragma unroll
+        for (int i = 0; i < G::CW; i++) C[i] = acc[i];
       }
-#pragma unroll
-      for (int i = 0; i < G::CW; i++) C[i] = acc[i];
-    }
+    });
     PBG_GANG_SYNC
   });
   STAMP(2)
   // packed lower triangle of M, then the bias (C_i = s_i . (N, F) of its composite)
-#pragma unroll 1
-  for (int j = X.t; j < D::NNZ + N; j += T) {
+#pragma unroll
+  for (int r_ = 0; r_ < (D::NNZ + N + T - 1) / T; r_++) {
+    const int j = r_ * T + X.t;
+    if (j >= D::NNZ + N) continue;
     if (j < D::NNZ) {
       const int gi = TD.me_i[j], gk = TD.me_k[j], bk = TD.me_b[j];
       const lds_float* C = X.l + G::O_CP + G::CW * bk;
@@ -612,6 +758,23 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   const uint64_t gang_mask = ((T == 64) ? ~0ull : ((1ull << T) - 1ull)) << (X.le * T);
   const uint64_t below = (1ull << (X.le * T + X.t)) - 1ull;
   int nc = 0;
+  // --- distributed: capsule ends of the self-collision geoms in world coordinates, one geom
+  // per lane, in the limit-row area (dead until the rows pass); read by the pair pass ------
+  constexpr int O_GE = G::O_LR;
+  static_assert(R::NPAIR == 0 || 6 * R::NG <= G::LRSZ, "geom ends exceed the limit-row area");
+  if constexpr (R::NPAIR > 0) {
+    static_for<0, (R::NG + T - 1) / T>([&](auto r_c) {
+      const int g = decltype(r_c)::value * T + X.t;
+      if (g < R::NG) {
+        m3 Rm; f3 x;
+        frame(TB.geom_body[g], Rm, x);
+        const f3 e0 = x + mul(Rm, mk3(TB.gp0[g][0], TB.gp0[g][1], TB.gp0[g][2]));
+        const f3 e1 = x + mul(Rm, mk3(TB.gp1[g][0], TB.gp1[g][1], TB.gp1[g][2]));
+        lds_float* e = X.l + O_GE + 6 * g;
+        e[0] = e0.x; e[1] = e0.y; e[2] = e0.z; e[3] = e1.x; e[4] = e1.y; e[5] = e1.z;
+      }
+    });
+  }
   // --- distributed: floor slots (slot order) ---------------------------------------------
   uint64_t sb = 0;
   static_for<0, G::ROUNDS_S>([&](auto r_c) {
@@ -641,8 +804,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   slot_bits = sb;
   // --- distributed: self-collision pairs (pair order) ------------------------------------
   if constexpr (R::NPAIR > 0) {
-#pragma unroll 1
-    for (int r = 0; r < (R::NPAIR + T - 1) / T; r++) {
+    PBG_GANG_SYNC  // the geom ends
+#pragma unroll
+    for (int r = 0; r < (R::NPAIR + T - 1) / T; r++) {  // rounds unrolled: their loads overlap
       const int pp = r * T + X.t;
       bool act = false;
       f3 PA, PB, nrm;
@@ -650,13 +814,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       int ga = 0, gb = 0;
       if (pp < R::NPAIR) {
         ga = TB.pga[pp]; gb = TB.pgb[pp];
-        m3 Ra; f3 xa, xb; m3 Rb;
-        frame(TB.geom_body[ga], Ra, xa);
-        frame(TB.geom_body[gb], Rb, xb);
-        const f3 a0 = xa + mul(Ra, mk3(TB.gp0[ga][0], TB.gp0[ga][1], TB.gp0[ga][2]));
-        const f3 a1 = xa + mul(Ra, mk3(TB.gp1[ga][0], TB.gp1[ga][1], TB.gp1[ga][2]));
-        const f3 b0 = xb + mul(Rb, mk3(TB.gp0[gb][0], TB.gp0[gb][1], TB.gp0[gb][2]));
-        const f3 b1 = xb + mul(Rb, mk3(TB.gp1[gb][0], TB.gp1[gb][1], TB.gp1[gb][2]));
+        const lds_float* ea = X.l + O_GE + 6 * ga;
+        const lds_float* eb = X.l + O_GE + 6 * gb;
+        const f3 a0 = mk3(ea[0], ea[1], ea[2]), a1 = mk3(ea[3], ea[4], ea[5]);
+        const f3 b0 = mk3(eb[0], eb[1], eb[2]), b1 = mk3(eb[3], eb[4], eb[5]);
         const f3 dc = (a0 + a1) - (b0 + b1);
         if (dot3(dc, dc) <= TB.pbound2[pp]) {
           // closest points of two segments (same branch structure as the lane kernel)
