@@ -371,41 +371,138 @@ PBG_DEV float cget(const GangCtx& X, int c, int w) {
   return X.g[(size_t)c * G::PERC + w];
 }
 
-// one PGS update of contact row (c, dir) with u sliced over the gang: returns the new
-// impulse (same bits in every lane) and updates this lane's slice.
+// A contact row in registers (loaded one step ahead of its update: PGS software
+// pipelining): this lane's slice of y, m_eff, target, lambda.
 template <class R, int T>
-PBG_DEV float gang_row(const GangCtx& X, int c, int dir, float* us, float lo, float hi, float* lam_out) {
+struct GRow {
+  float y[Gang<R, T>::NSL], meff, tgt, lam;
+};
+// row (c, dir); LDS: the caller knows every row of the wave is LDS-resident (no branch, so
+// the compiler's LDS wait before the next update counts only this row's loads)
+template <class R, int T, bool LDS>
+PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
   using G = Gang<R, T>;
-  constexpr int NSL = G::NSL;
   const int w0 = G::DW + 1 + dir * G::CRW;
-  float y[NSL], meff, tgt, lam;
-  if (c < X.cap) {
+  if (LDS || c < X.cap) {
     const lds_float* p = X.l + G::FIXED + c * G::PERC + w0;
 #pragma unroll
-    for (int m = 0; m < NSL; m++) y[m] = p[X.t + m * T];
-    meff = p[G::YS]; tgt = p[G::YS + 1]; lam = p[G::YS + 2];
+    for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t + m * T];
+    r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   } else {
     const float* p = X.g + (size_t)c * G::PERC + w0;
 #pragma unroll
-    for (int m = 0; m < NSL; m++) y[m] = p[X.t + m * T];
-    meff = p[G::YS]; tgt = p[G::YS + 1]; lam = p[G::YS + 2];
+    for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t + m * T];
+    r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   }
+}
+template <class R, int T, bool LDS>
+PBG_DEV float gang_load_word(const GangCtx& X, int c, int w) {
+  using G = Gang<R, T>;
+  if (LDS || c < X.cap) return X.l[G::FIXED + c * G::PERC + w];
+  return X.g[(size_t)c * G::PERC + w];
+}
+template <class R, int T, bool LDS>
+PBG_DEV void gang_set_lam(const GangCtx& X, int c, int dir, float v) {
+  using G = Gang<R, T>;
+  const int w = G::DW + 1 + dir * G::CRW + G::YS + 2;
+  if (X.t == 0) {
+    if (LDS || c < X.cap) X.l[G::FIXED + c * G::PERC + w] = v;
+    else X.g[(size_t)c * G::PERC + w] = v;
+  }
+}
+// PGS update of a loaded row with u sliced over the gang; the new impulse has the same bits
+// in every lane
+template <class R, int T>
+PBG_DEV float gang_update(const GRow<R, T>& r, float* us, float lo, float hi) {
   float part = 0.f;
 #pragma unroll
-  for (int m = 0; m < NSL; m++) part += y[m] * us[m];
+  for (int m = 0; m < Gang<R, T>::NSL; m++) part += r.y[m] * us[m];
   const float yu = gang_sum<T>(part);
-  const float nl = clampf(lam + meff * (tgt - yu), lo, hi);
-  const float dl = nl - lam;
+  const float nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
+  const float dl = nl - r.lam;
 #pragma unroll
-  for (int m = 0; m < NSL; m++) us[m] += y[m] * dl;
-  *lam_out = lam;
+  for (int m = 0; m < Gang<R, T>::NSL; m++) us[m] += r.y[m] * dl;
   return nl;
 }
-
-template <class R, int T>
-PBG_DEV void set_row_lam(const GangCtx& X, int c, int dir, float v) {
+// One PGS sweep over the contact rows in Bullet's order: all normals, then the two friction
+// rows of each contact whose normal impulse came out positive [EXT], box-clamped at
+// mu * lambda_n.  Rows are loaded one step ahead of their update (two register sets
+// alternate); the look-ahead loads are unconditional (a finished gang re-reads a valid row),
+// and the normal pass records the positive impulses in a bitmask, so the friction pass walks
+// those contacts without a load-then-test round trip.  The loop runs while any gang of the
+// wave has rows left; a finished gang skips the updates.
+template <class R, int T, bool LDS>
+PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
   using G = Gang<R, T>;
-  if (X.t == 0) cput<R, T>(X, c, G::DW + 1 + dir * G::CRW + G::YS + 2, v);
+  using Row = GRow<R, T>;
+  static_assert(G::MAXC <= 128, "positive-normal mask holds 128 contacts");
+  uint64_t pos0 = 0, pos1 = 0;
+  {
+    Row A, B;
+    gang_load_row<R, T, LDS>(X, 0, 0, A);
+    int c = 0;
+    while (wave_any(c < nc)) {
+      gang_load_row<R, T, LDS>(X, max(0, min(c + 1, nc - 1)), 0, B);
+      if (c < nc) {
+        const float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        const uint64_t bit = nl > 0.f ? 1ull << (c & 63) : 0ull;
+        if (c < 64) pos0 |= bit; else pos1 |= bit;
+      }
+      if (!wave_any(++c < nc)) break;
+      gang_load_row<R, T, LDS>(X, max(0, min(c + 1, nc - 1)), 0, A);
+      if (c < nc) {
+        const float nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        const uint64_t bit = nl > 0.f ? 1ull << (c & 63) : 0ull;
+        if (c < 64) pos0 |= bit; else pos1 |= bit;
+      }
+      ++c;
+    }
+  }
+  // next contact with a positive normal impulse (-1: none left)
+  auto next = [&]() -> int {
+    if (pos0) { const int c = __builtin_ctzll(pos0); pos0 &= pos0 - 1ull; return c; }
+    if (pos1) { const int c = 64 + __builtin_ctzll(pos1); pos1 &= pos1 - 1ull; return c; }
+    return -1;
+  };
+  constexpr int WN = G::DW + 1 + G::YS + 2;  // the normal row's lambda
+  int c = next();
+  if (!wave_any(c >= 0)) return;
+  Row A1, A2, B1, B2;
+  float limA, limB;
+  {
+    const int cc = max(c, 0);
+    gang_load_row<R, T, LDS>(X, cc, 1, A1);
+    gang_load_row<R, T, LDS>(X, cc, 2, A2);
+    limA = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
+  }
+  while (true) {
+    int c2 = next();
+    {
+      const int cc = max(c2, 0);
+      gang_load_row<R, T, LDS>(X, cc, 1, B1);
+      gang_load_row<R, T, LDS>(X, cc, 2, B2);
+      limB = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
+    }
+    if (c >= 0) {
+      gang_set_lam<R, T, LDS>(X, c, 1, gang_update<R, T>(A1, us, -limA, limA));
+      gang_set_lam<R, T, LDS>(X, c, 2, gang_update<R, T>(A2, us, -limA, limA));
+    }
+    if (!wave_any(c2 >= 0)) break;
+    c = next();
+    {
+      const int cc = max(c, 0);
+      gang_load_row<R, T, LDS>(X, cc, 1, A1);
+      gang_load_row<R, T, LDS>(X, cc, 2, A2);
+      limA = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
+    }
+    if (c2 >= 0) {
+      gang_set_lam<R, T, LDS>(X, c2, 1, gang_update<R, T>(B1, us, -limB, limB));
+      gang_set_lam<R, T, LDS>(X, c2, 2, gang_update<R, T>(B2, us, -limB, limB));
+    }
+    if (!wave_any(c >= 0)) break;
+  }
 }
 
 // Distributed unconstrained dynamics of one sub-step (the gang counterpart of dyn_mass):
@@ -958,6 +1055,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       lrm[li] = lm[li] > 0.f ? fast_rcp(lm[li]) : 0.f;  // off the sweeps' dependency chain
       llo[li] = 0.f; lhi[li] = 0.f;
     }
+    const bool all_lds = !wave_any(nc > X.cap);  // every contact row of the wave in LDS
     for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
 #pragma unroll
       for (int li = 0; li < NLIM; li++) {
@@ -978,25 +1076,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #pragma unroll
         for (int m = 0; m < NSL; m++) us[m] += ly[li][m] * dl;
       }
-#pragma unroll 1
-      for (int c = 0; wave_any(c < nc); c++) {  // contact normals
-        if (c >= nc) continue;
-        float lam;
-        const float nl = gang_row<R, T>(X, c, 0, us, 0.f, 3.0e38f, &lam);
-        set_row_lam<R, T>(X, c, 0, nl);
-      }
-#pragma unroll 1
-      for (int c = 0; wave_any(c < nc); c++) {  // frictions, only under a positive normal impulse [EXT]
-        if (c >= nc) continue;
-        const float ln = cget<R, T>(X, c, G::DW + 1 + G::YS + 2);
-        if (!(ln > 0.f)) continue;
-        const float lim = cget<R, T>(X, c, G::DW) * ln;
-        float lam;
-        float nl = gang_row<R, T>(X, c, 1, us, -lim, lim, &lam);
-        set_row_lam<R, T>(X, c, 1, nl);
-        nl = gang_row<R, T>(X, c, 2, us, -lim, lim, &lam);
-        set_row_lam<R, T>(X, c, 2, nl);
-      }
+      if (all_lds) gang_contact_sweep<R, T, true>(X, nc, us);
+      else gang_contact_sweep<R, T, false>(X, nc, us);
     }
   }
   // --- replicated: gather u, back-substitute, integrate ----------------------------------
