@@ -93,9 +93,9 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
-    // distributed dynamics for deep trees (Humanoid) or more than one wave per SIMD (its
+    // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
-    g->gang_dist = RR::NDOF >= 16 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
+    g->gang_dist = RR::NDOF >= 8 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
     if (g->force_dist == 0 || g->force_dist == 1) g->gang_dist = g->force_dist;  // pbg_create_debug
     g->team = 16;
     g->block = PBG_GANG_BLOCK;

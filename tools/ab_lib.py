@@ -1,7 +1,7 @@
 """A/B timing of two builds of libpbg_amd.so on the same GPU (dev tool): each variant runs in
 its own subprocess (the library is loaded once per process), alternating A, B, A, B; each run
 is bench-like (Philox actions, pre-roll, one HIP graph of the timed steps).
-python tools/ab_lib.py LIB_A LIB_B ENV:N [ENV:N ...]"""
+python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST] ..."""
 import os
 import subprocess
 import sys
@@ -14,7 +14,7 @@ from pybulletgym_amd import _native
 _native.LIB_PATH = "{lib}"
 from pybulletgym_amd.vec_env import VecEnv, sample_actions
 env_id, n = "{env}", {n}
-env = VecEnv(env_id, n, seed=0x5EED, autoreset=True)
+env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, gang_dist={gd})
 env.reset()
 K, P = 300, 200
 acts = sample_actions(env.info.action_dim, n, P + K, seed=0x5EED)
@@ -27,9 +27,9 @@ print("%.5f" % (e0.elapsed_time(e1) / K))
 '''
 
 
-def run(lib, env, n):
+def run(lib, env, n, gd=-1):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = CHILD.format(repo=repo, lib=os.path.abspath(lib), env=env, n=n)
+    code = CHILD.format(repo=repo, lib=os.path.abspath(lib), env=env, n=n, gd=gd)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if out.returncode:
         raise RuntimeError(out.stderr[-2000:])
@@ -39,9 +39,10 @@ def run(lib, env, n):
 if __name__ == "__main__":
     a, b = sys.argv[1], sys.argv[2]
     for spec in sys.argv[3:]:
-        env, n = spec.split(":")
+        env, n, *gd = spec.split(":")  # ENV:N[:GANG_DIST]
+        gd = int(gd[0]) if gd else -1
         ta, tb = [], []
         for _ in range(2):
-            ta.append(run(a, env, int(n)))
-            tb.append(run(b, env, int(n)))
+            ta.append(run(a, env, int(n), gd))
+            tb.append(run(b, env, int(n), gd))
         print(f"{env:28s} n={n:>6s}  A {min(ta):.4f} ms  B {min(tb):.4f} ms  B/A {min(tb) / min(ta):.3f}", flush=True)

@@ -10,7 +10,7 @@ if [ -n "$K" ]; then
   echo "tests rc=$rc" >> $OUT/tests.log; tail -3 $OUT/tests.log
   case $rc in 0|5) ;; *) exit $rc;; esac
 fi
-timeout -k 10 500 python tools/ab_lib.py ab/base.so pybullet-gym_amd/libpbg_amd.so "$@" > $OUT/ab.log 2>&1; rc=$?
+timeout -k 10 500 python tools/ab_lib.py ${BASE:-ab/base.so} pybullet-gym_amd/libpbg_amd.so "$@" > $OUT/ab.log 2>&1; rc=$?
 cat $OUT/ab.log; [ $rc = 0 ] || exit $rc
 if [ -f pybullet-gym_amd/libpbg_amd_stamps.so ]; then
   timeout -k 10 200 python tools/stamps.py "$@" > $OUT/stamps.log 2>&1; rc=$?; cat $OUT/stamps.log; exit $rc
