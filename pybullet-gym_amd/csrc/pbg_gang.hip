@@ -1206,7 +1206,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
-    else flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
+    else flag_pack<R, 4>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, X.t);
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }

@@ -1045,8 +1045,23 @@ struct PackOut {
 
 // robot_locomotors.py:31-64 calc_state + gym_locomotion_envs.py:59-114 reward/done.
 // GEN: any part count (golden-vector pack_kernel); otherwise the step's NP or NP + 1 parts.
-template <class R, bool GEN = false>
-PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, PackOut& out) {
+// Broadcast lane K of each DPP quad (a float64 as two dword moves).
+template <int K>
+PBG_DEV double quad_bcast_f64(double x) {
+  constexpr int CTRL = K * 85;  // quad_perm [K, K, K, K]
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Q = 4: the four lanes of each DPP quad hold the same env and identical inputs (quad and
+// gang kernels); the float64 transcendentals are dealt over them -- lane 0 roll, 1 pitch,
+// 2 yaw, 3 target angle (atan2 / asin), then lanes 0-1 sin/cos(-yaw) and 2-3 sin/cos(ang)
+// -- and broadcast back: the same library calls on the same arguments, so the same bits as
+// Q = 1, for two atan2 and one sin/cos pair less per pack.
+template <class R, bool GEN = false, int Q = 1>
+PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, PackOut& out, int lane = 0) {
   float j[2 * (R::NO > 0 ? R::NO : 1)];
 #pragma unroll
   for (int i = 0; i < R::NO; i++) {
@@ -1077,20 +1092,43 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   const double bz = in.pos[2];
   const double* q = in.quat;
   const double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
-  const double roll = atan2(2 * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+  const double ry = 2 * (q[1] * q[2] + q[3] * q[0]), rx = squ - sqx - sqy + sqz;
   const double sarg = -2 * (q[0] * q[2] - q[3] * q[1]);
-  const double pitch = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
-  const double yaw = atan2(2 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+  const double yy = 2 * (q[0] * q[1] + q[3] * q[2]), yx = squ + sqx - sqy - sqz;
   const double z0 = isnan(in.initial_z) ? bz : in.initial_z;
   const double dy = in.target_y - by, dx = in.target_x - bx;
-  const double theta = atan2(dy, dx);
+  double roll, pitch, yaw, theta, cy, sy, sa, ca;
+  if constexpr (Q == 4) {
+    const int k = lane & 3;
+    double r;
+    if (k == 1) r = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
+    else r = atan2(k == 0 ? ry : (k == 2 ? yy : dy), k == 0 ? rx : (k == 2 ? yx : dx));
+    roll = quad_bcast_f64<0>(r);
+    pitch = quad_bcast_f64<1>(r);
+    yaw = quad_bcast_f64<2>(r);
+    theta = quad_bcast_f64<3>(r);
+    const double arg = k < 2 ? -yaw : theta - yaw;
+    const double sv = sin(arg), cv = cos(arg);
+    sy = quad_bcast_f64<0>(sv);
+    cy = quad_bcast_f64<0>(cv);
+    sa = quad_bcast_f64<2>(sv);
+    ca = quad_bcast_f64<2>(cv);
+  } else {
+    (void)lane;
+    roll = atan2(ry, rx);
+    pitch = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
+    yaw = atan2(yy, yx);
+    theta = atan2(dy, dx);
+    cy = cos(-yaw);
+    sy = sin(-yaw);
+    sa = sin(theta - yaw);
+    ca = cos(theta - yaw);
+  }
   const double dist = sqrt(dy * dy + dx * dx);
-  const double ang = theta - yaw;
-  const double cy = cos(-yaw), sy = sin(-yaw);
   const double vx = cy * in.vel[0] + -sy * in.vel[1] + 0.0 * in.vel[2];
   const double vy = sy * in.vel[0] + cy * in.vel[1] + 0.0 * in.vel[2];
   const double vz = 0.0 * in.vel[0] + 0.0 * in.vel[1] + 1.0 * in.vel[2];
-  const float more[8] = {(float)(bz - z0), (float)sin(ang), (float)cos(ang), (float)(0.3 * vx),
+  const float more[8] = {(float)(bz - z0), (float)sa, (float)ca, (float)(0.3 * vx),
                          (float)(0.3 * vy), (float)(0.3 * vz), (float)roll, (float)pitch};
   bool has_nan = false;
   int o = 0;
@@ -1164,20 +1202,20 @@ PBG_DEV void flag_draw(const Buffers& B, int e, Flag& f) {
 // calc_state with HumanoidFlagrun's bookkeeping (:219-226): count the timeout down, pack
 // against the current flag, and if the target is within 1 m or the timeout ran out, re-draw
 // (`redraw(f)`) and pack again against the new flag.  Other robots: plain walker_pack.
-template <class R, class Redraw>
-PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po, Flag& f, Redraw&& redraw) {
+template <class R, int Q = 1, class Redraw>
+PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po, Flag& f, Redraw&& redraw, int lane = 0) {
   if constexpr (R::flagrun) {
     f.timeout -= 1;
     in.target_x = f.tx; in.target_y = f.ty;
-    walker_pack<R>(in, act, obs, po);
-    if (po.dist < 1.0 || f.timeout <= 0) {
+    walker_pack<R, false, Q>(in, act, obs, po, lane);
+    if (po.dist < 1.0 || f.timeout <= 0) {  // env-uniform: a quad takes it together
       redraw(f);
       in.target_x = f.tx; in.target_y = f.ty;
-      walker_pack<R>(in, act, obs, po);
+      walker_pack<R, false, Q>(in, act, obs, po, lane);
     }
   } else {
     (void)f; (void)redraw;
-    walker_pack<R>(in, act, obs, po);
+    walker_pack<R, false, Q>(in, act, obs, po, lane);
   }
 }
 template <class R>

@@ -1261,7 +1261,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
-    else walker_pack<R>(in, act, obs, po);
+    else walker_pack<R, false, 4>(in, act, obs, po, kb);
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
   STAMP(8)
