@@ -184,10 +184,12 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def timed_rollout(make_env, env_id, n, steps, warmup, preroll, dev, rank, world, no_graph):
-    """Rollout of n envs on this device: preroll + warmup untimed steps, then exactly `steps`
-    timed steps bracketed by a barrier + device sync on both sides.  Returns (env, elapsed_s
-    max over ranks, kernel_ms per launch, launches per graph)."""
+def timed_rollout(make_env, env_id, n, steps, warmup, preroll, dev, rank, world, no_graph, windows=1):
+    """Rollout of n envs on this device: preroll + warmup untimed steps, then `windows` timed
+    windows of exactly `steps` steps, each bracketed by a barrier + device sync on both sides
+    (the same captured action batches replayed; the envs keep stepping).  Returns (env,
+    elapsed_s, kernel_ms per launch, launches per graph, per-window ms per step): the median
+    window, its time the max over ranks."""
     import torch
     import torch.distributed as dist
     env = make_env(env_id, n, dev, ACTION_SEED, rank * n, True)
@@ -215,39 +217,43 @@ def timed_rollout(make_env, env_id, n, steps, warmup, preroll, dev, rank, world,
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)] \
             if no_graph else None
-    _sync(dev)
-    if world > 1:
-        dist.barrier()
-    _sync(dev)
-    t0 = time.perf_counter()
-    if timing:
-        e0.record(stream)
-    if dev.type == "cuda" and not no_graph:
-        for g in graphs:
-            g.replay()
-    else:
-        for i in range(steps):
-            if timing:
-                ev[i][0].record(stream)
-            env.step(acts[t_first + i])
-            if timing:
-                ev[i][1].record(stream)
-    if timing:
-        e1.record(stream)
-    _sync(dev)
-    if world > 1:
-        dist.barrier()
-    _sync(dev)
-    elapsed = time.perf_counter() - t0
-    if timing:
-        kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) if no_graph else e0.elapsed_time(e1)) / steps
-    else:
-        kernel_ms = elapsed / steps * 1e3
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-    return env, elapsed, kernel_ms, G
+    runs = []
+    for _ in range(windows):
+        _sync(dev)
+        if world > 1:
+            dist.barrier()
+        _sync(dev)
+        t0 = time.perf_counter()
+        if timing:
+            e0.record(stream)
+        if dev.type == "cuda" and not no_graph:
+            for g in graphs:
+                g.replay()
+        else:
+            for i in range(steps):
+                if timing:
+                    ev[i][0].record(stream)
+                env.step(acts[t_first + i])
+                if timing:
+                    ev[i][1].record(stream)
+        if timing:
+            e1.record(stream)
+        _sync(dev)
+        if world > 1:
+            dist.barrier()
+        _sync(dev)
+        elapsed = time.perf_counter() - t0
+        if timing:
+            kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) if no_graph else e0.elapsed_time(e1)) / steps
+        else:
+            kernel_ms = elapsed / steps * 1e3
+        if world > 1:
+            t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, kernel_ms = float(t[0]), float(t[1])
+        runs.append((elapsed, kernel_ms))
+    elapsed, kernel_ms = sorted(runs)[len(runs) // 2]
+    return env, elapsed, kernel_ms, G, [r[0] / steps * 1e3 for r in runs]
 
 
 def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
@@ -278,7 +284,9 @@ def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--windows", type=int, default=5,
+                    help="timed windows of --steps steps each; value and ms_per_step are the median window")
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--preroll", type=int, default=200, help="untimed steps before the warm-up (episode aging)")
     ap.add_argument("--envs-per-gpu", type=int, default=ENVS_PER_GPU)
@@ -323,8 +331,9 @@ def main():
 
     flops = load_flops()
     n = args.envs_per_gpu
-    env, elapsed, kernel_ms, G = timed_rollout(make_env, args.env, n, args.steps, args.warmup, args.preroll, dev,
-                                               rank, world, args.no_graph)
+    env, elapsed, kernel_ms, G, windows_ms = timed_rollout(make_env, args.env, n, args.steps, args.warmup,
+                                                           args.preroll, dev, rank, world, args.no_graph,
+                                                           windows=args.windows)
     head = leg_summary(env, world, n, args.steps, elapsed, kernel_ms, flops)
 
     gather_ms = None
@@ -344,8 +353,8 @@ def main():
             eid, cnt = spec.split(":")
             if eid == args.env:
                 continue
-            e2, el2, km2, _ = timed_rollout(make_env, eid, int(cnt), args.leg_steps, min(args.warmup, 20),
-                                            args.preroll, dev, rank, world, args.no_graph)
+            e2, el2, km2, _, _ = timed_rollout(make_env, eid, int(cnt), args.leg_steps, min(args.warmup, 20),
+                                               args.preroll, dev, rank, world, args.no_graph)
             legs[SHORT.get(eid, eid)] = leg_summary(e2, world, int(cnt), args.leg_steps, el2, km2, flops)
             e2.close()
 
@@ -358,6 +367,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "timed_windows": len(windows_ms),
+            "window_ms_per_step": windows_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
