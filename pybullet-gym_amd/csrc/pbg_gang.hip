@@ -357,18 +357,15 @@ struct GangTabs {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
   }
 
-// contact c, word w: LDS if resident, else the device workspace
-template <class R, int T>
-PBG_DEV void cput(const GangCtx& X, int c, int w, float v) {
+// f(p) with p the first word of contact c: its LDS record if resident, else its device
+// workspace record -- one branch for a whole record's loads or stores (a per-word
+// accessor left one divergent branch per word in the code: 442 branches in the detection
+// pass, 186 in the rows pass)
+template <class R, int T, class F>
+PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
   using G = Gang<R, T>;
-  if (c < X.cap) X.l[G::FIXED + c * G::PERC + w] = v;
-  else X.g[(size_t)c * G::PERC + w] = v;
-}
-template <class R, int T>
-PBG_DEV float cget(const GangCtx& X, int c, int w) {
-  using G = Gang<R, T>;
-  if (c < X.cap) return X.l[G::FIXED + c * G::PERC + w];
-  return X.g[(size_t)c * G::PERC + w];
+  if (c < X.cap) f(X.l + G::FIXED + c * G::PERC);
+  else f(X.g + (size_t)c * G::PERC);
 }
 
 // A contact row in registers (loaded one step ahead of its update: PGS software
@@ -848,9 +845,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   auto put_desc = [&](int c, f3 rA, f3 rB, f3 n, float dist, float fB, uint32_t mA, uint32_t mB, float floor_, float mu) {
     const float v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, 1.f, fB,
                             __builtin_bit_cast(float, mA), __builtin_bit_cast(float, mB), floor_, 0.f};
+    contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
-    for (int w = 0; w < G::DW; w++) cput<R, T>(X, c, w, v[w]);
-    cput<R, T>(X, c, G::DW, mu);
+      for (int w = 0; w < G::DW; w++) p[w] = v[w];
+      p[G::DW] = mu;
+    });
   };
   const uint64_t gang_mask = ((T == 64) ? ~0ull : ((1ull << T) - 1ull)) << (X.le * T);
   const uint64_t below = (1ull << (X.le * T + X.t)) - 1ull;
@@ -974,8 +973,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       c = (j - NLIM) / 3;
       dir = (j - NLIM) - 3 * c;
       float v[G::DW];
+      contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
-      for (int w = 0; w < G::DW; w++) v[w] = cget<R, T>(X, c, w);
+        for (int w = 0; w < G::DW; w++) v[w] = p[w];
+      });
       const f3 rA = mk3(v[0], v[1], v[2]), rB = mk3(v[3], v[4], v[5]), nrm = mk3(v[6], v[7], v[8]);
       dist = v[9];
       const float fB = v[11];
@@ -1028,12 +1029,15 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       p[YS + 2] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
     } else {
       const int w0r = G::DW + 1 + dir * G::CRW;
+      const float tgt = dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f;
+      contact_at<R, T>(X, c, [&](auto p0) {
+        auto p = p0 + w0r;
 #pragma unroll
-      for (int i = 0; i < YS; i++) cput<R, T>(X, c, w0r + i, i < N ? y[i] : 0.f);
-      cput<R, T>(X, c, w0r + YS, meff);
-      cput<R, T>(X, c, w0r + YS + 1,
-                 dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
-      cput<R, T>(X, c, w0r + YS + 2, 0.f);
+        for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
+        p[YS] = meff;
+        p[YS + 1] = tgt;
+        p[YS + 2] = 0.f;
+      });
     }
   }
   PBG_GANG_SYNC
