@@ -5,6 +5,7 @@
 
 #define PBG_DEV __device__ __forceinline__
 
+#include <type_traits>
 #include <utility>
 
 // Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Guarantees a
