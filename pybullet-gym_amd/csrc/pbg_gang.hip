@@ -764,36 +764,45 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     PBG_GANG_SYNC
   });
   STAMP(2)
-  // packed lower triangle of M, then the bias (C_i = s_i . (N, F) of its composite)
+  // per generalized index k (one per lane): f_k = I^c s_k of its composite (angular |
+  // linear part) into the dead kinematic area past the reference body's record (gang_O
+  // still reads that), and the bias C_k = s_k . (N, F) of the same composite
+  constexpr int O_FK = G::O_KV + G::KW * (Dims<R>::REF_BODY + 1);
+  static_assert(G::KW * (Dims<R>::REF_BODY + 1) + 6 * N <= G::MIN_CONTACT_WORDS, "f_k past the kinematic area");
 #pragma unroll
-  for (int r_ = 0; r_ < (D::NNZ + N + T - 1) / T; r_++) {
+  for (int r_ = 0; r_ < (N + T - 1) / T; r_++) {
+    const int k = r_ * T + X.t;
+    if (k >= N) continue;
+    const int bk = TD.g_body[k], d = TD.g_dof[k];
+    const lds_float* C = X.l + G::O_CP + G::CW * bk;
+    s6 J;
+#pragma unroll
+    for (int i = 0; i < 6; i++) J.a[i] = C[i];
+    const f3 p1 = mk3(C[6], C[7], C[8]);
+    const float cm = C[15];
+    const f3 swk = mk3(X.l[G::O_SW + 3 * k], X.l[G::O_SW + 3 * k + 1], X.l[G::O_SW + 3 * k + 2]);
+    const f3 svk = mk3(X.l[G::O_SV + 3 * k], X.l[G::O_SV + 3 * k + 1], X.l[G::O_SV + 3 * k + 2]);
+    const f3 Jw_ = mul(J, swk) + cross3(p1, svk);
+    const f3 Fv = cm * svk - cross3(p1, swk);
+    lds_float* f = X.l + O_FK + 6 * k;
+    f[0] = Jw_.x; f[1] = Jw_.y; f[2] = Jw_.z; f[3] = Fv.x; f[4] = Fv.y; f[5] = Fv.z;
+    const f3 F = mk3(C[9], C[10], C[11]), Nn = mk3(C[12], C[13], C[14]);
+    float r = -(dot3(swk, Nn) + dot3(svk, F));
+    if (d >= 0) r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
+    X.l[G::O_RHS + k] = r;
+  }
+  PBG_GANG_SYNC
+  // packed lower triangle of M: M_ik = s_i . f_k (+ armature)
+#pragma unroll
+  for (int r_ = 0; r_ < (D::NNZ + T - 1) / T; r_++) {
     const int j = r_ * T + X.t;
-    if (j >= D::NNZ + N) continue;
-    if (j < D::NNZ) {
-      const int gi = TD.me_i[j], gk = TD.me_k[j], bk = TD.me_b[j];
-      const lds_float* C = X.l + G::O_CP + G::CW * bk;
-      s6 J;
-#pragma unroll
-      for (int i = 0; i < 6; i++) J.a[i] = C[i];
-      const f3 p1 = mk3(C[6], C[7], C[8]);
-      const float cm = C[15];
-      const f3 swk = mk3(X.l[G::O_SW + 3 * gk], X.l[G::O_SW + 3 * gk + 1], X.l[G::O_SW + 3 * gk + 2]);
-      const f3 svk = mk3(X.l[G::O_SV + 3 * gk], X.l[G::O_SV + 3 * gk + 1], X.l[G::O_SV + 3 * gk + 2]);
-      const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
-      const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
-      const f3 Jw_ = mul(J, swk) + cross3(p1, svk);
-      const f3 Fv = cm * svk - cross3(p1, swk);
-      X.l[G::O_L + j] = (dot3(swi, Jw_) + dot3(svi, Fv)) + TD.me_arm[j];
-    } else {
-      const int gi = j - D::NNZ, bi = TD.g_body[gi], d = TD.g_dof[gi];
-      const lds_float* C = X.l + G::O_CP + G::CW * bi;
-      const f3 F = mk3(C[9], C[10], C[11]), Nn = mk3(C[12], C[13], C[14]);
-      const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
-      const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
-      float r = -(dot3(swi, Nn) + dot3(svi, F));
-      if (d >= 0) r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
-      X.l[G::O_RHS + gi] = r;
-    }
+    if (j >= D::NNZ) continue;
+    const int gi = TD.me_i[j], gk = TD.me_k[j];
+    const lds_float* f = X.l + O_FK + 6 * gk;
+    const f3 Jw_ = mk3(f[0], f[1], f[2]), Fv = mk3(f[3], f[4], f[5]);
+    const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
+    const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
+    X.l[G::O_L + j] = (dot3(swi, Jw_) + dot3(svi, Fv)) + TD.me_arm[j];
   }
   PBG_GANG_SYNC
 }
