@@ -61,48 +61,79 @@ def host_threads():
     return (min(avail, omp) if omp > 0 else avail), avail
 
 
-def cpu_baseline(seconds=12.0):
-    """The CPU oracle (float64 restatement of the same step, OpenMP over envs) on the host's
-    cores, on a bounded sample of the same workload: 4,096 Ant envs, Philox 0x5EED actions,
-    auto-reset on done or after 1,000 steps (reset noise from the host Philox mirror), stepped
-    until ~`seconds` of wall time."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
+def _oracle_rollout(n, threads, seconds, chunk=64):
+    """Step n Ant envs on the CPU oracle with `threads` OpenMP threads for ~`seconds` of timed
+    work.  Every step gets its own Philox 0x5EED action batch (counter = step, env) and every
+    auto-reset its own reset-noise draw (counter = env, episode), both generated in chunks
+    outside the timed intervals; the oracle's step and masked reset are timed."""
     import numpy as np
     import oracle
-    import pybulletgym_amd  # noqa: F401
     from pybulletgym_amd import rng
-    threads, avail = host_threads()
-    n = 4096
     e = oracle.OracleEnvs(ENV_ID, n, nthreads=threads, seed=ACTION_SEED)
     ids = np.arange(n)
     epi = np.zeros(n, np.int64)
     obs = e.reset(rng.reset_noise(ACTION_SEED, ids, 0, e.info.NR).astype(np.float64))
-    acts = rng.sample_actions(e.info.NA, ids, np.arange(16), seed=ACTION_SEED)  # cycled (host Philox is slow)
     steps = resets = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        obs, _, done, _ = e.step(acts[steps % 16])
-        steps += 1
-        finished = done | (e.aux[:, 2] >= 1000)
-        if finished.any():
-            epi[finished] += 1
-            q = np.zeros((n, e.info.NR))
-            for k in np.flatnonzero(finished):
-                q[k] = rng.reset_noise(ACTION_SEED, [k], int(epi[k]), e.info.NR)[0]
-            e.reset(q, mask=finished, obs=obs)
-            resets += int(finished.sum())
-    dt = time.perf_counter() - t0
+    timed = 0.0
+    while timed < seconds:
+        acts = rng.sample_actions(e.info.NA, ids, np.arange(steps, steps + chunk), seed=ACTION_SEED)
+        for a in acts:
+            t0 = time.perf_counter()
+            obs, _, done, _ = e.step(a)
+            timed += time.perf_counter() - t0
+            steps += 1
+            finished = done | (e.aux[:, 2] >= 1000)
+            if finished.any():
+                fin = np.flatnonzero(finished)
+                epi[fin] += 1
+                q = np.zeros((n, e.info.NR))
+                q[fin] = rng.reset_noise(ACTION_SEED, fin, epi[fin], e.info.NR)
+                t0 = time.perf_counter()
+                e.reset(q, mask=finished, obs=obs)
+                timed += time.perf_counter() - t0
+                resets += len(fin)
+            if timed >= seconds:
+                break
+    return steps, resets, timed
+
+
+def cpu_baseline(seconds=12.0, single_core_seconds=3.0):
+    """The CPU oracle (float64 restatement of the same step, OpenMP over envs) on the host's
+    cores, on a bounded sample of the same workload: 4,096 Ant envs, distinct Philox 0x5EED
+    actions per step, auto-reset on done or after 1,000 steps, ~`seconds` of timed stepping.
+    Threads: the CPUs this job may use (OMP_NUM_THREADS caps sched_getaffinity; the GPU box
+    grants one GPU job 16).  A short single-thread run gives the per-core rate, and the
+    all-CPU figure is that rate times the CPUs in sched_getaffinity (an extrapolation that
+    assumes linear scaling over envs, which the envs' independence allows; stated as such)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pybulletgym_amd  # noqa: F401
+    threads, avail = host_threads()
+    n = 4096
+    steps, resets, dt = _oracle_rollout(n, threads, seconds)
+    s1, _, dt1 = _oracle_rollout(512, 1, single_core_seconds)
+    per_core = 512 * s1 / dt1
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "per_core_value": per_core, "affinity_cpus": avail,
+            "extrapolated_all_affinity_cpus": per_core * avail,
             "sample": f"oracle/pbg_oracle.cpp (float64) on {n} Ant envs x {steps} steps with auto-reset "
-                      f"({resets} resets), {threads} OpenMP threads of {avail} CPUs available "
-                      f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), {dt:.1f} s"}
+                      f"({resets} resets), distinct Philox actions per step, {threads} OpenMP threads of {avail} "
+                      f"CPUs in sched_getaffinity (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
+                      f"{dt:.1f} s timed; per-core rate from 512 envs x {s1} steps on 1 thread ({dt1:.1f} s); "
+                      f"extrapolated_all_affinity_cpus = per_core_value x {avail} (linear-scaling assumption, "
+                      f"not measured)"}
+
+
+# Roofline inputs shipped with the package (they travel to the GPU box with the code):
+# the counted flops per env-step (tools/count_flops.py) and the PMC summaries of the step
+# kernels (tools/pmc_summary.py, tagged with the round of the profile they come from; the raw
+# rocprofv3 CSVs are under profiles/ with the same round prefix).
+PERF = os.path.join(REPO, "pybullet-gym_amd", "perf")
 
 
 def load_pmc(env_id, n):
-    """PMC summary of the step kernel (profiles/pmc_step_<robot>.json, written by
-    tools/pmc_summary.py from the committed rocprofv3 --pmc passes), if it was taken at
-    this env count."""
-    path = os.path.join(REPO, "profiles", f"pmc_step_{SHORT.get(env_id, env_id)}.json")
+    """PMC summary of the step kernel (pybullet-gym_amd/perf/pmc_step_<robot>.json), if it was
+    taken at this env count."""
+    path = os.path.join(PERF, f"pmc_step_{SHORT.get(env_id, env_id)}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -113,10 +144,10 @@ def load_pmc(env_id, n):
 
 
 def load_flops():
-    """Counted FP32 flops per env-step per robot (profiles/flops_per_env_step.json, written by
-    tools/count_flops.py from the op-counting build of the oracle)."""
+    """Counted FP32 flops per env-step per robot (pybullet-gym_amd/perf/flops_per_env_step.json,
+    written by tools/count_flops.py from the op-counting build of the oracle; copy in profiles/)."""
     try:
-        with open(os.path.join(REPO, "profiles", "flops_per_env_step.json")) as f:
+        with open(os.path.join(PERF, "flops_per_env_step.json")) as f:
             return json.load(f)
     except (OSError, ValueError):
         return {}
@@ -130,7 +161,7 @@ def valu_roofline(pmc, kernel_ms, n):
     ach = pmc["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e12
     return {"achieved": ach, "peak": peak, "unit": "T wave-instr/s", "frac": ach / peak,
             "valu_instr_per_env": pmc["valu_insts_per_launch"] * 64 / n,
-            "source": "profiles/" + os.path.basename(pmc.get("_path", "pmc"))}
+            "source": "pybullet-gym_amd/perf/" + os.path.basename(pmc.get("_path", "pmc")) + f" (round {pmc.get('round')})"}
 
 
 def occupancy(env):
@@ -269,13 +300,16 @@ def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
          "obs_finite": bool(torch.isfinite(env.obs).all()),
          "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                      "traffic_source": (f"pybullet-gym_amd/perf/{os.path.basename(pmc['_path'])} (round "
+                                         f"{pmc.get('round')}: FETCH_SIZE/WRITE_SIZE PMC passes, corrected)")
+                      if pmc else None,
                       "kernel": kernel_name(env), "kernel_ms": kernel_ms, "alg_bytes_per_env_step": alg}}
     f = flops.get(SHORT.get(env.env_id, env.env_id))
     if f:
         tf = f["flops_per_env_step"] * n / (kernel_ms * 1e-3) / 1e12
         d["flop_roofline"] = {"bound": "valu-fp32", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": tf / FP32_PEAK_TFLOPS, "flops_per_env_step": f["flops_per_env_step"],
-                              "source": "profiles/flops_per_env_step.json (counted, tools/count_flops.py)"}
+                              "source": "pybullet-gym_amd/perf/flops_per_env_step.json (counted, tools/count_flops.py)"}
     if pmc and pmc.get("valu_insts_per_launch"):
         d["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)
     return d
@@ -292,7 +326,7 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=ENVS_PER_GPU)
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-gather", action="store_true",
-                    help="N > 1: skip timing the RCCL obs all-gather (timed separately, outside `value`)")
+                    help="N > 1: skip timing the RCCL obs|reward|done all-gather (timed separately, outside `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
     ap.add_argument("--legs", default=EXTRA_LEGS,
@@ -322,7 +356,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     import pybulletgym_amd  # noqa: F401
-    from pybulletgym_amd.distributed import gather_flat
+    from pybulletgym_amd.distributed import gather_step
     if not args.dry_run_cpu:
         from pybulletgym_amd.vec_env import VecEnv
 
@@ -339,11 +373,11 @@ def main():
     gather_ms = None
     if not args.no_gather and world > 1:
         for _ in range(3):
-            gather_flat(env.obs)
+            gather_step(env.obs, env.reward, env.done)
         _sync(dev)
         t1 = time.perf_counter()
         for _ in range(20):
-            gather_flat(env.obs)
+            gather_step(env.obs, env.reward, env.done)
         _sync(dev)
         gather_ms = (time.perf_counter() - t1) / 20 * 1e3
 
@@ -391,10 +425,12 @@ def main():
                 out[k] = head[k]
         out.update(legs)
         if gather_ms is not None:
-            # the learner's optional flat batch: one all_gather_into_tensor of
-            # [envs_per_gpu, obs_dim] float32 per rank, timed after the rollout
-            out["allgather_obs_ms"] = gather_ms
-            out["allgather_obs_bytes"] = world * n * env.info.obs_dim * 4
+            # the learner's optional flat batch: obs, reward and done packed into
+            # one all_gather_into_tensor of [envs_per_gpu, obs_dim + 2] float32 per rank, timed
+            # after the rollout (outside `value`)
+            out["allgather_step_ms"] = gather_ms
+            out["allgather_step_bytes"] = world * n * (env.info.obs_dim + 2) * 4
+            out["allgather_payload"] = "obs | reward | done, float32 [global_envs, obs_dim + 2]"
         if args.dry_run_cpu:
             out["dry_run"] = "cpu/gloo stand-in env: control-flow check only, value is not a measurement"
         if world == 1 and not args.no_cpu_baseline and not args.dry_run_cpu:

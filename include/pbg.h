@@ -31,6 +31,12 @@ extern "C" {
 #define PBG_E_HIP (-3)
 #define PBG_E_NOMEM (-4)
 
+/* Layout version of the per-env state records of pbg_get_state / pbg_set_state (reported in
+ * pbg_info_t.record_version).  1: round-1 aux record (no episode counter); 2: aux ends with
+ * the episodes-started counter (the reset-noise Philox counter).  A checkpoint written under
+ * another version must not be passed to pbg_set_state (the aux width differs). */
+#define PBG_RECORD_VERSION 2
+
 typedef struct pbg_handle pbg_handle;
 
 typedef struct {
@@ -57,6 +63,7 @@ typedef struct {
   int vgprs;             /* step kernel registers per lane (hipFuncGetAttributes numRegs) */
   int scratch_bytes;     /* step kernel private segment per lane (0: no spills to memory) */
   int lds_rows;          /* contact rows (gang: contacts) resident in LDS per env */
+  int record_version;    /* PBG_RECORD_VERSION of the state / aux records (appended in round 3) */
 } pbg_info_t;
 
 typedef struct {
@@ -127,7 +134,10 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
  *   [10..12] base ang vel (world), then q[n_joints], qd[n_joints];
  * aux: [n, aux_words] float64 = [potential, initial_z, elapsed_steps, floor_in_parts,
  *   feet_contact[n_feet], (HumanoidFlagrun: walk target x, y, flag_timeout, flag draws),
- *   episodes started (the reset-noise RNG counter)]  (aux may be NULL in set_state). */
+ *   episodes started (the reset-noise RNG counter)], layout PBG_RECORD_VERSION.
+ * set_state with aux == NULL replaces the physical state only: the handle keeps its own
+ * bookkeeping -- potential, initial_z, elapsed steps, feet flags and the episode counter --
+ * so later resets continue that handle's reset-noise stream, not the checkpoint's. */
 int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream);
 int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream);
 
@@ -139,7 +149,8 @@ int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, v
 /* Batched action_space.sample() (robot_bases.py:24-25 Box(-1, 1)): out[s, e, i] = U(-1, 1)
  * float32 for s < n_steps, e < n_envs, i < action_dim; Philox4x32-10, key = seed, counter =
  * (step0 + s, env_offset + e, i / 4, 0xAC7) -- the bench's random-action protocol
- * (BASELINE.md section 2), independent of the sharding.  out: device [n_steps, n_envs, action_dim]. */
+ * (BASELINE.md section 2), independent of the sharding.  out: device [n_steps, n_envs, action_dim];
+ * the kernel runs on the device that owns `out` (pbg_pack likewise on its records' device). */
 int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, uint32_t step0, int env_offset,
                        float* out, void* stream);
 

@@ -27,7 +27,7 @@ class Info(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "robot_id", "n_envs", "action_dim", "obs_dim", "n_dof", "n_joints", "n_links", "n_feet", "state_words",
         "aux_words", "substeps", "max_episode_steps", "reset_dofs", "floating", "lanes_per_env", "block", "lds_bytes",
-        "vgprs", "scratch_bytes", "lds_rows")]
+        "vgprs", "scratch_bytes", "lds_rows", "record_version")]
 
 
 class StepIO(ctypes.Structure):

@@ -64,6 +64,7 @@ pbg_info_t info_of(int rid) {
   I.n_joints = R::NJ; I.n_links = R::NL; I.n_feet = R::NF; I.state_words = pbg::Records<R>::SD;
   I.aux_words = pbg::Records<R>::AD; I.substeps = R::substeps; I.max_episode_steps = R::max_episode_steps;
   I.reset_dofs = R::NR; I.floating = R::floating;
+  I.record_version = PBG_RECORD_VERSION;
   return I;
 }
 
@@ -96,6 +97,17 @@ struct DeviceGuard {
 int hip_check(int e, const char* what) {
   if (e == (int)hipSuccess) return PBG_OK;
   return fail(PBG_E_HIP, "%s: HIP error %ld", what, (long)e);
+}
+
+// The device that owns a device buffer (entry points without a handle launch there, whatever
+// the caller's current device is); -1 when the pointer is not device memory.
+int device_of(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ? a.device : -1;
 }
 
 }  // namespace
@@ -284,6 +296,9 @@ int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, u
                        float* out, void* stream) {
   if (action_dim <= 0 || n_envs <= 0 || n_steps <= 0 || !out)
     return fail(PBG_E_ARG, "pbg_sample_actions: bad arguments%s%ld");
+  const int dev = device_of(out);
+  if (dev < 0) return fail(PBG_E_ARG, "pbg_sample_actions: out is not device memory%s%ld");
+  DeviceGuard dg(dev);
   const long lanes = (long)n_steps * n_envs * ((action_dim + 3) / 4);
   hipLaunchKernelGGL(sample_actions_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      action_dim, n_envs, n_steps, (uint32_t)seed, (uint32_t)(seed >> 32), step0, env_offset, out);
@@ -294,6 +309,10 @@ int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, v
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_pack: unknown env id '%s'%ld", env_id ? env_id : "(null)");
   if (n <= 0 || !in_rec || !out_rec) return fail(PBG_E_ARG, "pbg_pack: bad arguments%s%ld");
+  const int dev = device_of(out_rec);
+  if (dev < 0 || device_of(in_rec) != dev)
+    return fail(PBG_E_ARG, "pbg_pack: in_rec / out_rec are not device memory of one GPU%s%ld");
+  DeviceGuard dg(dev);
   return hip_check(ops(rid)->pack(n, in_rec, out_rec, (hipStream_t)stream), "pack_kernel launch");
 }
 

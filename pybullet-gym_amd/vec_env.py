@@ -164,7 +164,25 @@ class VecEnv:
                       "pbg_get_state")
         return phys, aux
 
+    def state_dict(self) -> dict:
+        """Checkpoint of every env (pybullet saveState generalised): the state records plus the
+        env id and the record-layout version (include/pbg.h PBG_RECORD_VERSION)."""
+        phys, aux = self.get_state()
+        return {"env_id": self.env_id, "record_version": int(self.info.record_version), "phys": phys, "aux": aux}
+
+    def load_state_dict(self, sd: dict):
+        """Restore a state_dict(); refuses a checkpoint of another env id or record layout."""
+        if sd.get("env_id") != self.env_id:
+            raise _native.PbgError(f"checkpoint of {sd.get('env_id')!r} loaded into {self.env_id!r}")
+        if sd.get("record_version") != self.info.record_version:
+            raise _native.PbgError(f"checkpoint record version {sd.get('record_version')} != library's "
+                                   f"{self.info.record_version} (the aux record layout changed)")
+        self.set_state(sd["phys"], sd["aux"])
+
     def set_state(self, phys: torch.Tensor, aux: torch.Tensor = None):
+        """phys / aux: [n, state_words] / [n, aux_words] float64 records (pbg_get_state layout).
+        aux None: only the physical state is replaced; the handle keeps its bookkeeping,
+        including the episode counter that keys the next reset's noise (include/pbg.h)."""
         phys = phys.to(device=self.device, dtype=torch.float64).contiguous()
         assert phys.shape == (self.num_envs, self.info.state_words)
         if aux is not None:
