@@ -52,6 +52,8 @@ def lib():
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
         L.pbg_oracle_pack_flag.argtypes = [ctypes.c_int, P, P, P, P]
         L.pbg_oracle_set_rng.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        L.pbg_oracle_set_mca_seed.argtypes = [ctypes.c_uint64]
+        L.pbg_oracle_set_mca_seed.restype = None
         L.pbg_oracle_dynamics.argtypes = [ctypes.c_int, P, P, P]
         L.pbg_oracle_link_com.argtypes = [ctypes.c_int, P, P]
         _lib = L
@@ -82,7 +84,8 @@ class OracleEnvs:
 
     def __init__(self, name: str, n: int, nthreads: int = 1, seed: int = 0, env_offset: int = 0, precision: int = 64):
         """seed / env_offset key the Philox draws of HumanoidFlagrun's flag (as the kernels').
-        precision 32: the physics in IEEE float32 (the conditioning probe of the parity tests)."""
+        precision 32: the physics in IEEE float32 (the conditioning probe of the parity tests);
+        33: float32 Monte Carlo arithmetic (oracle/mca.h; set_mca_seed picks the stream)."""
         self.precision = precision
         lib().pbg_oracle_set_rng(seed, env_offset)
         self.rid = robot_id(name)
@@ -115,6 +118,12 @@ class OracleEnvs:
                                         _p(rew), _p(done), _p(nc), self.nthreads, _p(self.csig), _p(self.terms),
                                         self.precision, _p(self.asig)) == 0
         return obs, rew, done.astype(bool), nc
+
+
+def set_mca_seed(seed: int):
+    """Stream of the float32 Monte Carlo arithmetic (precision 33): env e of the next step
+    calls draws from the stream keyed by (seed, e)."""
+    lib().pbg_oracle_set_mca_seed(seed)
 
 
 def dynamics(name: str, state: np.ndarray):

@@ -33,6 +33,7 @@
 #include "../pybullet-gym_amd/csrc/models_gen.h"
 #include "../pybullet-gym_amd/csrc/sim_params.h"
 #include "counted.h"
+#include "mca.h"
 
 #include <cmath>
 
@@ -43,6 +44,8 @@
 #define MAXROWS (2 * MAXD + 3 * (MAXS + MAXPAIR))
 
 thread_local FlopCount g_flops;
+thread_local uint64_t g_mca_state;
+static uint64_t g_mca_seed = 0;
 
 namespace {
 
@@ -704,7 +707,9 @@ int pbg_oracle_reset(int robot, int n, double* state, double* aux, const double*
 // csig (nullable): per env the contact-set signature of the step (sim_params.h pbg_contact_hash);
 // rew_terms (nullable): [n][5] the terms the reward sums (the reference's self.rewards).
 // precision: 64 = the float64 oracle; 32 = the same physics in IEEE float32 (the pack stays
-// float64, as in the kernels) -- the parity tests' conditioning probe.
+// float64, as in the kernels) -- the parity tests' conditioning probe; 33 = float32 Monte Carlo
+// arithmetic (mca.h: every operation randomly rounded to a float32 neighbour, stream seeded by
+// pbg_oracle_set_mca_seed and the env index) -- the parity tests' outlier explanation.
 // asig (nullable): per env the solver active-set signature (sim_params.h pbg_solver_event).
 int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float* act, float* obs, double* rew,
                        uint8_t* done, int32_t* ncontact, int nthreads, uint32_t* csig, double* rew_terms,
@@ -727,8 +732,15 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     uint32_t sig = 0;
     double* cache = g_cache && (size_t)e < g_cache_n ? g_cache + (size_t)e * 4 * (MAXS + MAXPAIR) : nullptr;
     uint32_t as = 0;
-    const int nc = precision == 32 ? physics_step<float>(m, s, ac, slot_active, &sig, nullptr, &as)
-                                   : physics_step<double>(m, s, ac, slot_active, &sig, cache, &as);
+    int nc;
+    if (precision == 32) {
+      nc = physics_step<float>(m, s, ac, slot_active, &sig, nullptr, &as);
+    } else if (precision == 33) {
+      g_mca_state = g_mca_seed * 0x9E3779B97F4A7C15ull + (uint64_t)e * 0xD1B54A32D192ED03ull + 1;
+      nc = physics_step<Mca>(m, s, ac, slot_active, &sig, nullptr, &as);
+    } else {
+      nc = physics_step<double>(m, s, ac, slot_active, &sig, cache, &as);
+    }
     if (asig) asig[e] = as;
     if (ncontact) ncontact[e] = nc;
     if (csig) csig[e] = sig;
@@ -764,6 +776,10 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
   }
   return 0;
 }
+
+// Seed of the Monte Carlo arithmetic stream (precision 33); env e of a step call draws from
+// the stream keyed by (seed, e).
+void pbg_oracle_set_mca_seed(uint64_t seed) { g_mca_seed = seed; }
 
 int pbg_oracle_step(int robot, int n, double* state, double* aux, const float* act, float* obs, double* rew,
                     uint8_t* done, int32_t* ncontact, int nthreads, uint32_t* csig, double* rew_terms) {

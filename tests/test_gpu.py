@@ -157,16 +157,17 @@ def test_rng_reset_matches_host_philox(env_id):
 # Every outlier must be explained.  An env-step is an outlier when its
 # GPU error exceeds its class bound: class A above the strict bound, class B above
 # SPREAD_RATIO x the float64 oracle's own perturbation spread, class C whenever its error
-# exceeds the strict bound.  Each outlier is re-stepped from the same input state through
-# the oracle's IEEE float32 instantiation (the same physics as the float64 oracle, in the
-# kernels' precision): once from the exact state and F32_ULP_PROBES times from the state
-# moved by one float32 ulp per word (random sign).  The float32 envelope is the largest
-# error of those runs against float64.  A class A/B outlier is explained when
+# exceeds the strict bound.  Each outlier is re-stepped from the same input state through the
+# oracle's float32 instantiations: IEEE float32 once, and F32_MCA_RUNS times in float32 Monte
+# Carlo arithmetic (oracle/mca.h: every operation rounded to a random float32 neighbour, an
+# error of up to one ulp per operation -- the accuracy class of the kernels' own v_rcp /
+# v_sqrt / v_rsq and short sincos).  The float32 envelope is the largest error of those runs
+# against float64.  A class A/B outlier is explained when
 #   GPU error <= EXPLAIN_FACTOR x float32 envelope
-# (float32 arithmetic alone moves this step as far as the kernel does).  A class C outlier
-# is explained when one of the float32 runs also lands in a different discrete state than
-# float64 (the step sits on a contact / limit / alive threshold at float32 resolution) or
-# meets the same envelope rule.  An unexplained outlier fails the test.
+# (float32 arithmetic of the same algorithm moves this step as far as the kernel does).  A
+# class C outlier is explained when one of the float32 runs also lands in a different discrete
+# state than float64 (the step sits on a contact / limit / alive threshold at float32
+# resolution) or meets the envelope rule.  An unexplained outlier fails the test.
 STRICT_REL = 1e-4
 STRICT_SHARE = 0.999
 HARD_MAX = 1e-2
@@ -179,15 +180,25 @@ SPREAD_RATIO = 10.0
 COND_FRAC = 0.6
 LOOSE_FRAC = 0.05
 EXPLAIN_FACTOR = 3.0
-F32_ULP_PROBES = 3
+F32_MCA_RUNS = 32       # first pass per outlier ...
+F32_MCA_RUNS_MAX = 2048  # ... and the escalation for an outlier the first pass leaves unexplained (a
+                        # step on a PGS active-set boundary that ~1 % of float32 roundings cross)
 # The MuJoCo-observation variants (not the north_star's ids) carry raw
 # joint and base velocities (the PyBullet observation scales joint speeds by 0.1) and the raw
 # quaternion: the same state error reads ten times larger, so their class-A bound is 1e-3, and
 # far more of their env-steps are ill conditioned at float32.
 STRICT_REL_ENV = {e: 1e-3 for e in ("HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0",
                                     "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0")}
-COND_FRAC_ENV = {"AntMuJoCoEnv-v0": 0.85, "HumanoidMuJoCoEnv-v0": 0.85, "HopperMuJoCoEnv-v0": 0.7,
-                 "Walker2DMuJoCoEnv-v0": 0.7, "HalfCheetahMuJoCoEnv-v0": 0.7}
+# Ceiling on the ill-conditioned (class B) share per env id: the largest share any
+# test measured for it (profiles/r03_parity.jsonl; 60-step, 1,000-step config and kernel-variant
+# tests) plus 0.1.  Every class-B outlier is explained separately (above), so this bounds how
+# much of the comparison may fall outside the strict class.
+COND_FRAC_ENV = {"InvertedPendulumPyBulletEnv-v0": 0.05, "InvertedPendulumSwingupPyBulletEnv-v0": 0.05,
+                 "InvertedDoublePendulumPyBulletEnv-v0": 0.05, "InvertedDoublePendulumMuJoCoEnv-v0": 0.05,
+                 "HopperPyBulletEnv-v0": 0.67, "HalfCheetahPyBulletEnv-v0": 0.26, "AntPyBulletEnv-v0": 0.51,
+                 "HumanoidPyBulletEnv-v0": 0.38, "Walker2DPyBulletEnv-v0": 0.65,
+                 "HumanoidFlagrunPyBulletEnv-v0": 0.35, "HopperMuJoCoEnv-v0": 0.19, "Walker2DMuJoCoEnv-v0": 0.40,
+                 "HalfCheetahMuJoCoEnv-v0": 0.64, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.85}
 
 
 def _probe_state(state, rng):
@@ -195,32 +206,47 @@ def _probe_state(state, rng):
     return state + rng.uniform(-1.0, 1.0, state.shape) * (PROBE_REL * np.abs(state) + PROBE_ABS)
 
 
-def _ulp_state(state, rng):
-    """Every state word (a float32 value) moved by one float32 ulp up, down or not at all."""
-    s = state.astype(np.float32)
-    d = rng.integers(-1, 2, s.shape)
-    up = np.nextafter(s, np.float32(np.inf))
-    dn = np.nextafter(s, np.float32(-np.inf))
-    return np.where(d > 0, up, np.where(d < 0, dn, s)).astype(np.float64)
-
-
-def _f32_envelope(env_id, state, aux, act, oo, csig64, disc64, kind, seed=0):
-    """The float32 oracle re-stepped from `state` (exact, then F32_ULP_PROBES one-ulp moves):
-    (largest relative obs error against the float64 result `oo`, whether any run's discrete
-    state -- contact-set signature or discrete reward terms -- differs from float64's)."""
+def _f32_envelope(env_id, state, aux, act, oo, csig64, disc64, kind, seed=0, runs=F32_MCA_RUNS):
+    """The oracle's float32 physics re-stepped from `state`: IEEE float32 once, then `runs`
+    Monte Carlo arithmetic runs (oracle/mca.h) per env-step.  Returns (largest relative obs
+    error against the float64 result `oo`, whether any run's discrete state -- contact-set
+    signature or discrete reward terms -- differs from float64's)."""
     k = len(state)
-    f32 = oracle.OracleEnvs(env_id, k, nthreads=min(16, os.cpu_count() or 1), seed=seed, precision=32)
-    r = np.random.default_rng(seed + 99)
-    env = np.zeros(k)
-    disc = np.zeros(k, bool)
-    for j in range(1 + F32_ULP_PROBES):
-        f32.state[:] = state if j == 0 else _ulp_state(state, r)
-        f32.aux[:] = aux
-        op, _, _, _ = f32.step(act)
-        env = np.maximum(env, _rel(op, oo))
-        disc |= f32.csig != csig64
-        disc |= (_discrete_terms(f32.terms, kind) != disc64).any(axis=1)
+    th = min(16, os.cpu_count() or 1)
+    f32 = oracle.OracleEnvs(env_id, k, nthreads=th, seed=seed, precision=32)
+    f32.state[:] = state
+    f32.aux[:] = aux
+    op, _, _, _ = f32.step(act)
+    env = _rel(op, oo)
+    disc = (f32.csig != csig64) | (_discrete_terms(f32.terms, kind) != disc64).any(axis=1)
+    R = runs
+    mca = oracle.OracleEnvs(env_id, k * R, nthreads=th, seed=seed, precision=33)
+    oracle.set_mca_seed(seed + R)
+    mca.state[:] = np.repeat(state, R, axis=0)
+    mca.aux[:] = np.repeat(aux, R, axis=0)
+    om, _, _, _ = mca.step(np.repeat(act, R, axis=0))
+    env = np.maximum(env, _rel(om, np.repeat(oo, R, axis=0)).reshape(k, R).max(axis=1))
+    flip = (mca.csig != np.repeat(csig64, R)) | \
+        (_discrete_terms(mca.terms, kind) != np.repeat(disc64, R, axis=0)).any(axis=1)
+    disc |= flip.reshape(k, R).any(axis=1)
     return env, disc
+
+
+def _explainer(env_id, s_in, x_in, act, oo, csig64, disc64, kind, seed):
+    """explain(idx) for SplitStats.add: the float32 envelope of the env-steps idx, escalated
+    to F32_MCA_RUNS_MAX Monte Carlo runs for those the first F32_MCA_RUNS leave unexplained."""
+    def explain(idx, rel):
+        env, flip = _f32_envelope(env_id, s_in[idx], x_in[idx], act[idx], oo[idx], csig64[idx], disc64[idx], kind,
+                                  seed)
+        again = np.flatnonzero(rel > EXPLAIN_FACTOR * env)
+        if len(again):
+            j = idx[again]
+            e2, f2 = _f32_envelope(env_id, s_in[j], x_in[j], act[j], oo[j], csig64[j], disc64[j], kind, seed,
+                                   runs=F32_MCA_RUNS_MAX)
+            env[again] = np.maximum(env[again], e2)
+            flip[again] |= f2
+        return env, flip
+    return explain
 
 
 def _report(rec):
@@ -247,11 +273,12 @@ class SplitStats:
         self.out = {c: [0, 0, 0.0] for c in "ABC"}
         self.unexplained = []
         self.worst = {}
+        self.dump = []  # (state, aux, act, gpu obs, oracle obs) of unexplained outliers (PBG_PARITY_DUMP)
 
-    def add(self, og, oo, rg, ro, dg, do, cg, co, same, cond=None, probe=None, explain=None, step=None):
+    def add(self, og, oo, rg, ro, dg, do, cg, co, same, cond=None, probe=None, explain=None, step=None, inputs=None):
         """same: per env-step True where the discrete state agrees (contact set, discrete
         reward terms); cond: True where the conditioning probe passed (None: all); probe: the
-        oracle's own spread (class B's yardstick); explain(idx) -> (float32 envelope, discrete
+        oracle's own spread (class B's yardstick); explain(idx, rel) -> (float32 envelope, discrete
         flip) of the env-steps idx (outlier explanation; None: outliers are not re-stepped)."""
         a = same if cond is None else same & cond
         b = same & ~a
@@ -278,7 +305,7 @@ class SplitStats:
         if explain is None or not outl.any():
             return
         idx = np.flatnonzero(outl)
-        env32, flip = explain(idx)
+        env32, flip = explain(idx, rel[idx])
         ok = rel[idx] <= EXPLAIN_FACTOR * env32
         ok |= c[idx] & flip
         ratio = rel[idx] / np.maximum(env32, 1e-30)
@@ -294,6 +321,8 @@ class SplitStats:
             if not ok[j] and len(self.unexplained) < 20:
                 self.unexplained.append(dict(step=step, env=int(i), cls=cl, gpu_rel=float(rel[i]),
                                              f32_envelope=float(env32[j]), f32_flip=bool(flip[j])))
+                if inputs is not None:
+                    self.dump.append((inputs[0][i], inputs[1][i], inputs[2][i], og[i], oo[i]))
             if rel[i] > self.worst.get(cl, {}).get("gpu_rel", -1.0):
                 self.worst[cl] = dict(step=step, env=int(i), gpu_rel=float(rel[i]), f32_envelope=float(env32[j]),
                                       f32_flip=bool(flip[j]), explained=bool(ok[j]))
@@ -316,6 +345,12 @@ class SplitStats:
                    outliers_count_explained_maxratio={k: v for k, v in self.out.items()},
                    outlier_worst=self.worst, unexplained=self.unexplained)
         _report(rec)
+        ddir = os.environ.get("PBG_PARITY_DUMP")
+        if ddir and self.dump:
+            os.makedirs(ddir, exist_ok=True)
+            fn = "".join(c if c.isalnum() else "_" for c in self.name) + ".npz"
+            np.savez(os.path.join(ddir, fn), **{k: np.array([d[j] for d in self.dump])
+                                                 for j, k in enumerate(("state", "aux", "act", "og", "oo"))})
         assert self.nA > 0
         assert not self.unexplained, rec
         assert rec["classA_share_within_bound"] >= STRICT_SHARE and rec["classA_max_rel_obs"] <= HARD_MAX, rec
@@ -382,9 +417,8 @@ def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None):
         d64 = _discrete_terms(orc.terms, kind)
         same = (sg == orc.csig) & (_discrete_terms(tg, kind) == d64).all(axis=1)
 
-        def explain(i, s_in=s_in, x_in=x_in, a=a, oo=oo, cs=orc.csig.copy(), d64=d64.copy()):
-            return _f32_envelope(env_id, s_in[i], x_in[i], a[i], oo[i], cs[i], d64[i], kind, seed=seed)
-        st.add(og, oo, rg, ro, term_g, do, cg, co, same, cond, probe, explain=explain, step=t)
+        explain = _explainer(env_id, s_in, x_in, a, oo, orc.csig.copy(), d64.copy(), kind, seed)
+        st.add(og, oo, rg, ro, term_g, do, cg, co, same, cond, probe, explain=explain, step=t, inputs=(s_in, x_in, a))
     env.close()
     return st.check()
 
@@ -578,12 +612,12 @@ def _variant_vs_lane(env_id, n, steps, seed=3, **opts):
         # each of the float32 envelope's size, so the same EXPLAIN_FACTOR rule applies
         ol = rl.obs.cpu().numpy().astype(np.float64)
 
-        def explain(i, s_in=s_in, x_in=x_in, an=an, oo=oo, cs=orc.csig.copy(),
-                    d64=_discrete_terms(orc.terms, kind).copy()):
-            return _f32_envelope(env_id, s_in[i], x_in[i], an[i], oo[i], cs[i], d64[i], kind, seed=seed)
+        explain = _explainer(env_id, s_in, x_in, an, oo, orc.csig.copy(), _discrete_terms(orc.terms, kind).copy(),
+                             kind, seed)
         st.add(rv.obs.cpu().numpy(), ol, var.reward64.cpu().numpy(),
                lane.reward64.cpu().numpy(), rv.done.cpu().numpy(), rl.done.cpu().numpy(),
-               var.ncontact.cpu().numpy(), lane.ncontact.cpu().numpy(), same, cond, probe, explain=explain, step=t)
+               var.ncontact.cpu().numpy(), lane.ncontact.cpu().numpy(), same, cond, probe, explain=explain, step=t,
+               inputs=(s_in, x_in, an))
     st.check()
     return var.info.lanes_per_env
 

@@ -181,3 +181,34 @@ def test_reset_semantics():
     h = oracle.OracleEnvs("humanoid", 1)
     h.reset(np.zeros((1, 17)))
     assert h.aux[0, 1] == 0.8  # Humanoid fixes initial_z (robot_locomotors.py:183)
+
+
+@pytest.mark.parametrize("env_id", ["HopperPyBulletEnv-v0", "AntPyBulletEnv-v0"])
+def test_mca_float32_runs_bracket_ieee_float32(env_id):
+    """The float32 Monte Carlo arithmetic instantiation (oracle/mca.h, precision 33) that the
+    GPU parity tests use to explain outliers: a stream is reproducible for a seed and differs
+    across seeds; over a rollout its spread around float64 has the scale of the IEEE float32
+    instantiation's error (median within 10x either way), far below the physics itself."""
+    n, R = 64, 8
+    e = oracle.OracleEnvs(env_id, n, nthreads=8)
+    e.reset(np.random.default_rng(0).uniform(-0.1, 0.1, (n, e.info.NR)))
+    acts = np.random.default_rng(1).uniform(-1, 1, (12, n, e.info.NA)).astype(np.float32)
+    for t in range(10):
+        e.step(acts[t])
+    st, ax, a = e.state.copy(), e.aux.copy(), acts[10]
+
+    def run(prec, seed=0, reps=1):
+        o = oracle.OracleEnvs(env_id, n * reps, nthreads=8, precision=prec)
+        oracle.set_mca_seed(seed)
+        o.state[:] = np.repeat(st, reps, 0)
+        o.aux[:] = np.repeat(ax, reps, 0)
+        return o.step(np.repeat(a, reps, 0))[0]
+    o64, o32 = run(64), run(32)
+    m1, m2, m3 = run(33, 5), run(33, 5), run(33, 6)
+    np.testing.assert_array_equal(m1, m2)
+    assert (m1 != m3).any()
+    rel = lambda x, y: (np.abs(x.astype(np.float64) - y) / np.maximum(1, np.abs(y))).max(axis=1)  # noqa: E731
+    e32 = rel(o32, o64)
+    emca = rel(run(33, 7, R), np.repeat(o64, R, 0)).reshape(n, R).max(axis=1)
+    assert np.median(emca) <= 10 * max(np.median(e32), 1e-7) and np.median(e32) <= 10 * max(np.median(emca), 1e-7)
+    assert np.median(emca) < 1e-3
