@@ -41,7 +41,7 @@
 #define MAXD 32
 #define MAXS 32
 #define MAXPAIR 72
-#define MAXROWS (2 * MAXD + 3 * (MAXS + MAXPAIR))
+#define MAXROWS (2 * MAXD + 6 * (MAXS + MAXPAIR))  // 3 rows per contact + the rule study's 3 torsional
 
 thread_local FlopCount g_flops;
 thread_local uint64_t g_mca_state;
@@ -58,7 +58,8 @@ int g_flags = 0;
 // rules the HIP kernels implement; every product-parity comparison runs with the defaults.
 enum { OPT_CONTACT_ERP, OPT_DEEP_ERP, OPT_DEEP_THR, OPT_DEEP_MODE, OPT_LIMIT_MODE, OPT_DAMP_MODE, OPT_FRIC_MODE,
        OPT_WARM, OPT_WARM_FRIC, OPT_LIMIT_ERP, OPT_ITERS, OPT_SEP_MODE, OPT_SLOP, OPT_SEP_ABS, OPT_LIM_SEP_ABS,
-       OPT_COUNT };
+       OPT_SPRINGS, OPT_ROLL_MU, OPT_SPIN_MU, OPT_LIM_DEEP_MODE, OPT_LIMIT_CFM, OPT_CONTACT_CFM, OPT_CONTACT_THR,
+       OPT_MARGIN, OPT_SELF_COLLISION, OPT_COUNT };
 double g_opt[OPT_COUNT];
 const double g_opt_default[OPT_COUNT] = {
     -1.0,             // contact ERP of penetrating contact normal rows (-1: the model's, models_gen.h)
@@ -76,12 +77,29 @@ const double g_opt_default[OPT_COUNT] = {
     0.0,              // linear slop added to the contact distance
     1.0,              // separated contact rows: 1 = J nu_new >= -d/dt (Bullet's absolute rhs), 0 = J dnu >= -d/dt
     1.0,              // separated joint-limit rows: the same choice
+    0.0,              // joint springs: scale on the MJCF stiffness table (pbg_oracle_set_springs): tau -= s k q
+    0.0,              // rolling friction: combined coefficient of two angular rows about the contact tangents
+    0.0,              // spinning friction: combined coefficient of an angular row about the contact normal
+    0.0,              // joint-limit violations deeper than OPT_DEEP_THR: 0 = OPT_LIMIT_ERP, 1 = velocity only
+                      //   (btMultiBodyJointLimitConstraint's split-impulse branch; split impulse is not
+                      //   solved for multibodies), 2 = ERP 0.9 (m_erp2 from setDefaultContactERP)
+    0.0,              // joint-limit CFM: m_eff = 1 / (J M^-1 J^T + cfm)
+    0.0,              // contact CFM (normal and friction rows)
+    PBG_CONTACT_THRESHOLD,  // contact processing / breaking threshold
+    0.0,              // collision margin added around every robot geom (MJCF geom margin)
+    1.0,              // self-collision pairs: 1 = on (URDF_USE_SELF_COLLISION, robot_bases.py:116), 0 = off
 };
 struct OptInit { OptInit() { for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = g_opt_default[i]; } } g_opt_init;
 // persistent contact impulses per env and collision candidate (warm starting):
 // [env][candidate][normal, t1, t2, active]
 double* g_cache = nullptr;
 size_t g_cache_n = 0;
+#define MAX_ROBOTS 15
+double g_springs[MAX_ROBOTS][MAXD];  // rule study: MJCF joint stiffness per robot and dof
+// contact diagnostics (pbg_oracle_contact_diag; single env, single thread): per contact of every
+// sub-step [sub, candidate, dist, lambda_n, lambda_t1, lambda_t2, mu, v_n, v_t1, v_t2] after the solve
+double* g_diag = nullptr;
+int g_diag_n = 0, g_diag_cap = 0;
 
 // ------------------------------------------------------------------ model view
 struct MV {
@@ -268,6 +286,15 @@ typedef struct {
 } pbg_pack_out;
 
 void pbg_oracle_set_flags(int flags) { g_flags = flags; }
+
+// Joint stiffness table of the rule study (MJCF <joint stiffness>, dof order); the spring
+// torque -OPT_SPRINGS * k_d * q_d enters only when OPT_SPRINGS != 0.
+int pbg_oracle_set_springs(int robot, const double* k, int n) {
+  const MV* mp = model(robot);
+  if (!mp || robot < 0 || robot >= MAX_ROBOTS) return -1;
+  for (int d = 0; d < MAXD; d++) g_springs[robot][d] = (k && d < n) ? k[d] : 0.0;
+  return 0;
+}
 
 // Physics-rule variants (see OPT_*): v[i] for i < n replaces option i; n = 0 restores the defaults.
 int pbg_oracle_set_physics(const double* v, int n) {
@@ -775,6 +802,15 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     for (int f = 0; f < m.NF; f++) a[4 + f] = feet_out[f];
   }
   return 0;
+}
+
+// Contact diagnostics of the next step calls (rule study, tools/walker_diag.py): out holds cap
+// records of 10 doubles (see g_diag); returns the records written since the last call and
+// re-arms the buffer (out NULL: off).
+int pbg_oracle_contact_diag(double* out, int cap) {
+  const int n = g_diag_n;
+  g_diag = out; g_diag_cap = cap; g_diag_n = 0;
+  return n;
 }
 
 // Seed of the Monte Carlo arithmetic stream (precision 33); env e of a step call draws from

@@ -301,11 +301,12 @@ template <class T> struct ContactT {
 template <class T>
 int detect_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, uint8_t* slot_active, int sub, uint32_t* sig) {
   int nc = 0;
-  const T thr(PBG_CONTACT_THRESHOLD);
+  const T thr(g_opt[OPT_CONTACT_THR]);
+  const double margin = g_opt[OPT_MARGIN];
   for (int s = 0; s < m.NS; s++) {
     int b = m.slot_link[s] + 1;
     V3T<T> c = k.x[b] + mul(k.R[b], v3c<T>(m.slot_point[s]));
-    T r(m.slot_radius[s]);
+    T r(m.slot_radius[s] + margin);
     T dist = c.z - r;
     slot_active[s] = dist < thr;
     if (slot_active[s]) {
@@ -319,7 +320,7 @@ int detect_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, uint8_t* sl
       ct.dist = dist; ct.mu = T(m.slot_mu[s]);
     }
   }
-  for (int p = 0; p < m.NPAIR; p++) {
+  for (int p = 0; p < (g_opt[OPT_SELF_COLLISION] != 0.0 ? m.NPAIR : 0); p++) {
     int ba = m.pair_a[p] + 1, bb = m.pair_b[p] + 1;
     V3T<T> a0 = k.x[ba] + mul(k.R[ba], v3c<T>(m.pa0[p])), a1 = k.x[ba] + mul(k.R[ba], v3c<T>(m.pa1[p]));
     V3T<T> b0 = k.x[bb] + mul(k.R[bb], v3c<T>(m.pb0[p])), b1 = k.x[bb] + mul(k.R[bb], v3c<T>(m.pb1[p]));
@@ -327,15 +328,15 @@ int detect_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, uint8_t* sl
     segment_closest(a0, a1, b0, b1, ca, cb);
     V3T<T> dvec = ca - cb;
     T d = norm(dvec);
-    T dist = d - T(m.pra[p]) - T(m.prb[p]);
+    T dist = d - T(m.pra[p] + margin) - T(m.prb[p] + margin);
     if (dist < thr) {
       if (sig) *sig += pbg_contact_hash((uint32_t)sub, (uint32_t)(m.NS + p));
       V3T<T> n = d > T(1e-9) ? (T(1) / d) * dvec : v3(T(0), T(0), T(1));
       ContactT<T>& ct = out[nc++];
       ct.cand = m.NS + p;
       ct.body_a = ba; ct.body_b = bb;
-      ct.pa = ca - T(m.pra[p]) * n;
-      ct.pb = cb + T(m.prb[p]) * n;
+      ct.pa = ca - T(m.pra[p] + margin) * n;
+      ct.pb = cb + T(m.prb[p] + margin) * n;
       ct.n = n; ct.dist = dist; ct.mu = T(m.pmu[p]);
     }
   }
@@ -349,6 +350,18 @@ template <class T> void contact_row_jacobian(const MV& m, const KinT<T>& k, cons
   if (c.body_b >= 0) {
     point_jacobian(m, k, c.body_b, c.pb, Jv, Jw);
     for (int j = 0; j < m.NDOF; j++) J[j] = J[j] - (dir.x * Jv[0][j] + dir.y * Jv[1][j] + dir.z * Jv[2][j]);
+  }
+}
+
+// angular row: relative angular velocity of body A w.r.t. body B about dir (rolling / spinning
+// friction, rule study)
+template <class T> void contact_angular_jacobian(const MV& m, const KinT<T>& k, const ContactT<T>& c, V3T<T> dir, T* J) {
+  T Jv[3][MAXD], Jw[3][MAXD];
+  point_jacobian(m, k, c.body_a, c.pa, Jv, Jw);
+  for (int j = 0; j < m.NDOF; j++) J[j] = dir.x * Jw[0][j] + dir.y * Jw[1][j] + dir.z * Jw[2][j];
+  if (c.body_b >= 0) {
+    point_jacobian(m, k, c.body_b, c.pb, Jv, Jw);
+    for (int j = 0; j < m.NDOF; j++) J[j] = J[j] - (dir.x * Jw[0][j] + dir.y * Jw[1][j] + dir.z * Jw[2][j]);
   }
 }
 
@@ -366,9 +379,9 @@ template <class T> inline T dotn(int n, const T* a, const T* b) {
 // is the round-1 relative form J dnu >= -pos/dt (kept for the rule study).
 template <class T>
 void setup_row(int n, const T L[MAXD][MAXD], const T* nu, RowT<T>& r, T pos, int positional, double erp, T dt,
-               bool sep_abs) {
+               bool sep_abs, double cfm = 0.0) {
   chol_solve(n, L, r.J, r.W);
-  T D = dotn(n, r.J, r.W);
+  T D = dotn(n, r.J, r.W) + T(cfm);
   r.meff = D > T(1e-12) ? T(1) / D : T(0);
   T vJ = dotn(n, r.J, nu);
   if (!positional) r.target = T(0);                                       // friction
@@ -421,6 +434,9 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   const T* qdd_src = g_opt[OPT_DAMP_MODE] != 0.0 ? qd_step : qd0;  // applyJointDamping once per step
   for (int d = 0; d < m.NJ; d++)
     rhs[gidx(m, d)] = rhs[gidx(m, d)] + (tau[d] - ((g_flags & 8) ? T(0) : T(m.damping[d]) * qdd_src[d]));
+  if (g_opt[OPT_SPRINGS] != 0.0)  // rule study: MJCF joint stiffness as a spring to q = 0
+    for (int d = 0; d < m.NJ; d++)
+      rhs[gidx(m, d)] = rhs[gidx(m, d)] - T(g_opt[OPT_SPRINGS] * g_springs[m.robot_id][d]) * s[PBG_BASE_WORDS + d];
   cholesky(n, M);
   chol_solve(n, M, rhs, qdd);
   // generalized velocity nu = [v_base, w_base, qd]
@@ -442,7 +458,10 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
       RowT<T>& r = rows[nr++];
       for (int i = 0; i < n; i++) r.J[i] = T(0);
       r.J[gidx(m, d)] = side == 0 ? T(1) : T(-1);
-      setup_row(n, M, nu, r, pos, 1, g_opt[OPT_LIMIT_ERP], dt, g_opt[OPT_LIM_SEP_ABS] != 0.0);
+      double lerp = g_opt[OPT_LIMIT_ERP];
+      if (g_opt[OPT_LIM_DEEP_MODE] != 0.0 && pos <= T(g_opt[OPT_DEEP_THR]))
+        lerp = g_opt[OPT_LIM_DEEP_MODE] == 1.0 ? -1.0 : 0.9;
+      setup_row(n, M, nu, r, pos, 1, lerp, dt, g_opt[OPT_LIM_SEP_ABS] != 0.0, g_opt[OPT_LIMIT_CFM]);
       r.lo = T(0); r.hi = T(PBG_LIMIT_MAX_IMPULSE); r.normal = -1;
     }
   }
@@ -466,7 +485,7 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     const T dist = cts[c].dist + T(g_opt[OPT_SLOP]);
     const bool deep = dist <= T(g_opt[OPT_DEEP_THR]);
     const double e = deep ? (g_opt[OPT_DEEP_MODE] != 0.0 ? -1.0 : deep_erp) : erp;
-    setup_row(n, M, nu, r, dist, 1, e, dt, g_opt[OPT_SEP_ABS] != 0.0);
+    setup_row(n, M, nu, r, dist, 1, e, dt, g_opt[OPT_SEP_ABS] != 0.0, g_opt[OPT_CONTACT_CFM]);
     r.lo = T(0); r.hi = T(1e30); r.normal = -1; r.mu = cts[c].mu;
   }
   int first_friction = nr;
@@ -477,8 +496,26 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     for (int f = 0; f < fric_dirs; f++) {
       RowT<T>& r = rows[nr++];
       contact_row_jacobian(m, k, cts[c], f == 0 ? t1 : t2, r.J);
-      setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false);
+      setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false, g_opt[OPT_CONTACT_CFM]);
       r.normal = first_normal + c; r.mu = cts[c].mu; r.lo = r.hi = T(0);
+    }
+  }
+  // rule study: spinning (about the normal) and rolling (about the tangents) friction rows,
+  // solved after the friction rows under the same positive-normal rule, bounded by mu * lambda_n
+  // (btMultiBodyConstraintSolver's torsional friction constraints)
+  const double spin = g_opt[OPT_SPIN_MU], roll = g_opt[OPT_ROLL_MU];
+  if (spin > 0.0 || roll > 0.0) {
+    for (int c = 0; c < nc; c++) {
+      V3T<T> t1, t2;
+      plane_space(cts[c].n, t1, t2);
+      for (int a = 0; a < 3; a++) {
+        const double mu = a == 0 ? spin : roll;
+        if (!(mu > 0.0)) continue;
+        RowT<T>& r = rows[nr++];
+        contact_angular_jacobian(m, k, cts[c], a == 0 ? cts[c].n : (a == 1 ? t1 : t2), r.J);
+        setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false);
+        r.normal = first_normal + c; r.mu = T(mu); r.lo = r.hi = T(0);
+      }
     }
   }
   // warm start: last sub-step's impulses of the same candidates (Bullet's persistent
@@ -535,6 +572,20 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
           rows[i].hi = rows[i].mu * ln;
           event(it, crow(i), solve_row(n, rows[i], nu));
         }
+      }
+    }
+  }
+  if (g_diag) {  // contact diagnostics (rule study)
+    for (int c = 0; c < nc && g_diag_n < g_diag_cap; c++) {
+      double* o = g_diag + 10 * g_diag_n++;
+      const RowT<T>& rn = rows[first_normal + c];
+      o[0] = sub; o[1] = cts[c].cand; o[2] = (double)cts[c].dist; o[3] = (double)rn.lambda;
+      o[6] = (double)cts[c].mu; o[7] = (double)dotn(n, rn.J, nu);
+      for (int f = 0; f < 2; f++) {
+        const bool have = f < fric_dirs;
+        const RowT<T>& rf = rows[first_friction + fric_dirs * c + (have ? f : 0)];
+        o[4 + f] = have ? (double)rf.lambda : 0.0;
+        o[8 + f] = have ? (double)dotn(n, rf.J, nu) : 0.0;
       }
     }
   }

@@ -1,0 +1,69 @@
+"""Walker2D / Humanoid policy-failure diagnosis on the CPU oracle: rolls the
+reference's pretrained policy in one env and prints, for the steps before the episode ends,
+the torso state and every floor contact of the last sub-step -- which foot (slot link), its
+penetration, the normal impulse, the friction impulse against its cap mu * lambda_n
+(1.00 = sliding on the friction box) and the post-solve slip velocity.  Test infrastructure
+(imports the oracle and the policies).
+
+  python tools/walker_diag.py [env_id] [episode] [last_steps] [k=v,... physics rule]"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.join(HERE, "..")
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, REPO)
+import oracle  # noqa: E402
+import policies  # noqa: E402
+import physics_rules  # noqa: E402
+
+
+def main(env_id="Walker2DPyBulletEnv-v0", episode=0, last=12, rule=""):
+    key = oracle.ENV_KEYS[env_id]
+    tab = json.load(open(os.path.join(REPO, "pybullet-gym_amd", "models", f"{key}.json")))
+    physics_rules.load_springs()
+    physics_rules.set_physics(physics_rules.parse(rule)[1] if rule else {})
+    L = oracle.lib()
+    L.pbg_oracle_contact_diag.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    pi = policies.Policy(env_id)
+    n = episode + 1
+    q0 = policies.reset_draws(n, oracle.Info(oracle.robot_id(env_id)).NR, 0)[episode:episode + 1]
+    e = oracle.OracleEnvs(env_id, 1, nthreads=1)
+    obs = e.reset(q0)
+    buf = np.zeros((4096, 10))
+    hist = []
+    for t in range(1000):
+        L.pbg_oracle_contact_diag(buf.ctypes.data, len(buf))
+        a = pi.act(obs)
+        obs, r, d, _ = e.step(a)
+        k = L.pbg_oracle_contact_diag(None, 0)
+        recs = buf[:k].copy()
+        hist.append((t, obs[0].copy(), a[0].copy(), float(r[0]), bool(d[0]), recs))
+        if d[0]:
+            break
+    print(f"{env_id} episode {episode}: {len(hist)} steps, return {sum(h[3] for h in hist):.1f}"
+          + (f"  rule {rule}" if rule else ""))
+    slot_link = tab["slot_link"]
+    names = tab["link_name"]
+    for t, o, a, r, d, recs in hist[-last:]:
+        print(f" t{t:4d} z-z0 {o[0]:+.3f} pitch {o[7]:+.3f} vx {o[3] / 0.3:+.2f} r {r:+.2f} done {d} "
+              f"|a| max {np.abs(a).max():.2f}")
+        subs = recs[:, 0] == recs[:, 0].max() if len(recs) else []
+        for c in recs[subs] if len(recs) else []:
+            cand = int(c[1])
+            who = names[slot_link[cand]] if cand < len(slot_link) else f"pair{cand - len(slot_link)}"
+            cap = c[6] * c[3]
+            ft = np.hypot(c[4], c[5])
+            print(f"      {who:12s} dist {c[2]:+.4f} lam_n {c[3]:8.3f} |lam_t|/cap {ft / cap if cap > 0 else 0:5.2f} "
+                  f"v_n {c[7]:+.3f} slip {np.hypot(c[8], c[9]):.3f}")
+
+
+if __name__ == "__main__":
+    args = sys.argv[1:]
+    main(args[0] if args else "Walker2DPyBulletEnv-v0", int(args[1]) if len(args) > 1 else 0,
+         int(args[2]) if len(args) > 2 else 12, args[3] if len(args) > 3 else "")
