@@ -322,74 +322,128 @@ PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k
 }
 
 // ------------------------------------------------------------------ contact rows
-// Per env (shared by its quad): [mu (NC) | rows], LDS [word][env] with stride = envs per
-// workgroup; rows beyond the LDS capacity in a device workspace [word][env].
-// Row: y_branch in four lane slots (NDB words each; the owner branch's slot holds its y,
-// the other three zeros) | y_base (6) + 2 zero words | meff | target | lambda.  Every lane
-// reads its own slot and its base slice (components k, k + 4; words 6 and 7 are the zero
-// pad of lanes 2 and 3), so a row update needs no owner test: the dot products and the
-// axpy of the non-owner lanes see zeros.
+// Row r of the wave's 16 envs (LDS, one region per row of ES * W words):
+//   P: 64 lanes x PW words, lane L = 4 e + k at PW * L: this lane's branch slot y_branch
+//      (NDB words: the owner branch's y, zeros in the other three lanes) | base slice
+//      (components k and k + 4 of y_base; lanes 2 and 3 hold a zero for k + 4)
+//   S: 16 envs x 4 words at 64 PW + 4 e: m_eff | target | lambda | mu (the contact's friction)
+// With PW = 4 (Ant: NDB = 2) a lane reads its whole P with one ds_read_b128 and its env's S
+// with another (the quad's four lanes read the same S address: a broadcast); every 16-lane
+// b128 group covers 16 distinct 16-B slots of the 256-B bank row, so a row load has no bank
+// conflict (the round-2 [word][env] layout put the quad's four branch slots on one bank:
+// 4-way conflicts, 47 % of LDS-active cycles).  Rows beyond the LDS capacity live in the
+// device workspace, [word][env] with the same word order (P of lanes 0..3, then S).
+// Row update: one quad reduction of the lane's slice dot, no owner test (the non-owner lanes'
+// branch words are zero).
 template <class R, int ES>
 struct TRows {
   using T = Team<R>;
-  static constexpr int NDB = T::NDB, W = T::W, NC = T::NC, MR = 3 * T::NC;
-  static constexpr int YB = 4 * NDB;  // first base word
-  static constexpr int HEAD = NC;
+  static constexpr int NDB = T::NDB, NC = T::NC, MR = 3 * T::NC;
+  static constexpr int PW = NDB + 2;    // per-lane words of a row
+  static constexpr int W = 4 * PW + 4;  // words per env per row (P of its 4 lanes + S)
+  static constexpr int SOFF = 4 * ES * PW;  // S block within a row region
+  static constexpr int HEAD = 0;        // per-env words before the rows (pack staging overlaps the rows)
   static_assert(NC <= 32, "contact_sweep keeps one bit per contact in a 32-bit mask");
   static constexpr int WORDS = MR * W;  // device workspace words per env
-  lds_float* lds;  // LDS base + env slot
-  float* gbl;      // workspace base + env
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v4f lds_float4;
+  typedef __attribute__((address_space(3))) v2f lds_float2;
+  lds_float* lds;   // LDS base + env slot (pack staging, [word][env])
+  lds_float* rows;  // LDS base of the wave's row regions
+  float* gbl;       // workspace base + env
   int n;
-  int cap;         // rows resident in LDS
-  PBG_DEV lds_float& mu(int c) const { return lds[(size_t)c * ES]; }
+  int cap;          // rows resident in LDS
+  int lane;         // lane in the wave (4 e + k)
   PBG_DEV lds_float& stage(int w) const { return lds[(size_t)w * ES]; }
-  // slot: the writing lane's branch for a branch contact, -1 for a base contact (every
-  // lane writes the same words then)
-  template <class P>
-  static PBG_DEV void put_at(P p, size_t st, int slot, const float* yb, const float* yB, float meff, float target) {
+  PBG_DEV lds_float* P(int r) const { return rows + (size_t)r * ES * W + PW * lane; }
+  PBG_DEV lds_float* S(int r) const { return rows + (size_t)r * ES * W + SOFF + 4 * (lane >> 2); }
+  // row words of lane k in the workspace ([word][env], stride n)
+  PBG_DEV float* gP(int r, int k) const { return gbl + ((size_t)r * W + (size_t)k * PW) * n; }
+  PBG_DEV float* gS(int r) const { return gbl + ((size_t)r * W + 4 * PW) * n; }
+  // slot: the writing lane's branch for a branch contact (the owner writes all four lanes'
+  // P), -1 for a base contact (every lane of the quad writes, each its own P)
+  PBG_DEV void put(int r, int slot, const float* yb, const float* yB, float meff, float target, float mu) const {
+    const int k0 = lane & 3;
+    auto pw = [&](int k, int i) -> float {  // word i of lane k's P
+      if (i < NDB) return k == slot ? yb[i] : 0.f;
+      if (i == NDB) return yB[k];
+      return k < 2 ? yB[k + 4] : 0.f;
+    };
+    if (r < cap) {
+      lds_float* p0 = rows + (size_t)r * ES * W + PW * (lane & ~3);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < 4; k++) {
+        if (slot < 0 && k != k0) continue;
+        float v[PW];
 #pragma unroll
-      for (int i = 0; i < NDB; i++) p[(k * NDB + i) * st] = k == slot ? yb[i] : 0.f;
+        for (int i = 0; i < PW; i++) v[i] = pw(k, i);
+        if constexpr (PW == 4) {
+          *(lds_float4*)(p0 + PW * k) = v4f{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int i = 0; i < PW; i++) p0[PW * k + i] = v[i];
+        }
+      }
+      *(lds_float4*)S(r) = v4f{meff, target, 0.f, mu};
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (slot < 0 && k != k0) continue;
+        float* q = gP(r, k);
+#pragma unroll
+        for (int i = 0; i < PW; i++) q[(size_t)i * n] = pw(k, i);
+      }
+      float* q = gS(r);
+      q[0] = meff; q[n] = target; q[2 * (size_t)n] = 0.f; q[3 * (size_t)n] = mu;
     }
-#pragma unroll
-    for (int g = 0; g < 6; g++) p[(YB + g) * st] = yB[g];
-    p[(YB + 6) * st] = 0.f;
-    p[(YB + 7) * st] = 0.f;
-    p[(YB + 8) * st] = meff;
-    p[(YB + 9) * st] = target;
-    p[(YB + 10) * st] = 0.f;
   }
   // One row in registers (loaded ahead of its update: PGS software pipelining): this
   // lane's branch slot and base slice.
   struct Row {
     float yb[NDB], yB[2], meff, tgt, lam;
   };
-  template <class P>
-  static PBG_DEV void load_at(P p, size_t st, int kb, Row& r) {
-#pragma unroll
-    for (int i = 0; i < NDB; i++) r.yb[i] = p[(kb * NDB + i) * st];
-    r.yB[0] = p[(YB + kb) * st];
-    r.yB[1] = p[(YB + 4 + kb) * st];
-    r.meff = p[(YB + 8) * st];
-    r.tgt = p[(YB + 9) * st];
-    r.lam = p[(YB + 10) * st];
-  }
   // LDS: every row of the wave is resident (the common case, no workspace branches)
   template <bool LDS>
   PBG_DEV void load(int r, int kb, Row& row) const {
-    if (LDS || r < cap) load_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, kb, row);
-    else load_at(gbl + (size_t)r * W * n, (size_t)n, kb, row);
+    if (LDS || r < cap) {
+      if constexpr (PW == 4) {
+        const v4f a = *(const lds_float4*)P(r);
+        row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
+      } else {
+        const lds_float* p = P(r);
+#pragma unroll
+        for (int i = 0; i < NDB; i++) row.yb[i] = p[i];
+        row.yB[0] = p[NDB]; row.yB[1] = p[NDB + 1];
+      }
+      // m_eff and target as one b64, lambda as a b32: a b128 whose fourth register (mu) is
+      // dead lets the allocator reuse it at once, and the write-after-write on the pending
+      // load forces an lgkmcnt(0) wait right behind the look-ahead load (no pipelining)
+      const v2f b = *(const lds_float2*)S(r);
+      row.meff = b.x; row.tgt = b.y; row.lam = S(r)[2];
+    } else {
+      const float* p = gP(r, kb);
+#pragma unroll
+      for (int i = 0; i < NDB; i++) row.yb[i] = p[(size_t)i * n];
+      row.yB[0] = p[(size_t)NDB * n]; row.yB[1] = p[(size_t)(NDB + 1) * n];
+      const float* q = gS(r);
+      row.meff = q[0]; row.tgt = q[n]; row.lam = q[2 * (size_t)n];
+    }
   }
   template <bool LDS>
   PBG_DEV void set_lam(int r, float v) const {
-    if (LDS || r < cap) lds[(size_t)(HEAD + r * W + YB + 10) * ES] = v;
-    else gbl[((size_t)r * W + YB + 10) * n] = v;
+    if (LDS || r < cap) S(r)[2] = v;
+    else gS(r)[2 * (size_t)n] = v;
   }
+  // friction bound of contact c: mu * lambda of its normal row (one ds_read_b64)
   template <bool LDS>
-  PBG_DEV float get_lam(int r) const {
-    if (LDS || r < cap) return lds[(size_t)(HEAD + r * W + YB + 10) * ES];
-    return gbl[((size_t)r * W + YB + 10) * n];
+  PBG_DEV float fric_limit(int c) const {
+    if (LDS || 3 * c < cap) {
+      const v2f v = *(const lds_float2*)(S(3 * c) + 2);
+      return v.y * v.x;
+    }
+    const float* q = gS(3 * c);
+    return q[3 * (size_t)n] * q[2 * (size_t)n];
   }
   // projected Gauss-Seidel update of a loaded row (u: the branch part ub, the base slice
   // uBs); returns the new impulse, bitwise identical in the four lanes
@@ -405,10 +459,6 @@ struct TRows {
 #pragma unroll
     for (int i = 0; i < NDB; i++) ub[i] += r.yb[i] * dl;
     return nl;
-  }
-  PBG_DEV void put(int r, int slot, const float* yb, const float* yB, float meff, float target) const {
-    if (r < cap) put_at(lds + (size_t)(HEAD + r * W) * ES, (size_t)ES, slot, yb, yB, meff, target);
-    else put_at(gbl + (size_t)r * W * n, (size_t)n, slot, yb, yB, meff, target);
   }
 };
 
@@ -461,14 +511,14 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
   Row A1, A2, B1, B2;
   rw.template load<LDS>(3 * c + 1, kb, A1);
   rw.template load<LDS>(3 * c + 2, kb, A2);
-  float limA = rw.mu(c) * rw.template get_lam<LDS>(3 * c), limB;
+  float limA = rw.template fric_limit<LDS>(c), limB;
   while (true) {
     bool more = pos != 0u;
     int c2 = more ? __builtin_ctz(pos) : c;
     pos &= pos - 1u;
     rw.template load<LDS>(3 * c2 + 1, kb, B1);
     rw.template load<LDS>(3 * c2 + 2, kb, B2);
-    limB = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
+    limB = rw.template fric_limit<LDS>(c2);
     rw.template set_lam<LDS>(3 * c + 1, RW::update(A1, ub, uB, -limA, limA));
     rw.template set_lam<LDS>(3 * c + 2, RW::update(A2, ub, uB, -limA, limA));
     if (!more) break;
@@ -478,7 +528,7 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
     pos &= pos - 1u;
     rw.template load<LDS>(3 * c2 + 1, kb, A1);
     rw.template load<LDS>(3 * c2 + 2, kb, A2);
-    limA = rw.mu(c2) * rw.template get_lam<LDS>(3 * c2);
+    limA = rw.template fric_limit<LDS>(c2);
     rw.template set_lam<LDS>(3 * c + 1, RW::update(B1, ub, uB, -limB, limB));
     rw.template set_lam<LDS>(3 * c + 2, RW::update(B2, ub, uB, -limB, limB));
     if (!more) break;
@@ -914,9 +964,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
       rw.put(3 * n0 + dir, -1, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f, (float)R::slot_mu[sl]);
     }
-    rw.mu(n0) = (float)R::slot_mu[sl];
     n0++;
   });
   // this branch's active slots, then their contact indices (exclusive quad prefix)
@@ -974,9 +1023,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
       rw.put(3 * ci + dir, kb, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f, pk<T::SMU, sl>(L));
     }
-    rw.mu(ci) = pk<T::SMU, sl>(L);
     ci++;
   });
   if (3 * nc > rw.cap) {  // rows in the device workspace: same-CU visibility
@@ -1215,6 +1263,8 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   });
   TRows<R, ES> rw;
   rw.lds = (lds_float*)lds_dyn + (threadIdx.x >> 2);
+  rw.rows = (lds_float*)lds_dyn + TRows<R, ES>::HEAD * ES;
+  rw.lane = threadIdx.x;
   rw.gbl = scratch + e;
   rw.n = B.n;
   rw.cap = lds_rows;
