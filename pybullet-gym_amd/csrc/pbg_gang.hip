@@ -31,8 +31,11 @@
 // Per-env LDS region (words), [gang-shared]:
 //   L (NNZ) | Ld (N) | u (YS) | sw (3N) | sv (3N) | body frames (12 NB) | limit pos (2 NLIM)
 //   | limit rows NLIM x (YS + 5) | contacts 0..cap-1 x PERC
-// contact c: descriptor (DW) | mu | 3 rows x (y (YS) | m_eff | target | lambda); contacts
-// at c >= cap live at the same offsets in the env's device workspace.
+// contact c: descriptor (DW) | mu | 3 rows x (y (YS) | m_eff | target | lambda); a row's y is
+// lane-major (lane t's NSL words y[t], y[t + T], ... contiguous: one ds_read_b64 for
+// Humanoid's two); contacts at c >= cap live at the same offsets in the env's device
+// workspace.  (Pairing m_eff | target and lambda | mu for b64 loads needs an even row length:
+// one word more per contact, which costs HalfCheetah at 8,192 envs one LDS-resident contact.)
 namespace pbg {
 
 #define PBG_GANG_BLOCK 256  // lanes per gang workgroup (4 waves)
@@ -300,9 +303,15 @@ struct Gang {
   static constexpr int YS = NSL * T;           // padded row length
   static constexpr int MAXC = R::NS + R::NPAIR;
   static constexpr int DW = 16;                // descriptor: rA 3 | rB 3 | n 3 | dist | fA | fB | mA | mB | floor | pad
-  static constexpr int CRW = YS + 3;           // y | m_eff | target | lambda
+  // rows of NSL = 2 robots (Humanoid) are laid out for one ds_read_b64 of a lane's y pair:
+  // an even row length, the first row at an even LDS word (the env region, FIXED and the
+  // record length are even)
+  static constexpr bool Y64 = NSL == 2;
+  static constexpr int CRW = YS + 3 + (Y64 ? 1 : 0);  // y (lane-major) | m_eff | target | lambda [| pad]
   static constexpr int LRW = YS + 5;           // y | m_eff | t_lo | t_hi | pad 2
-  static constexpr int PERC = DW + 1 + 3 * CRW;
+  static constexpr int RW0 = DW + 1;  // first row of a contact record (after descriptor and mu)
+  // word of generalized index i in a lane-major row: lane i % T, slice i / T
+  static constexpr int yw(int i) { return (i % T) * NSL + i / T; }
   static constexpr int NJ1 = R::NJ > 0 ? R::NJ : 1;
   static constexpr int BW = 27;                // body record: Rm 9 | x 3 | c 3 | w 3 | v 3 | al 3 | ac 3
   static constexpr int FW = 12;                // its frame part (Rm | x) lives at O_FR, stride FW; the
@@ -314,7 +323,8 @@ struct Gang {
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
   static constexpr int LRSZ = NLIM * LRW > NB * CW ? NLIM * LRW : NB * CW;
-  static constexpr int FIXED = O_LR + LRSZ;
+  static constexpr int FIXED = O_LR + LRSZ + (Y64 ? ((O_LR + LRSZ + RW0) & 1) : 0);  // Y64: rows start even
+  static constexpr int PERC = RW0 + 3 * CRW + (Y64 ? ((RW0 + 3 * CRW) & 1) : 0);
   // the kinematic parts are dead once M and the bias are built, before any contact is
   // written: they share the start of the contact area (the env region holds >= KW*NB words)
   static constexpr int O_KV = FIXED;
@@ -379,29 +389,45 @@ struct GRow {
 template <class R, int T, bool LDS>
 PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
   using G = Gang<R, T>;
-  const int w0 = G::DW + 1 + dir * G::CRW;
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const v2f lds_v2f;
+  const int w0 = G::RW0 + dir * G::CRW;
   if (LDS || c < X.cap) {
     const lds_float* p = X.l + G::FIXED + c * G::PERC + w0;
+    if constexpr (G::Y64) {
+      static_assert((G::FIXED + G::RW0) % 2 == 0 && G::PERC % 2 == 0 && G::CRW % 2 == 0, "b64 rows");
+      const v2f a = *(lds_v2f*)(p + 2 * X.t);
+      r.y[0] = a.x; r.y[1] = a.y;
+    } else {
 #pragma unroll
-    for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t + m * T];
+      for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t * G::NSL + m];
+    }
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   } else {
     const float* p = X.g + (size_t)c * G::PERC + w0;
 #pragma unroll
-    for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t + m * T];
+    for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t * G::NSL + m];
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   }
 }
+// friction bound of contact c: mu * lambda of its normal row
 template <class R, int T, bool LDS>
-PBG_DEV float gang_load_word(const GangCtx& X, int c, int w) {
+PBG_DEV float gang_fric_limit(const GangCtx& X, int c) {
   using G = Gang<R, T>;
-  if (LDS || c < X.cap) return X.l[G::FIXED + c * G::PERC + w];
-  return X.g[(size_t)c * G::PERC + w];
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const v2f lds_v2f;
+  constexpr int w = G::RW0 + G::YS + 2;
+  if (LDS || c < X.cap) {
+    const lds_float* p = X.l + G::FIXED + c * G::PERC;
+    return p[G::DW] * p[w];
+  }
+  const float* p = X.g + (size_t)c * G::PERC;
+  return p[G::DW] * p[w];
 }
 template <class R, int T, bool LDS>
 PBG_DEV void gang_set_lam(const GangCtx& X, int c, int dir, float v) {
   using G = Gang<R, T>;
-  const int w = G::DW + 1 + dir * G::CRW + G::YS + 2;
+  const int w = G::RW0 + dir * G::CRW + G::YS + 2;
   if (X.t == 0) {
     if (LDS || c < X.cap) X.l[G::FIXED + c * G::PERC + w] = v;
     else X.g[(size_t)c * G::PERC + w] = v;
@@ -424,14 +450,18 @@ PBG_DEV float gang_update(const GRow<R, T>& r, float* us, float lo, float hi) {
 // One PGS sweep over the contact rows in Bullet's order: all normals, then the two friction
 // rows of each contact whose normal impulse came out positive [EXT], box-clamped at
 // mu * lambda_n.  Rows are loaded one step ahead of their update (two register sets
-// alternate); the look-ahead loads are unconditional (a finished gang re-reads a valid row),
-// and the normal pass records the positive impulses in a bitmask, so the friction pass walks
-// those contacts without a load-then-test round trip.  The loop runs while any gang of the
-// wave has rows left; a finished gang skips the updates.
+// alternate); the look-ahead loads are unconditional (the last row re-reads itself), and the
+// normal pass records the positive impulses in a bitmask, so the friction pass walks those
+// contacts without a load-then-test round trip.  Each gang leaves the loops on its own
+// (the DPP reductions stay inside the gang's row of 16 lanes): with a wave-uniform loop and a
+// masked update, a finished gang's look-ahead registers stayed pending on the skipped path
+// and the compiler's wait at the loop head drained every LDS load (lgkmcnt(0)), so no row's
+// loads overlapped the previous update.
 template <class R, int T, bool LDS>
 PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
   using G = Gang<R, T>;
   using Row = GRow<R, T>;
+  if (nc <= 0) return;
   // positive normal impulses, one bit per contact in NW 32-bit words (Hopper, Walker2D,
   // HalfCheetah: one word; Humanoid: three), set and walked branch-free (selects over the
   // words) -- the 64-bit mask with a branch per word cost 6-8 % of the step.
@@ -460,21 +490,17 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
     Row A, B;
     gang_load_row<R, T, LDS>(X, 0, 0, A);
     int c = 0;
-    while (wave_any(c < nc)) {
-      gang_load_row<R, T, LDS>(X, max(0, min(c + 1, nc - 1)), 0, B);
-      if (c < nc) {
-        const float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
-        gang_set_lam<R, T, LDS>(X, c, 0, nl);
-        mark(c, nl);
-      }
-      if (!wave_any(++c < nc)) break;
-      gang_load_row<R, T, LDS>(X, max(0, min(c + 1, nc - 1)), 0, A);
-      if (c < nc) {
-        const float nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
-        gang_set_lam<R, T, LDS>(X, c, 0, nl);
-        mark(c, nl);
-      }
-      ++c;
+    while (true) {
+      gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, B);
+      float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+      gang_set_lam<R, T, LDS>(X, c, 0, nl);
+      mark(c, nl);
+      if (++c >= nc) break;
+      gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, A);
+      nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
+      gang_set_lam<R, T, LDS>(X, c, 0, nl);
+      mark(c, nl);
+      if (++c >= nc) break;
     }
   }
   // next contact with a positive normal impulse (-1: none left)
@@ -495,42 +521,33 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
     });
     return c;
   };
-  constexpr int WN = G::DW + 1 + G::YS + 2;  // the normal row's lambda
   int c = next();
-  if (!wave_any(c >= 0)) return;
+  if (c < 0) return;
   Row A1, A2, B1, B2;
-  float limA, limB;
-  {
-    const int cc = max(c, 0);
-    gang_load_row<R, T, LDS>(X, cc, 1, A1);
-    gang_load_row<R, T, LDS>(X, cc, 2, A2);
-    limA = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
-  }
+  gang_load_row<R, T, LDS>(X, c, 1, A1);
+  gang_load_row<R, T, LDS>(X, c, 2, A2);
+  float limA = gang_fric_limit<R, T, LDS>(X, c), limB;
   while (true) {
     int c2 = next();
-    {
-      const int cc = max(c2, 0);
-      gang_load_row<R, T, LDS>(X, cc, 1, B1);
-      gang_load_row<R, T, LDS>(X, cc, 2, B2);
-      limB = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
-    }
-    if (c >= 0) {
-      gang_set_lam<R, T, LDS>(X, c, 1, gang_update<R, T>(A1, us, -limA, limA));
-      gang_set_lam<R, T, LDS>(X, c, 2, gang_update<R, T>(A2, us, -limA, limA));
-    }
-    if (!wave_any(c2 >= 0)) break;
-    c = next();
-    {
-      const int cc = max(c, 0);
-      gang_load_row<R, T, LDS>(X, cc, 1, A1);
-      gang_load_row<R, T, LDS>(X, cc, 2, A2);
-      limA = gang_load_word<R, T, LDS>(X, cc, G::DW) * gang_load_word<R, T, LDS>(X, cc, WN);
-    }
-    if (c2 >= 0) {
-      gang_set_lam<R, T, LDS>(X, c2, 1, gang_update<R, T>(B1, us, -limB, limB));
-      gang_set_lam<R, T, LDS>(X, c2, 2, gang_update<R, T>(B2, us, -limB, limB));
-    }
-    if (!wave_any(c >= 0)) break;
+    const bool more = c2 >= 0;
+    c2 = more ? c2 : c;  // the last look-ahead re-reads the current contact
+    gang_load_row<R, T, LDS>(X, c2, 1, B1);
+    gang_load_row<R, T, LDS>(X, c2, 2, B2);
+    limB = gang_fric_limit<R, T, LDS>(X, c2);
+    gang_set_lam<R, T, LDS>(X, c, 1, gang_update<R, T>(A1, us, -limA, limA));
+    gang_set_lam<R, T, LDS>(X, c, 2, gang_update<R, T>(A2, us, -limA, limA));
+    if (!more) break;
+    c = c2;
+    c2 = next();
+    const bool more2 = c2 >= 0;
+    c2 = more2 ? c2 : c;
+    gang_load_row<R, T, LDS>(X, c2, 1, A1);
+    gang_load_row<R, T, LDS>(X, c2, 2, A2);
+    limA = gang_fric_limit<R, T, LDS>(X, c2);
+    gang_set_lam<R, T, LDS>(X, c, 1, gang_update<R, T>(B1, us, -limB, limB));
+    gang_set_lam<R, T, LDS>(X, c, 2, gang_update<R, T>(B2, us, -limB, limB));
+    if (!more2) break;
+    c = c2;
   }
 }
 
@@ -1069,12 +1086,12 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       p[YS + 1] = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
       p[YS + 2] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
     } else {
-      const int w0r = G::DW + 1 + dir * G::CRW;
+      const int w0r = G::RW0 + dir * G::CRW;
       const float tgt = dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f;
       contact_at<R, T>(X, c, [&](auto p0) {
         auto p = p0 + w0r;
 #pragma unroll
-        for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
+        for (int i = 0; i < YS; i++) p[G::yw(i)] = i < N ? y[i] : 0.f;
         p[YS] = meff;
         p[YS + 1] = tgt;
         p[YS + 2] = 0.f;

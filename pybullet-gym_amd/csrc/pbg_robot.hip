@@ -101,6 +101,7 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     g->block = PBG_GANG_BLOCK;
     g->lds_rows = cap;
     g->env_words = G::FIXED + (cap * G::PERC > G::MIN_CONTACT_WORDS ? cap * G::PERC : G::MIN_CONTACT_WORDS);
+    g->env_words += g->env_words & 1;  // even: every env region 8-byte aligned (b64 row loads)
     g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
     g->scratch_words_per_env = G::GWORDS;
     const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;
