@@ -53,7 +53,8 @@ typedef struct {
   int n_feet;
   int state_words;       /* per-env physical state record (see pbg_get_state) */
   int aux_words;         /* per-env bookkeeping record (see pbg_get_state) */
-  int substeps;          /* stepSimulation sub-steps per env step (scene_bases.py:65) */
+  int substeps;          /* stepSimulation sub-steps per env step (the handle's frame_skip,
+                            scene_bases.py:73 numSubSteps) */
   int max_episode_steps; /* gym TimeLimit (envs/__init__.py) */
   int reset_dofs;        /* joints randomised by reset (robot_locomotors.py:18-19) */
   int floating;
@@ -97,6 +98,26 @@ typedef struct {
   int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics */
 } pbg_debug_opts_t;
 
+/* Scene / World parameters (scene_bases.py:8-18 Scene(gravity, timestep, frame_skip), 58-73
+ * World: setGravity, numSolverIterations, numSubSteps).  pbg_default_sim_params fills the values
+ * the reference's env constructs its scene with (gym_locomotion_envs.py:18-19 StadiumScene(9.8,
+ * 0.0165/4, 4); gym_pendulum_envs.py:14 SingleRobotEmptyScene(9.8, 0.0165, 1); iterations 5,
+ * scene_bases.py:65) plus the solver ERPs the kernels use; pbg_create_ex takes a modified copy.
+ * An env step is frame_skip sub-steps of `timestep` seconds; the potential divides by
+ * Scene.dt = timestep * frame_skip (scene_bases.py:17); HumanoidFlagrun's flag timeout is
+ * 600 / frame_skip steps (robot_locomotors.py:218). */
+typedef struct {
+  double gravity;         /* m/s^2 along -z (World.gravity; 0 = weightless) */
+  double timestep;        /* seconds per physics sub-step (Scene.timestep), in (0, 0.1] */
+  int frame_skip;         /* sub-steps per env step (Scene.frame_skip = numSubSteps), 1..64 */
+  int solver_iterations;  /* PGS sweeps per sub-step (World.numSolverIterations), 1..1000 */
+  double contact_erp;     /* [0, 1]: share of a contact penetration corrected per sub-step */
+  double joint_limit_erp; /* [0, 1]: share of a joint-limit violation corrected per sub-step */
+} pbg_sim_params_t;
+
+/* The reference's parameters for env_id (see pbg_sim_params_t). */
+int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out);
+
 /* gym.make(env_id) for n envs (envs/__init__.py:4-103 registry entries; the env's
  * physics client is created here instead of lazily in BaseBulletEnv._reset,
  * env_bases.py:46-56).  env_id (robot_id order): "InvertedPendulumPyBulletEnv-v0",
@@ -109,6 +130,12 @@ int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int en
 /* pbg_create with test / diagnostic launch options (opts NULL = pbg_create). */
 int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                      const pbg_debug_opts_t* opts, pbg_handle** out);
+/* pbg_create with the scene built from `params` (NULL = pbg_default_sim_params) and test /
+ * diagnostic launch options (NULL = defaults).  PBG_E_ARG for parameters out of range. */
+int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                  const pbg_sim_params_t* params, const pbg_debug_opts_t* opts, pbg_handle** out);
+/* The parameters a handle was created with. */
+int pbg_get_sim_params(const pbg_handle* h, pbg_sim_params_t* out);
 /* BaseBulletEnv._close (env_bases.py:103-107) */
 void pbg_destroy(pbg_handle* h);
 /* action_space / observation_space / model sizes (robot_bases.py:24-27) */

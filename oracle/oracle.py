@@ -49,6 +49,7 @@ def lib():
                                          ctypes.c_int, P]
         L.pbg_oracle_count_flops.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
         L.pbg_oracle_set_physics.argtypes = [P, ctypes.c_int]
+        L.pbg_oracle_set_sim_params.argtypes = [P]
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
         L.pbg_oracle_pack_flag.argtypes = [ctypes.c_int, P, P, P, P]
         L.pbg_oracle_set_rng.argtypes = [ctypes.c_uint64, ctypes.c_int]
@@ -118,6 +119,20 @@ class OracleEnvs:
                                         _p(rew), _p(done), _p(nc), self.nthreads, _p(self.csig), _p(self.terms),
                                         self.precision, _p(self.asig)) == 0
         return obs, rew, done.astype(bool), nc
+
+
+SIM_PARAM_FIELDS = ("gravity", "timestep", "frame_skip", "solver_iterations", "contact_erp", "joint_limit_erp")
+
+
+def set_sim_params(params: dict = None):
+    """The scene of the product's pbg_create_ex (include/pbg.h pbg_sim_params_t) for every
+    following oracle call: ``params`` maps all six SIM_PARAM_FIELDS; None restores the
+    reference's scene."""
+    if params is None:
+        lib().pbg_oracle_set_sim_params(None)
+        return
+    v = np.array([float(params[k]) for k in SIM_PARAM_FIELDS], np.float64)
+    lib().pbg_oracle_set_sim_params(v.ctypes.data_as(ctypes.c_void_p))
 
 
 def set_mca_seed(seed: int):

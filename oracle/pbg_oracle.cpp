@@ -59,7 +59,7 @@ int g_flags = 0;
 enum { OPT_CONTACT_ERP, OPT_DEEP_ERP, OPT_DEEP_THR, OPT_DEEP_MODE, OPT_LIMIT_MODE, OPT_DAMP_MODE, OPT_FRIC_MODE,
        OPT_WARM, OPT_WARM_FRIC, OPT_LIMIT_ERP, OPT_ITERS, OPT_SEP_MODE, OPT_SLOP, OPT_SEP_ABS, OPT_LIM_SEP_ABS,
        OPT_SPRINGS, OPT_ROLL_MU, OPT_SPIN_MU, OPT_LIM_DEEP_MODE, OPT_LIMIT_CFM, OPT_CONTACT_CFM, OPT_CONTACT_THR,
-       OPT_MARGIN, OPT_SELF_COLLISION, OPT_COUNT };
+       OPT_MARGIN, OPT_SELF_COLLISION, OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_COUNT };
 double g_opt[OPT_COUNT];
 const double g_opt_default[OPT_COUNT] = {
     -1.0,             // contact ERP of penetrating contact normal rows (-1: the model's, models_gen.h)
@@ -77,7 +77,7 @@ const double g_opt_default[OPT_COUNT] = {
     0.0,              // linear slop added to the contact distance
     1.0,              // separated contact rows: 1 = J nu_new >= -d/dt (Bullet's absolute rhs), 0 = J dnu >= -d/dt
     1.0,              // separated joint-limit rows: the same choice
-    0.0,              // joint springs: scale on the MJCF stiffness table (pbg_oracle_set_springs): tau -= s k q
+    1.0,              // joint springs: scale on the model's stiffness (mjcf.py B7): tau -= s k q
     0.0,              // rolling friction: combined coefficient of two angular rows about the contact tangents
     0.0,              // spinning friction: combined coefficient of an angular row about the contact normal
     0.0,              // joint-limit violations deeper than OPT_DEEP_THR: 0 = OPT_LIMIT_ERP, 1 = velocity only
@@ -88,14 +88,15 @@ const double g_opt_default[OPT_COUNT] = {
     PBG_CONTACT_THRESHOLD,  // contact processing / breaking threshold
     0.0,              // collision margin added around every robot geom (MJCF geom margin)
     1.0,              // self-collision pairs: 1 = on (URDF_USE_SELF_COLLISION, robot_bases.py:116), 0 = off
+    PBG_GRAVITY,      // scene gravity (pbg_oracle_set_sim_params, the product's pbg_sim_params_t)
+    -1.0,             // sub-step timestep (-1: the model's dt_sub)
+    -1.0,             // sub-steps per env step (-1: the model's frame_skip)
 };
 struct OptInit { OptInit() { for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = g_opt_default[i]; } } g_opt_init;
 // persistent contact impulses per env and collision candidate (warm starting):
 // [env][candidate][normal, t1, t2, active]
 double* g_cache = nullptr;
 size_t g_cache_n = 0;
-#define MAX_ROBOTS 15
-double g_springs[MAX_ROBOTS][MAXD];  // rule study: MJCF joint stiffness per robot and dof
 // contact diagnostics (pbg_oracle_contact_diag; single env, single thread): per contact of every
 // sub-step [sub, candidate, dist, lambda_n, lambda_t1, lambda_t2, mu, v_n, v_t1, v_t2] after the solve
 double* g_diag = nullptr;
@@ -110,7 +111,7 @@ struct MV {
   const int *link_parent, *link_jtype, *link_dof;
   const double (*off_pos)[3], (*axis)[3], (*anchor)[3], (*com)[3], (*off_quat)[4], (*inertia)[6];
   const double* mass;
-  const double *lower, *upper, *damping, *armature;
+  const double *lower, *upper, *damping, *stiffness, *armature;
   const int *limited, *dof_jtype;
   const int* act_dof; const double* act_gain;
   const int* obs_dof; const double* obs_vel_scale; const int* reset_dof; const double* reset_offset;
@@ -135,7 +136,7 @@ MV view() {
   m.link_dof = R::link_dof; m.off_pos = R::link_offset_pos; m.axis = R::link_axis;
   m.anchor = R::link_anchor; m.com = R::link_com; m.off_quat = R::link_offset_quat;
   m.inertia = R::link_inertia; m.mass = R::link_mass; m.lower = R::dof_lower; m.upper = R::dof_upper;
-  m.damping = R::dof_damping; m.armature = R::dof_armature; m.limited = R::dof_limited;
+  m.damping = R::dof_damping; m.stiffness = R::dof_stiffness; m.armature = R::dof_armature; m.limited = R::dof_limited;
   m.dof_jtype = R::dof_jtype; m.act_dof = R::act_dof; m.act_gain = R::act_gain;
   m.obs_dof = R::obs_dof; m.obs_vel_scale = R::obs_vel_scale; m.reset_dof = R::reset_dof;
   m.reset_offset = R::reset_offset;
@@ -145,6 +146,13 @@ MV view() {
   m.pb0 = R::pair_b0; m.pb1 = R::pair_b1; m.pra = R::pair_ra; m.prb = R::pair_rb; m.pmu = R::pair_mu;
   return m;
 }
+
+// the scene parameters in force (pbg_oracle_set_sim_params): sub-step, frame_skip, Scene.dt,
+// HumanoidFlagrun's flag timeout 600 / frame_skip rounded up (robot_locomotors.py:218-223)
+double sim_dt(const MV& m) { return g_opt[OPT_DT] > 0.0 ? g_opt[OPT_DT] : m.dt_sub; }
+int sim_substeps(const MV& m) { return g_opt[OPT_SUBSTEPS] > 0.0 ? (int)g_opt[OPT_SUBSTEPS] : m.substeps; }
+double sim_env_dt(const MV& m) { return sim_dt(m) * sim_substeps(m); }
+int sim_flag_timeout(const MV& m) { return (600 + sim_substeps(m) - 1) / sim_substeps(m); }
 
 const MV* model(int robot) {
   static MV views[15] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
@@ -250,7 +258,7 @@ void flag_draw(int e, Flag& f) {
   const double u0 = (double)(c[0] >> 8) * (1.0 / 16777216.0), u1 = (double)(c[1] >> 8) * (1.0 / 16777216.0);
   f.tx = (-PBG_STADIUM_HALFLEN + 2.0 * PBG_STADIUM_HALFLEN * u0) * PBG_FLAG_COMPACT;
   f.ty = (-PBG_STADIUM_HALFWIDTH + 2.0 * PBG_STADIUM_HALFWIDTH * u1) * PBG_FLAG_COMPACT;
-  f.timeout = PBG_FLAG_TIMEOUT;
+  f.timeout = sim_flag_timeout(*model(8));  // HumanoidFlagrun
   f.count++;
 }
 
@@ -287,12 +295,13 @@ typedef struct {
 
 void pbg_oracle_set_flags(int flags) { g_flags = flags; }
 
-// Joint stiffness table of the rule study (MJCF <joint stiffness>, dof order); the spring
-// torque -OPT_SPRINGS * k_d * q_d enters only when OPT_SPRINGS != 0.
-int pbg_oracle_set_springs(int robot, const double* k, int n) {
-  const MV* mp = model(robot);
-  if (!mp || robot < 0 || robot >= MAX_ROBOTS) return -1;
-  for (int d = 0; d < MAXD; d++) g_springs[robot][d] = (k && d < n) ? k[d] : 0.0;
+
+// The scene of the product's pbg_create_ex (include/pbg.h pbg_sim_params_t, fields in order):
+// v = [gravity, timestep, frame_skip, solver_iterations, contact_erp, joint_limit_erp]; NULL
+// restores the reference's scene.  The other rule options are left as they are.
+int pbg_oracle_set_sim_params(const double* v) {
+  const int ids[6] = {OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_ITERS, OPT_CONTACT_ERP, OPT_LIMIT_ERP};
+  for (int i = 0; i < 6; i++) g_opt[ids[i]] = v ? v[i] : g_opt_default[ids[i]];
   return 0;
 }
 
@@ -335,7 +344,7 @@ int pbg_oracle_info(int robot, int* out) {
   if (!m) return -1;
   int v[] = {m->NL, m->NJ, m->NDOF, m->NA, m->NO, m->NR, m->NF, m->NP, m->NS, m->NPAIR, m->OBS,
              PBG_BASE_WORDS + 2 * m->NJ, PBG_AUX_RECORD_WORDS(m->NF, m->flagrun), m->floating, m->kind,
-             m->substeps};
+             sim_substeps(*m)};
   memcpy(out, v, sizeof(v));
   return 0;
 }
@@ -414,7 +423,7 @@ static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* ou
   out->initial_z = z0;
   out->pitch = rpy[1];
   out->at_limit = at_limit;
-  double dt = m.dt_sub * m.substeps;  // scene.dt = timestep*frame_skip (scene_bases.py:17)
+  double dt = sim_env_dt(m);  // scene.dt = timestep*frame_skip (scene_bases.py:17)
   out->potential = -dist / dt;         // robot_locomotors.py:79
   for (int i = 0; i < m.NF; i++) out->feet_out[i] = in->feet_prev[i];
   if (!in->act) {
@@ -476,7 +485,7 @@ static void flag_pack(int robot, const MV& m, pbg_pack_in* in, pbg_pack_out* out
   in->target_x = f.tx; in->target_y = f.ty;
   pbg_oracle_pack(robot, in, out);
   if (out->dist < 1.0 || f.timeout <= 0) {
-    if (next) { f.tx = next[0]; f.ty = next[1]; f.timeout = PBG_FLAG_TIMEOUT; f.count++; }
+    if (next) { f.tx = next[0]; f.ty = next[1]; f.timeout = sim_flag_timeout(m); f.count++; }
     else flag_draw(e, f);
     in->target_x = f.tx; in->target_y = f.ty;
     pbg_oracle_pack(robot, in, out);
@@ -523,7 +532,7 @@ static void mujoco_planar_obs(const MV& m, const double* jq, const double* jqd, 
   out->potential = x_after; out->initial_z = 0.0; out->dist = 0.0;
   for (int i = 0; i < 5; i++) out->rewards[i] = 0.0;
   if (!act) { out->reward = 0.0; out->done = 0; return; }
-  const double potential = (x_after - x_before) / (m.dt_sub * m.substeps);
+  const double potential = (x_after - x_before) / sim_env_dt(m);
   float sq[MAXD];
   for (int i = 0; i < m.NA; i++) sq[i] = act[i] * act[i];
   const float power_cost = (float)m.power_cost * np_sum_f32(sq, m.NA);

@@ -188,7 +188,7 @@ template <class T> void mass_and_bias(const MV& m, const KinT<T>& k, T M[MAXD][M
     C[i] = T(0);
     for (int j = 0; j < n; j++) M[i][j] = T(0);
   }
-  const V3T<T> g = v3(T(0), T(0), T((g_flags & 16) ? 0.0 : -PBG_GRAVITY));
+  const V3T<T> g = v3(T(0), T(0), T((g_flags & 16) ? 0.0 : -g_opt[OPT_GRAVITY]));
   const T kd_lin((g_flags & 4) ? 0.0 : PBG_LINEAR_DAMPING);
   const T kd_ang((g_flags & 4) ? 0.0 : PBG_ANGULAR_DAMPING);
   T Jv[3][MAXD], Jw[3][MAXD];
@@ -418,7 +418,7 @@ template <class T> inline T clampv(T v) {
 template <class T>
 int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint32_t* sig, double* cache,
             const T* qd_step, uint32_t* asig) {
-  const T dt(m.dt_sub);
+  const T dt(sim_dt(m));
   const int n = m.NDOF;
   static thread_local KinT<T> k;
   static thread_local T M[MAXD][MAXD];
@@ -434,9 +434,12 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   const T* qdd_src = g_opt[OPT_DAMP_MODE] != 0.0 ? qd_step : qd0;  // applyJointDamping once per step
   for (int d = 0; d < m.NJ; d++)
     rhs[gidx(m, d)] = rhs[gidx(m, d)] + (tau[d] - ((g_flags & 8) ? T(0) : T(m.damping[d]) * qdd_src[d]));
-  if (g_opt[OPT_SPRINGS] != 0.0)  // rule study: MJCF joint stiffness as a spring to q = 0
+  // joint springs tau = -k*q (mjcf.py B7: MJCF <joint stiffness>, explicit per sub-step like the
+  // damping; the rule study scales k by OPT_SPRINGS, 0 = none)
+  if (g_opt[OPT_SPRINGS] != 0.0)
     for (int d = 0; d < m.NJ; d++)
-      rhs[gidx(m, d)] = rhs[gidx(m, d)] - T(g_opt[OPT_SPRINGS] * g_springs[m.robot_id][d]) * s[PBG_BASE_WORDS + d];
+      if (m.stiffness[d] != 0.0)
+        rhs[gidx(m, d)] = rhs[gidx(m, d)] - T(g_opt[OPT_SPRINGS] * m.stiffness[d]) * s[PBG_BASE_WORDS + d];
   cholesky(n, M);
   chol_solve(n, M, rhs, qdd);
   // generalized velocity nu = [v_base, w_base, qd]
@@ -647,7 +650,7 @@ int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_acti
   }
   for (int d = 0; d < m.NJ; d++) qd_step[d] = s[PBG_BASE_WORDS + m.NJ + d];
   int nc = 0;
-  for (int sub = 0; sub < m.substeps; sub++) nc = substep<T>(m, s, tau, slot_active, sub, sig, cache, qd_step, asig);
+  for (int sub = 0; sub < sim_substeps(m); sub++) nc = substep<T>(m, s, tau, slot_active, sub, sig, cache, qd_step, asig);
   for (int i = 0; i < SD; i++) state[i] = (double)s[i];
   return nc;
 }

@@ -42,6 +42,16 @@ class DebugOpts(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_int), ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int)]
 
 
+class SimParams(ctypes.Structure):
+    """pbg_sim_params_t: the scene of a handle (scene_bases.py:8-18,58-73)."""
+    _fields_ = [("gravity", ctypes.c_double), ("timestep", ctypes.c_double), ("frame_skip", ctypes.c_int),
+                ("solver_iterations", ctypes.c_int), ("contact_erp", ctypes.c_double),
+                ("joint_limit_erp", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 _lib = None
 
 
@@ -59,6 +69,10 @@ def lib():
     L.pbg_create.restype = I
     L.pbg_create_debug.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(DebugOpts),
                                    ctypes.POINTER(H)]
+    L.pbg_create_ex.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(SimParams),
+                                ctypes.POINTER(DebugOpts), ctypes.POINTER(H)]
+    L.pbg_default_sim_params.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimParams)]
+    L.pbg_get_sim_params.argtypes = [H, ctypes.POINTER(SimParams)]
     L.pbg_sample_actions.argtypes = [I, I, I, ctypes.c_uint64, ctypes.c_uint32, I, P, P]
     L.pbg_destroy.argtypes = [H]
     L.pbg_destroy.restype = None
@@ -72,13 +86,15 @@ def lib():
     L.pbg_pack.argtypes = [ctypes.c_char_p, I, P, P, P]
     L.pbg_last_error.restype = ctypes.c_char_p
     for f in ("pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state", "pbg_set_state",
-              "pbg_pack_record_sizes", "pbg_pack", "pbg_create_debug", "pbg_sample_actions"):
+              "pbg_pack_record_sizes", "pbg_pack", "pbg_create_debug", "pbg_sample_actions", "pbg_create_ex",
+              "pbg_default_sim_params", "pbg_get_sim_params"):
         getattr(L, f).restype = I
     _lib = L
     return L
 
 
-EXPORTED = ("pbg_create", "pbg_create_debug", "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex",
+EXPORTED = ("pbg_create", "pbg_create_debug", "pbg_create_ex", "pbg_default_sim_params", "pbg_get_sim_params",
+            "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex",
             "pbg_get_state", "pbg_set_state", "pbg_pack_record_sizes", "pbg_pack", "pbg_sample_actions",
             "pbg_last_error")
 
@@ -87,6 +103,24 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = lib().pbg_last_error().decode(errors="replace")
         raise PbgError(f"{what} failed ({rc}): {msg}")
+
+
+def default_sim_params(env_id: str) -> SimParams:
+    """The scene parameters the reference builds env_id with (host-only call, no GPU needed)."""
+    p = SimParams()
+    check(lib().pbg_default_sim_params(env_id_bytes(env_id), ctypes.byref(p)), "pbg_default_sim_params")
+    return p
+
+
+def sim_params(env_id: str, overrides: dict = None) -> SimParams:
+    """default_sim_params(env_id) with the fields in `overrides` replaced (unknown keys raise)."""
+    p = default_sim_params(env_id)
+    names = {n for n, _ in SimParams._fields_}
+    for k, v in (overrides or {}).items():
+        if k not in names:
+            raise PbgError(f"unknown sim parameter {k!r}; known: {sorted(names)}")
+        setattr(p, k, v)
+    return p
 
 
 def env_id_bytes(env_id: str) -> bytes:

@@ -134,6 +134,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
     dof = dict(
         lower=[links[i].lower for i in dof_link], upper=[links[i].upper for i in dof_link],
         limited=[int(links[i].limited) for i in dof_link], damping=[links[i].damping for i in dof_link],
+        stiffness=[links[i].stiffness for i in dof_link],
         armature=[links[i].armature for i in dof_link], jtype=[links[i].jtype for i in dof_link],
         link=dof_link)
 
@@ -218,7 +219,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
         link_inertia=[inertia6(l.inertia) for l in links], link_chain_mask=chain_mask,
         link_anc_mask=anc_mask,
         dof_lower=dof["lower"], dof_upper=dof["upper"], dof_limited=dof["limited"],
-        dof_damping=dof["damping"], dof_armature=dof["armature"], dof_jtype=dof["jtype"],
+        dof_damping=dof["damping"], dof_stiffness=dof["stiffness"], dof_armature=dof["armature"], dof_jtype=dof["jtype"],
         dof_link=dof["link"],
         act_dof=act_dof, act_gain=act_gain, obs_dof=obs_dof, obs_vel_scale=vel_scale,
         reset_dof=reset_dof, reset_offset=[spec.reset_offset if i == 0 else 0.0 for i in range(len(reset_dof))],
@@ -306,7 +307,7 @@ def emit_struct(t: Dict) -> str:
     L.append(_arr2("link_offset_quat", "double", t["link_offset_quat"], 4))
     L.append(_arr2("link_inertia", "double", t["link_inertia"], 6))
     L.append(_arr1("link_mass", "double", t["link_mass"]))
-    for k in ("dof_lower", "dof_upper", "dof_damping", "dof_armature"):
+    for k in ("dof_lower", "dof_upper", "dof_damping", "dof_stiffness", "dof_armature"):
         L.append(_arr1(k, "double", t[k]))
     for k in ("dof_limited", "dof_jtype", "dof_link"):
         L.append(_arr1(k, "int", t[k]))

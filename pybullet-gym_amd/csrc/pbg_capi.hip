@@ -1,6 +1,7 @@
 // pbg_capi.hip -- the C-ABI (include/pbg.h).  Owns handles and device buffers and
 // dispatches to the per-robot launchers of pbg_robot.hip (one translation unit each).
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -55,6 +56,7 @@ struct Ops {
   int (*pack)(int, const double*, double*, hipStream_t);
   pbg_info_t info;
   int pack_in, pack_out;
+  pbg_sim_params_t defaults;
 };
 
 template <class R>
@@ -68,10 +70,37 @@ pbg_info_t info_of(int rid) {
   return I;
 }
 
+// the scene the reference's env builds (include/pbg.h pbg_sim_params_t)
+template <class R>
+pbg_sim_params_t defaults_of() {
+  pbg_sim_params_t p;
+  p.gravity = PBG_GRAVITY;
+  p.timestep = R::dt_sub;
+  p.frame_skip = R::substeps;
+  p.solver_iterations = PBG_SOLVER_ITERATIONS;
+  p.contact_erp = R::contact_erp;
+  p.joint_limit_erp = PBG_LIMIT_ERP;
+  return p;
+}
+
+int check_sim_params(const pbg_sim_params_t& p) {
+  if (!isfinite(p.gravity) || fabs(p.gravity) > 1000.0)
+    return fail(PBG_E_ARG, "pbg_create: gravity must be finite with |gravity| <= 1000%s%ld");
+  if (!(p.timestep > 0.0 && p.timestep <= 0.1))
+    return fail(PBG_E_ARG, "pbg_create: timestep must be in (0, 0.1]%s%ld");
+  if (p.frame_skip < 1 || p.frame_skip > 64)
+    return fail(PBG_E_ARG, "pbg_create: frame_skip must be in 1..64%s (got %ld)", "", p.frame_skip);
+  if (p.solver_iterations < 1 || p.solver_iterations > 1000)
+    return fail(PBG_E_ARG, "pbg_create: solver_iterations must be in 1..1000%s (got %ld)", "", p.solver_iterations);
+  if (!(p.contact_erp >= 0.0 && p.contact_erp <= 1.0) || !(p.joint_limit_erp >= 0.0 && p.joint_limit_erp <= 1.0))
+    return fail(PBG_E_ARG, "pbg_create: contact_erp and joint_limit_erp must be in [0, 1]%s%ld");
+  return PBG_OK;
+}
+
 #define PBG_OPS(NAME, RID)                                                                               \
   Ops{pbg::plan_##NAME, pbg::launch_step_##NAME, pbg::launch_reset_##NAME, pbg::launch_get_state_##NAME, \
       pbg::launch_set_state_##NAME, pbg::launch_pack_##NAME, info_of<pbg_models::NAME>(RID),             \
-      pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT}
+      pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT, defaults_of<pbg_models::NAME>()}
 
 const Ops* ops(int rid) {
   static const Ops table[15] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
@@ -119,23 +148,39 @@ struct pbg_handle {
   float* scratch;
   pbg::Geometry geo;
   pbg_info_t info;
+  pbg_sim_params_t params;
 };
 
 extern "C" {
 
 const char* pbg_last_error(void) { return g_err; }
 
+int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out) {
+  const int rid = env_robot_id(env_id);
+  if (rid < 0) return fail(PBG_E_ENV, "pbg_default_sim_params: unknown env id '%s'%ld", env_id ? env_id : "(null)");
+  if (!out) return fail(PBG_E_ARG, "pbg_default_sim_params: out is NULL%s%ld");
+  *out = ops(rid)->defaults;
+  return PBG_OK;
+}
+
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out) {
-  return pbg_create_debug(env_id, n_envs, device, seed, env_offset, nullptr, out);
+  return pbg_create_ex(env_id, n_envs, device, seed, env_offset, nullptr, nullptr, out);
 }
 
 int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                      const pbg_debug_opts_t* opts, pbg_handle** out) {
+  return pbg_create_ex(env_id, n_envs, device, seed, env_offset, nullptr, opts, out);
+}
+
+int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                  const pbg_sim_params_t* params, const pbg_debug_opts_t* opts, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
   *out = nullptr;
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_create: unknown env id '%s'%ld", env_id ? env_id : "(null)");
   if (n_envs <= 0) return fail(PBG_E_ARG, "pbg_create: n_envs must be > 0%s (got %ld)", "", n_envs);
+  const pbg_sim_params_t sp = params ? *params : ops(rid)->defaults;
+  if (check_sim_params(sp)) return PBG_E_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return fail(PBG_E_HIP, "pbg_create: no HIP device %s%ld", "", device);
@@ -149,10 +194,14 @@ int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, 
   h->ops = o;
   h->info = o->info;
   h->info.n_envs = n_envs;
+  h->info.substeps = sp.frame_skip;
+  h->params = sp;
   pbg::Buffers& B = h->B;
   B.n = n_envs;
   B.seed = seed;
   B.env_offset = env_offset;
+  B.sp = pbg::resolve_sim_params(sp.timestep, sp.frame_skip, sp.solver_iterations, sp.gravity, sp.contact_erp,
+                                 sp.joint_limit_erp, PBG_ANGULAR_MOTION_THRESHOLD);
   const size_t n = (size_t)n_envs;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -198,6 +247,12 @@ void pbg_destroy(pbg_handle* h) {
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   delete h;
+}
+
+int pbg_get_sim_params(const pbg_handle* h, pbg_sim_params_t* out) {
+  if (!h || !out) return fail(PBG_E_ARG, "pbg_get_sim_params: NULL argument%s%ld");
+  *out = h->params;
+  return PBG_OK;
 }
 
 int pbg_info(const pbg_handle* h, pbg_info_t* out) {

@@ -128,7 +128,7 @@ struct GangDynTab {
   int me_i[NNZ], me_k[NNZ], me_b[NNZ];  // packed lower-triangle entries of M: rows, cols, composite
   float me_arm[NNZ];                     // armature on joint diagonals
   int g_body[N], g_dof[N];               // composite owning generalized index i; its joint dof (-1: base)
-  float damping[NJ1];
+  float damping[NJ1], stiffness[NJ1];
 };
 template <class R>
 constexpr int body_depth(int b) {
@@ -199,7 +199,10 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
     t.g_dof[i] = di;
     t.g_body[i] = di >= 0 ? R::dof_link[di] + 1 : 0;
   }
-  for (int d = 0; d < R::NJ; d++) t.damping[d] = (float)R::dof_damping[d];
+  for (int d = 0; d < R::NJ; d++) {
+    t.damping[d] = (float)R::dof_damping[d];
+    t.stiffness[d] = (float)R::dof_stiffness[d];
+  }
   return t;
 }
 template <class R>
@@ -341,6 +344,7 @@ struct GangCtx {
   int cap;       // contacts resident in LDS
   int t;         // lane in the gang
   int le;        // gang in the wave
+  SimP P;        // scene parameters (kernel arguments)
 };
 // word w (0..26) of body b's record: frame part (w < 12) or kinematic part
 template <class R, int T>
@@ -667,7 +671,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   using G = Gang<R, T>;
   auto& TD = GangTabs<R>::dyn(X.tabs);
   constexpr int NB = D::NB, N = R::NDOF, NLEV = gang_nlev<R>();
-  constexpr float g = (float)PBG_GRAVITY;
+  const float g = X.P.gravity;
   const bool w0 = X.t == 0;
   // base record and joint state (replicated registers -> LDS)
   if (w0) {
@@ -805,7 +809,10 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     f[0] = Jw_.x; f[1] = Jw_.y; f[2] = Jw_.z; f[3] = Fv.x; f[4] = Fv.y; f[5] = Fv.z;
     const f3 F = mk3(C[9], C[10], C[11]), Nn = mk3(C[12], C[13], C[14]);
     float r = -(dot3(swk, Nn) + dot3(svk, F));
-    if (d >= 0) r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
+    if (d >= 0) {
+      r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
+      if constexpr (has_springs<R>()) r -= TD.stiffness[d] * X.l[G::O_Q + d];  // mjcf.py B7
+    }
     X.l[G::O_RHS + k] = r;
   }
   PBG_GANG_SYNC
@@ -832,7 +839,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   using G = Gang<R, T>;
   auto& TB = GangTabs<R>::tab(X.tabs);
   constexpr int N = R::NDOF, NB = D::NB, NLIM = D::NLIM, NSL = G::NSL, YS = G::YS;
-  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
+  const SimP& P = X.P;
   const bool w0 = X.t == 0;  // the gang's writer for replicated values
   auto stage_solution = [&](const float* L, const float* Ld, const float* u) {
     if (w0) {
@@ -860,13 +867,13 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
 #pragma unroll
     for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
-    dyn_solve<R>(s, L, rhs, Ld, nu, u);
+    dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
     stage_solution(L, Ld, u);
   } else {
     // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
     {
       float L[D::NNZ], Ld[N], nu[N], u[N];
-      dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
+      dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
       STAMP(3)
       stage_solution(L, Ld, u);
     }
@@ -950,8 +957,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     if (act) {
       csig += pbg_contact_hash(sub, (uint32_t)sl);  // this lane's share of the signature
       const int c = nc + __popcll(bal & gang_mask & below);
-      const f3 P = mk3(cc.x, cc.y, cc.z - rad);
-      put_desc(c, P - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[TB.slot_body[sl]], 0u, 1.f, TB.slot_mu[sl]);
+      const f3 cp = mk3(cc.x, cc.y, cc.z - rad);
+      put_desc(c, cp - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[TB.slot_body[sl]], 0u, 1.f, TB.slot_mu[sl]);
     }
     nc += __popcll(mine);
   });
@@ -1083,11 +1090,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
       const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
       p[YS] = meff;
-      p[YS + 1] = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
-      p[YS + 2] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
+      p[YS + 1] = pos_target(plo, P.k_limit, P.k_sep);
+      p[YS + 2] = pos_target(phi, P.k_limit, P.k_sep);
     } else {
       const int w0r = G::RW0 + dir * G::CRW;
-      const float tgt = dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f;
+      const float tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
       contact_at<R, T>(X, c, [&](auto p0) {
         auto p = p0 + w0r;
 #pragma unroll
@@ -1118,7 +1125,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       llo[li] = 0.f; lhi[li] = 0.f;
     }
     const bool all_lds = !wave_any(nc > X.cap);  // every contact row of the wave in LDS
-    for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+    for (int it = 0; it < P.iterations; it++) {
 #pragma unroll
       for (int li = 0; li < NLIM; li++) {
         float part = 0.f;
@@ -1153,7 +1160,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
 #pragma unroll
     for (int i = 0; i < N; i++) { Ld[i] = X.l[G::O_LD + i]; u[i] = X.l[G::O_U + i]; }
-    integrate<R>(s, L, Ld, u, nu);
+    integrate<R>(s, L, Ld, u, nu, P);
   }
   PBG_GANG_SYNC  // the next sub-step's staging overwrites this one's LDS
   STAMP(6)
@@ -1209,10 +1216,16 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   X.l = lds + TT::WORDS + (threadIdx.x / T) * env_words;
   X.g = scratch + (size_t)e * G::GWORDS;
   X.cap = cap;
+  X.P = B.sp;
   const bool w0 = X.t == 0;
   STAMP_DECL
   State<R> s;
   load_state<R>(s, B.st, B.n, e);
+  // the pack's bookkeeping loads, issued here so their latency overlaps the physics
+  const int el = B.elapsed[e] + 1;
+  uint32_t flags = B.flags[e];
+  const double pot_old = B.pot[e];
+  const float z0_old = B.z0[e];
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
@@ -1233,15 +1246,13 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   int nc = 0;
   uint32_t csig = 0;  // per-lane share; gang-summed below
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++)
+  for (int sub = 0; sub < B.sp.substeps; sub++)
     nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits, (uint32_t)sub, csig SUB_STAMP_PASS);
   if (io.ncontact && w0) io.ncontact[e] = nc;
   if (io.csig) {
     const uint32_t sig = gang_sum_u32<T>(csig);
     if (w0) io.csig[e] = sig;
   }
-  const int el = B.elapsed[e] + 1;
-  uint32_t flags = B.flags[e];
   float obs[R::OBS];
   PackOut po;
   double pot_new = 0.0;
@@ -1249,11 +1260,13 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
   } else if constexpr (R::kind == 2) {
-    mujoco_planar_pack_state<R>(s, B.pot[e], act, obs, po);
+    mujoco_planar_pack_state<R>(s, pot_old, act, obs, po, B.sp.env_dt);
     pot_new = po.potential;
   } else {
     PackIn<R> in;
+    in.env_dt = B.sp.env_dt;
     gather<R>(s, flags & 1u, in);
+    STAMPX(12)
     uint32_t fnew = 0;
 #pragma unroll
     for (int f = 0; f < R::NF; f++) {
@@ -1265,8 +1278,8 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
       in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
     }
     in.feet_new = fnew;
-    in.potential_old = B.pot[e];
-    in.initial_z = B.z0[e];
+    in.potential_old = pot_old;
+    in.initial_z = z0_old;
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
     else flag_pack<R, 4>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, X.t);
     pot_new = po.potential;

@@ -44,9 +44,11 @@ __device__ unsigned long long g_stamps[16];
 #define STAMP_DECL unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_acc[16] = {0};
 #define STAMP(i) { __builtin_amdgcn_sched_barrier(0); unsigned long long _n = __builtin_amdgcn_s_memtime(); _st_acc[i] += _n - _st_t; _st_t = _n; __builtin_amdgcn_sched_barrier(0); }
 #define STAMP_FLUSH if ((threadIdx.x & 63) == 0) { for (int _i = 0; _i < 16; _i++) atomicAdd(&g_stamps[_i], _st_acc[_i]); }
+#define STAMPX(i) STAMP(i)  // finer split, diagnostic build only (no phase barrier in the product)
 #else
 #define STAMP_DECL
 #define STAMP(i) PBG_PHASE_BARRIER
+#define STAMPX(i)
 #define STAMP_FLUSH
 #endif
 
@@ -63,6 +65,14 @@ template <int A, int B>
 struct IntTab {
   int v[A][B];
 };
+
+// any joint spring (mjcf.py B7)?  Robots without one compile no spring term at all.
+template <class R>
+constexpr bool has_springs() {
+  for (int d = 0; d < R::NJ; d++)
+    if (R::dof_stiffness[d] != 0.0) return true;
+  return false;
+}
 
 template <class R>
 struct Dims {
@@ -421,7 +431,8 @@ struct Rows {
 // minus pos/dt when separated, positionalError = -erp pos/dt when penetrating) in absolute form:
 // a separated row admits an approach of at most pos/dt (speculative contact), a penetrating
 // one pushes out at erp * pos / dt.  Continuous at pos = 0.
-PBG_DEV float pos_target(float pos, float erp, float inv_dt) { return -(pos > 0.f ? 1.f : erp) * inv_dt * pos; }
+// k_pen / k_sep: the slopes -erp/dt and -1/dt of SimP (pbg_types.h), pre-formed on the host.
+PBG_DEV float pos_target(float pos, float k_pen, float k_sep) { return (pos > 0.f ? k_sep : k_pen) * pos; }
 
 // tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
 // of this sub-step's collision pass (feet contacts come from the last sub-step).
@@ -468,10 +479,10 @@ PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, f3* sw, f3* sv, f3& O) {
 // matrix and bias, its sparse Cholesky factor L (Ld = 1/diag), the predicted velocity
 // nu = clamp(nu + dt M^-1 (tau - C)) and u = L^T nu.  Shared by the lane and gang kernels.
 template <class R>
-PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs SUB_STAMP_ARGS) {
+PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs, const SimP& P SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
-  constexpr float g = (float)PBG_GRAVITY;
+  const float g = P.gravity;
 
   // --- phase A: one forward pass over the bodies: kinematics, velocities, bias
   // accelerations, and each body's inertia + wrench about the reference point O added
@@ -618,21 +629,25 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs 
     }
   }
   }
-#pragma unroll
-  for (int d = 0; d < NJ; d++) {
+  // joint damping -d qd and springs -k q (mjcf.py B6 / B7), explicit from this sub-step's state
+  static_for<0, NJ>([&](auto d_c) {
+    constexpr int d = decltype(d_c)::value;
     L[D::lidx(D::gj(d), D::gj(d))] += (float)R::dof_armature[d];
-    rhs[D::gj(d)] += tau[d] - (float)R::dof_damping[d] * s.qd[d];
-  }
+    float r = tau[d];
+    if constexpr (R::dof_damping[d] != 0.0) r -= (float)R::dof_damping[d] * s.qd[d];
+    if constexpr (R::dof_stiffness[d] != 0.0) r -= (float)R::dof_stiffness[d] * s.q[d];
+    rhs[D::gj(d)] += r;
+  });
   STAMP(1)
 }
 
 // Cholesky of the mass matrix held in L (in place, no fill-in in leaf-first order; Ld =
 // 1 / diag(L)), nu = clamp(nu + dt M^-1 rhs), u = L^T nu.
 template <class R>
-PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld, float* nu, float* u) {
+PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld, float* nu, float* u, const SimP& P) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
-  constexpr float dt = (float)R::dt_sub;
+  const float dt = P.dt;
 #pragma unroll
   for (int j = 0; j < N; j++) {
     float sjj = L[D::lidx(j, j)];
@@ -696,18 +711,19 @@ PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld,
 }
 
 template <class R>
-PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u SUB_STAMP_ARGS) {
+PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u,
+                      const SimP& P SUB_STAMP_ARGS) {
   float rhs[R::NDOF];
-  dyn_mass<R>(s, tau, L, rhs SUB_STAMP_PASS);
-  dyn_solve<R>(s, L, rhs, Ld, nu, u);
+  dyn_mass<R>(s, tau, L, rhs, P SUB_STAMP_PASS);
+  dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
 }
 
 // nu = L^-T u, clamp, semi-implicit Euler (exponential-map base rotation).  nu: scratch.
 template <class R>
-PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float* u, float* nu) {
+PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float* u, float* nu, const SimP& P) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
-  constexpr float dt = (float)R::dt_sub;
+  const float dt = P.dt;
   // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
 #pragma unroll
   for (int i = N - 1; i >= 0; i--) {
@@ -734,11 +750,11 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
     // exponential-map quaternion update with the world angular velocity  [EXT]
     const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
     float ang = norm3(wv);
-    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
     float sh, dw;
     sincos_fast(0.5f * ang * dt, &sh, &dw);
     f3 ax;
-    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
+    if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
     else ax = (sh / ang) * wv;
     const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
     const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
@@ -752,14 +768,12 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
 
 template <class R, int LS>
 PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw, uint32_t sub,
-                    uint32_t& csig SUB_STAMP_ARGS) {
+                    uint32_t& csig, const SimP& P SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
-  constexpr float dt = (float)R::dt_sub;
-  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
   float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
   float Ld[N], nu[N], u[N];
-  dynamics<R>(s, tau, L, Ld, nu, u SUB_STAMP_PASS);
+  dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
   f3 O;
   STAMP(2)
   // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
@@ -784,8 +798,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
     // lower row J = +e_d (pos = q - lo), upper row J = -e_d (pos = hi - q)
     const float plo = s.q[d] - (float)R::dof_lower[d], phi = (float)R::dof_upper[d] - s.q[d];
-    const float tlo = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
-    const float thi = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
+    const float tlo = pos_target(plo, P.k_limit, P.k_sep);
+    const float thi = pos_target(phi, P.k_limit, P.k_sep);
 #pragma unroll
     for (int i = 0; i < N; i++)
       if (D::LIMPOS.v[li][i] >= 0) rw.lim(off + D::LIMPOS.v[li][i]) = y[i];
@@ -816,8 +830,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     slot_active[sl] = act;
     if (!act) return;
     csig += pbg_contact_hash(sub, (uint32_t)sl);
-    const f3 P = mk3(cc.x, cc.y, cc.z - rad);
-    const f3 rP = P - O;
+    const f3 cp = mk3(cc.x, cc.y, cc.z - rad);
+    const f3 rP = cp - O;
     const int lnk = R::slot_link[sl];
 #pragma unroll
     for (int dir = 0; dir < 3; dir++) {
@@ -841,7 +855,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
       rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
+             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f);
     }
     rw.mu(nc) = (float)R::slot_mu[sl];
     nc++;
@@ -923,7 +937,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
          
         }
         rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-               dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f);
+               dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f);
       }
       rw.mu(nc) = (float)R::pair_mu[pp];
       nc++;
@@ -932,7 +946,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 
   STAMP(4)
   // --- PGS: 5 sweeps in u-space (gym_locomotion_envs -> scene_bases.py:65 numSolverIterations=5)
-  for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+  for (int it = 0; it < P.iterations; it++) {
     // joint limits: lower then upper row of each limited dof, sharing y (compile-time)
     static_for<0, D::NLIM>([&](auto li_c) {
       constexpr int li = decltype(li_c)::value;
@@ -973,7 +987,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   }
 
   STAMP(5)
-  integrate<R>(s, L, Ld, u, nu);
+  integrate<R>(s, L, Ld, u, nu, P);
   STAMP(6)
   return nc;
 }
@@ -1033,6 +1047,7 @@ struct PackIn {
   double potential_old, initial_z;  // initial_z NaN: take from this calc_state
   double target_x = PBG_WALK_TARGET_X, target_y = PBG_WALK_TARGET_Y;  // robot.walk_target_x/y
   double avel[3] = {0.0, 0.0, 0.0};  // base angular velocity (MuJoCo-observation walkers)
+  double env_dt = R::dt_sub * R::substeps;  // Scene.dt (SimP::env_dt; the pack kernel: defaults)
 };
 struct PackOut {
   double reward, potential, initial_z, dist;  // dist: walk_target_dist
@@ -1142,7 +1157,7 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   out.dist = dist;
   out.pitch = pitch;
   out.at_limit = at_limit;
-  out.potential = -dist / (R::dt_sub * R::substeps);  // robot_locomotors.py:79; scene_bases.py:17
+  out.potential = -dist / in.env_dt;  // robot_locomotors.py:79; scene_bases.py:17
   uint32_t fb = 0;
 #pragma unroll
   for (int i = 0; i < R::NF; i++) fb |= (in.feet_prev[i] != 0.f ? 1u : 0u) << i;
@@ -1196,7 +1211,7 @@ PBG_DEV void flag_draw(const Buffers& B, int e, Flag& f) {
   const u4 r = philox4x32_10(ctr, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
   f.tx = (-PBG_STADIUM_HALFLEN + 2.0 * PBG_STADIUM_HALFLEN * (double)u01(r.x)) * PBG_FLAG_COMPACT;
   f.ty = (-PBG_STADIUM_HALFWIDTH + 2.0 * PBG_STADIUM_HALFWIDTH * (double)u01(r.y)) * PBG_FLAG_COMPACT;
-  f.timeout = PBG_FLAG_TIMEOUT;
+  f.timeout = B.sp.flag_timeout;
   f.count++;
 }
 // calc_state with HumanoidFlagrun's bookkeeping (:219-226): count the timeout down, pack
@@ -1238,7 +1253,7 @@ PBG_DEV void store_flag(const Buffers& B, int e, const Flag& f) {
 // out.potential carries x_after (the next step's x_before).
 template <class R>
 PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_after, double x_before, const float* act,
-                                float* obs, PackOut& out) {
+                                float* obs, PackOut& out, double env_dt = R::dt_sub * R::substeps) {
   constexpr int NO = R::NO;
   constexpr float c = (float)R::qvel_clip;
   int o = 0;
@@ -1253,7 +1268,7 @@ PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_af
 #pragma unroll
   for (int i = 0; i < 5; i++) out.terms[i] = 0.0;
   if (!act) { out.reward = 0.0; out.done = false; return; }
-  const double potential = (x_after - x_before) / (R::dt_sub * R::substeps);
+  const double potential = (x_after - x_before) / env_dt;
   float sq[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) sq[i] = act[i] * act[i];
@@ -1279,13 +1294,14 @@ PBG_DEV void mujoco_planar_pack(const double* jq, const double* jqd, double x_af
   }
 }
 template <class R>
-PBG_DEV void mujoco_planar_pack_state(const State<R>& s, double x_before, const float* act, float* obs, PackOut& po) {
+PBG_DEV void mujoco_planar_pack_state(const State<R>& s, double x_before, const float* act, float* obs, PackOut& po,
+                                      double env_dt) {
   double jq[R::NO], jqd[R::NO];
 #pragma unroll
   for (int i = 0; i < R::NO; i++) { jq[i] = s.q[R::obs_dof[i]]; jqd[i] = s.qd[R::obs_dof[i]]; }
   Kin<R> k;
   fk_pos<R>(s, k);
-  mujoco_planar_pack<R>(jq, jqd, (double)k.c[R::robot_body + 1].x, x_before, act, obs, po);
+  mujoco_planar_pack<R>(jq, jqd, (double)k.c[R::robot_body + 1].x, x_before, act, obs, po, env_dt);
 }
 
 // MuJoCo-observation Ant / Humanoid (mujoco robot_locomotors.py:210-319): WalkerBase.calc_state
@@ -1508,11 +1524,12 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
     return;
   } else if constexpr (R::kind == 2) {
     // reset: calc_state, then env.potential = calc_potential() stores x_after (env_bases.py:69-70)
-    mujoco_planar_pack_state<R>(s, 0.0, nullptr, obs, po);
+    mujoco_planar_pack_state<R>(s, 0.0, nullptr, obs, po, B.sp.env_dt);
     has_floor = true; pot = po.potential; z0 = 0.f;
     return;
   } else {
   PackIn<R> in;
+  in.env_dt = B.sp.env_dt;
   gather<R>(s, has_floor, in);
 #pragma unroll
   for (int f = 0; f < R::NF; f++) in.feet_prev[f] = 0.f;
@@ -1588,7 +1605,8 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   int nc = 0;
   uint32_t csig = 0;
   STAMP(7)
-  for (int sub = 0; sub < R::substeps; sub++) nc = substep<R, LS>(s, tau, slot_active, rw, (uint32_t)sub, csig SUB_STAMP_PASS);
+  for (int sub = 0; sub < B.sp.substeps; sub++)
+    nc = substep<R, LS>(s, tau, slot_active, rw, (uint32_t)sub, csig, B.sp SUB_STAMP_PASS);
   if (io.ncontact) io.ncontact[e] = nc;
   if (io.csig) io.csig[e] = csig;
   const int el = B.elapsed[e] + 1;
@@ -1599,10 +1617,11 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
   } else if constexpr (R::kind == 2) {
-    mujoco_planar_pack_state<R>(s, B.pot[e], act, obs, po);
+    mujoco_planar_pack_state<R>(s, B.pot[e], act, obs, po, B.sp.env_dt);
     pot_new = po.potential;
   } else {
     PackIn<R> in;
+    in.env_dt = B.sp.env_dt;
     gather<R>(s, flags & 1u, in);
     uint32_t fnew = 0;
 #pragma unroll

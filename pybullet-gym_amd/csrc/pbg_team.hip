@@ -225,6 +225,7 @@ struct Team {
   static constexpr BTab<NDB> DLO = dofs(R::dof_lower);
   static constexpr BTab<NDB> DHI = dofs(R::dof_upper);
   static constexpr BTab<NDB> DAMP = dofs(R::dof_damping);
+  static constexpr BTab<NDB> STIFF = dofs(R::dof_stiffness);
   static constexpr BTab<NDB> ARM = dofs(R::dof_armature);
   static constexpr BTab<NDB> GAIN = make_gain();
   static constexpr BTabI<NDB> ACTI = make_acti();
@@ -539,12 +540,11 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int ES>
 PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t& slot_bits, uint32_t& base_bits,
-                         const TRows<R, ES>& rw SUB_STAMP_ARGS) {
+                         const TRows<R, ES>& rw, const SimP& P SUB_STAMP_ARGS) {
   using T = Team<R>;
   constexpr int NDB = T::NDB, NLB = T::NLB;
-  constexpr float dt = (float)R::dt_sub;
-  constexpr float inv_dt = (float)(1.0 / R::dt_sub);
-  constexpr float g = (float)PBG_GRAVITY;
+  const float dt = P.dt;
+  const float g = P.gravity;
   const int kb = L.k;
 
   // --- phase A: branch kinematics, velocities, bias accelerations; composites of the
@@ -725,6 +725,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     constexpr int a = T::lg(j);
     Lbr[a][a] += pk<T::ARM, j>(L);
     rb[a] += tau[j] - pk<T::DAMP, j>(L) * s.qd[j];
+    if constexpr (has_springs<R>()) rb[a] -= pk<T::STIFF, j>(L) * s.q[j];  // mjcf.py B7
   });
 
   STAMP(1)
@@ -904,8 +905,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; }
       const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
       const float plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
-      Ltl[li] = pos_target(plo, (float)PBG_LIMIT_ERP, inv_dt);
-      Lth[li] = pos_target(phi, (float)PBG_LIMIT_ERP, inv_dt);
+      Ltl[li] = pos_target(plo, P.k_limit, P.k_sep);
+      Lth[li] = pos_target(phi, P.k_limit, P.k_sep);
       Lm[li] = meff;
 #pragma unroll
       for (int a = 0; a < NDB; a++) Lyb[li][a] = y[a];
@@ -964,7 +965,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
       rw.put(3 * n0 + dir, -1, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f, (float)R::slot_mu[sl]);
+             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (float)R::slot_mu[sl]);
     }
     n0++;
   });
@@ -1023,7 +1024,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
       rw.put(3 * ci + dir, kb, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, (float)R::contact_erp, inv_dt)) : 0.f, pk<T::SMU, sl>(L));
+             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, pk<T::SMU, sl>(L));
     }
     ci++;
   });
@@ -1040,7 +1041,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   // u's base part sliced over the quad: lane kb owns components kb and kb + 4 (kb < 2)
   float uBs[2] = {kb == 0 ? uB[0] : (kb == 1 ? uB[1] : (kb == 2 ? uB[2] : uB[3])),
                   kb == 0 ? uB[4] : (kb == 1 ? uB[5] : 0.f)};
-  for (int it = 0; it < PBG_SOLVER_ITERATIONS; it++) {
+  for (int it = 0; it < P.iterations; it++) {
     static_for<0, 4>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       static_for<0, NLIMB>([&](auto l_c) {
@@ -1114,11 +1115,11 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   {
     const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
     float ang = norm3(wv);
-    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = (float)PBG_ANGULAR_MOTION_THRESHOLD / dt;
+    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
     float sh, dw;
     sincos_fast(0.5f * ang * dt, &sh, &dw);
     f3 ax;
-    if (ang < 0.001f) ax = (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) * wv;
+    if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
     else ax = (sh / ang) * wv;
     const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
     const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
@@ -1208,6 +1209,7 @@ PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, co
     s.qd[j] = 0.f;
   });
   PackIn<R> in;
+  in.env_dt = B.sp.env_dt;
   team_gather<R, ES>(s, L, rw, has_floor, in);
 #pragma unroll
   for (int f = 0; f < R::NF; f++) in.feet_prev[f] = 0.f;
@@ -1248,6 +1250,11 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     s.q[j] = B.st[(size_t)(SB + kb * NDB + j) * B.n + e];
     s.qd[j] = B.st[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e];
   }
+  // the pack's bookkeeping loads, issued here so their latency overlaps the physics
+  const int el = B.elapsed[e] + 1;
+  uint32_t flags = B.flags[e];
+  const double pot_old = B.pot[e];
+  const float z0_old = B.z0[e];
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
@@ -1272,8 +1279,8 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   int nc = 0;
   STAMP(7)
   uint32_t csig = 0;  // this lane's share of the contact-set signature
-  for (int sub = 0; sub < R::substeps; sub++) {
-    nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw SUB_STAMP_PASS);
+  for (int sub = 0; sub < B.sp.substeps; sub++) {
+    nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw, B.sp SUB_STAMP_PASS);
     if (io.csig) {  // base slots counted by lane 0, branch k's slots (global NS0 + k NSB + sl) by lane k
       if (kb == 0)
         for (int sl = 0; sl < T::NS0; sl++)
@@ -1298,18 +1305,17 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     if (f >= 0 && ((slot_bits >> sl) & 1u)) fb |= 1u << f;
   });
   const uint32_t fnew = (uint32_t)quad_sum_i((int)fb);  // disjoint bits: sum == or
-  const int el = B.elapsed[e] + 1;
-  uint32_t flags = B.flags[e];
   float obs[R::OBS];
   PackOut po;
   {
     PackIn<R> in;
+    in.env_dt = B.sp.env_dt;
     team_gather<R, ES>(s, L, rw, flags & 1u, in);
 #pragma unroll
     for (int f = 0; f < R::NF; f++) in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
     in.feet_new = fnew;
-    in.potential_old = B.pot[e];
-    in.initial_z = B.z0[e];
+    in.potential_old = pot_old;
+    in.initial_z = z0_old;
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
     else walker_pack<R, false, 4>(in, act, obs, po, kb);
     flags = (flags & 0xFFu) | (po.feet_out << 8);

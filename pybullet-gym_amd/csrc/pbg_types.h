@@ -3,6 +3,42 @@
 #include <stdint.h>
 
 namespace pbg {
+// Scene / World parameters of a handle (include/pbg.h pbg_sim_params_t; scene_bases.py:8-18,
+// 58-73), resolved once on the host at create into the constants the kernels use.  Every
+// derived float is formed in float arithmetic exactly as the kernels formed it when these
+// were compile-time constants, so default parameters reproduce the old bits.
+struct SimP {
+  float dt;          // Scene.timestep: one stepSimulation sub-step
+  float gravity;     // World.gravity: setGravity(0, 0, -gravity)
+  float k_sep;       // position-target slope of a separated row: -1 / dt (pos_target)
+  float k_contact;   // ... of a penetrating contact normal: -contact_erp / dt
+  float k_limit;     // ... of a violated joint limit: -limit_erp / dt
+  float ang_max;     // [EXT] angular motion threshold / dt (exponential-map integration)
+  float dt3c;        // dt^3 / 48 (small-angle quaternion series)
+  int substeps;      // Scene.frame_skip = numSubSteps
+  int iterations;    // World.numSolverIterations
+  int flag_timeout;  // HumanoidFlagrun: 600 / frame_skip steps, rounded up (robot_locomotors.py:218-223)
+  double env_dt;     // Scene.dt = timestep * frame_skip (the potential's divisor, scene_bases.py:17)
+};
+
+inline SimP resolve_sim_params(double timestep, int frame_skip, int iterations, double gravity, double contact_erp,
+                               double limit_erp, double angular_motion_threshold) {
+  SimP p;
+  p.dt = (float)timestep;
+  const float inv_dt = (float)(1.0 / timestep);
+  p.gravity = (float)gravity;
+  p.k_sep = -inv_dt;
+  p.k_contact = -(float)contact_erp * inv_dt;
+  p.k_limit = -(float)limit_erp * inv_dt;
+  p.ang_max = (float)angular_motion_threshold / p.dt;
+  p.dt3c = p.dt * p.dt * p.dt * 0.020833333333f;
+  p.substeps = frame_skip;
+  p.iterations = iterations;
+  p.flag_timeout = (600 + frame_skip - 1) / frame_skip;
+  p.env_dt = timestep * frame_skip;
+  return p;
+}
+
 struct Buffers {
   int n;                   // envs on this device
   float* st;               // [SD][n] physical state, SoA
@@ -15,6 +51,7 @@ struct Buffers {
   int32_t* ftm;            // [2][n] flag_timeout, flag draws so far (HumanoidFlagrun RNG counter)
   uint64_t seed;
   int env_offset;          // global id of env 0 (multi-GPU sharding)
+  SimP sp;                 // the handle's scene parameters (kernel arguments)
 };
 
 struct StepIO {

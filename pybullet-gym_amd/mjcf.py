@@ -4,7 +4,7 @@ The reference hands an MJCF path to ``pybullet.loadMJCF`` (``robot_bases.py:108,
 and then walks the resulting multibody with ``getJointInfo`` in
 ``XmlBasedRobot.addToScene`` (``robot_bases.py:32-91``).  pybullet's MJCF importer is
 third-party C++ that is not in /root/reference, so every rule it applies is restated
-here as an explicit, documented choice (SURVEY.md Appendix B, items B2-B6; all
+here as an explicit, documented choice (SURVEY.md Appendix B, items B2-B7; all
 unpinned by anything in this container):
 
 * B2 topology: a root body without joints becomes a floating base (Ant, Humanoid); a
@@ -37,6 +37,12 @@ unpinned by anything in this container):
   only ``limited`` from joint defaults).  Evidence: with inherited damping 1 the
   pretrained swing-up policy never swings the pole up (mean return -666); without it,
   878 -- and InvertedDoublePendulum 4368 -> 6491 (tests/test_policies.py).
+* B7 stiffness: the joint element's own ``stiffness`` attribute as a spring to q = 0,
+  tau -= k*q from each sub-step's position (explicit, beside B6's damping); not inherited
+  from ``<default>``.  Evidence (round 3): the pretrained HalfCheetah
+  policy runs every 64-episode rollout to the 1,000-step limit with it (mean return 729 ->
+  1,301; without it episodes end at 702 steps on average), Humanoid 30 -> 37; no other
+  robot's MJCF sets a non-zero stiffness.
 * The base frame is the base's centre of mass (pybullet reports base and link
   positions of the inertial frame); link frames are MJCF body frames and keep a COM
   offset.  Inertial frames are not rotated to principal axes.
@@ -140,6 +146,7 @@ class Link:
     upper: float = -1.0       # lower > upper -> no limits (pybullet convention)
     limited: bool = False
     damping: float = 0.0
+    stiffness: float = 0.0    # B7: spring to q = 0 (N m / rad or N / m)
     armature: float = 0.0
     mass: float = 0.0
     com: np.ndarray = field(default_factory=lambda: np.zeros(3))
@@ -418,6 +425,7 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
         return dict(jtype=jtype, axis=axis, anchor=anchor, lower=lo if limited else 0.0,
                     upper=hi if limited else -1.0, limited=limited,
                     damping=float(j.get("damping", "0")),  # B6: the joint's own attribute only
+                    stiffness=float(j.get("stiffness", "0")),  # B7: likewise
                     armature=0.0,  # B3: btMultiBody has no armature
                     joint_name=j.get("name"))
 

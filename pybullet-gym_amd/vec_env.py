@@ -44,13 +44,19 @@ class VecEnv:
     so a learner that keeps a batch across steps must ``clone()`` it (the buffers are never
     reallocated, which is what lets a step be captured into a HIP graph).
 
+    ``sim_params``: a dict overriding fields of the reference's scene (``gravity``, ``timestep``,
+    ``frame_skip``, ``solver_iterations``, ``contact_erp``, ``joint_limit_erp``; include/pbg.h
+    pbg_sim_params_t, scene_bases.py:8-18,58-73), or a ``_native.SimParams``; None = the
+    reference's values (``self.sim_params`` holds the ones in force).
+
     ``kernel`` / ``lds_rows`` / ``gang_dist`` are test and diagnostic launch options
     (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
     a cap on LDS-resident contact rows, forced replicated (0) / distributed (1) gang dynamics.
     """
 
     def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
-                 autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1):
+                 autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1,
+                 sim_params=None):
         if not torch.cuda.is_available():
             raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.env_id = env_id
@@ -61,9 +67,12 @@ class VecEnv:
         h = ctypes.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         opts = _native.DebugOpts(int(kernel), int(lds_rows), int(gang_dist))
-        _native.check(L.pbg_create_debug(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
-                                         ctypes.byref(opts), ctypes.byref(h)), "pbg_create")
+        sp = sim_params if isinstance(sim_params, _native.SimParams) else _native.sim_params(env_id, sim_params)
+        _native.check(L.pbg_create_ex(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
+                                      ctypes.byref(sp), ctypes.byref(opts), ctypes.byref(h)), "pbg_create")
         self._h = h
+        self.sim_params = _native.SimParams()
+        _native.check(L.pbg_get_sim_params(h, ctypes.byref(self.sim_params)), "pbg_get_sim_params")
         info = _native.Info()
         _native.check(L.pbg_info(h, ctypes.byref(info)), "pbg_info")
         self.info = info
@@ -82,6 +91,11 @@ class VecEnv:
         self.reward_terms = None
         self.contact_sig = None
         self._io = _native.StepIO()
+
+    @staticmethod
+    def default_sim_params(env_id: str) -> dict:
+        """The reference's scene for env_id as a dict (pbg_default_sim_params; no GPU needed)."""
+        return _native.default_sim_params(env_id).as_dict()
 
     # ---------------------------------------------------------------- lifecycle
     def close(self):
@@ -166,17 +180,23 @@ class VecEnv:
 
     def state_dict(self) -> dict:
         """Checkpoint of every env (pybullet saveState generalised): the state records plus the
-        env id and the record-layout version (include/pbg.h PBG_RECORD_VERSION)."""
+        env id, the record-layout version (include/pbg.h PBG_RECORD_VERSION) and the scene
+        parameters the states were simulated under."""
         phys, aux = self.get_state()
-        return {"env_id": self.env_id, "record_version": int(self.info.record_version), "phys": phys, "aux": aux}
+        return {"env_id": self.env_id, "record_version": int(self.info.record_version), "phys": phys, "aux": aux,
+                "sim_params": self.sim_params.as_dict()}
 
     def load_state_dict(self, sd: dict):
-        """Restore a state_dict(); refuses a checkpoint of another env id or record layout."""
+        """Restore a state_dict(); refuses a checkpoint of another env id, record layout or scene
+        (a checkpoint without "sim_params" is taken to be of the reference's scene)."""
         if sd.get("env_id") != self.env_id:
             raise _native.PbgError(f"checkpoint of {sd.get('env_id')!r} loaded into {self.env_id!r}")
         if sd.get("record_version") != self.info.record_version:
             raise _native.PbgError(f"checkpoint record version {sd.get('record_version')} != library's "
                                    f"{self.info.record_version} (the aux record layout changed)")
+        sp = sd.get("sim_params", self.default_sim_params(self.env_id))
+        if sp != self.sim_params.as_dict():
+            raise _native.PbgError(f"checkpoint scene {sp} != this handle's {self.sim_params.as_dict()}")
         self.set_state(sd["phys"], sd["aux"])
 
     def set_state(self, phys: torch.Tensor, aux: torch.Tensor = None):

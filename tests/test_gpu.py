@@ -181,7 +181,7 @@ COND_FRAC = 0.6
 LOOSE_FRAC = 0.05
 EXPLAIN_FACTOR = 3.0
 F32_MCA_RUNS = 32       # first pass per outlier ...
-F32_MCA_RUNS_MAX = 2048  # ... and the escalation for an outlier the first pass leaves unexplained (a
+F32_MCA_RUNS_LADDER = (256, 2048)  # ... and the escalation for an outlier a pass leaves unexplained (a
                         # step on a PGS active-set boundary that ~1 % of float32 roundings cross)
 # The MuJoCo-observation variants (not the north_star's ids) carry raw
 # joint and base velocities (the PyBullet observation scales joint speeds by 0.1) and the raw
@@ -234,15 +234,18 @@ def _f32_envelope(env_id, state, aux, act, oo, csig64, disc64, kind, seed=0, run
 
 def _explainer(env_id, s_in, x_in, act, oo, csig64, disc64, kind, seed):
     """explain(idx) for SplitStats.add: the float32 envelope of the env-steps idx, escalated
-    to F32_MCA_RUNS_MAX Monte Carlo runs for those the first F32_MCA_RUNS leave unexplained."""
-    def explain(idx, rel):
+    through F32_MCA_RUNS_LADDER Monte Carlo runs for those the previous pass leaves unexplained
+    (neither within EXPLAIN_FACTOR x the envelope nor, class C (mask c), with a discrete flip)."""
+    def explain(idx, rel, c):
         env, flip = _f32_envelope(env_id, s_in[idx], x_in[idx], act[idx], oo[idx], csig64[idx], disc64[idx], kind,
                                   seed)
-        again = np.flatnonzero(rel > EXPLAIN_FACTOR * env)
-        if len(again):
+        for runs in F32_MCA_RUNS_LADDER:
+            again = np.flatnonzero((rel > EXPLAIN_FACTOR * env) & ~(c & flip))
+            if not len(again):
+                break
             j = idx[again]
             e2, f2 = _f32_envelope(env_id, s_in[j], x_in[j], act[j], oo[j], csig64[j], disc64[j], kind, seed,
-                                   runs=F32_MCA_RUNS_MAX)
+                                   runs=runs)
             env[again] = np.maximum(env[again], e2)
             flip[again] |= f2
         return env, flip
@@ -278,7 +281,7 @@ class SplitStats:
     def add(self, og, oo, rg, ro, dg, do, cg, co, same, cond=None, probe=None, explain=None, step=None, inputs=None):
         """same: per env-step True where the discrete state agrees (contact set, discrete
         reward terms); cond: True where the conditioning probe passed (None: all); probe: the
-        oracle's own spread (class B's yardstick); explain(idx, rel) -> (float32 envelope, discrete
+        oracle's own spread (class B's yardstick); explain(idx, rel, c) -> (float32 envelope, discrete
         flip) of the env-steps idx (outlier explanation; None: outliers are not re-stepped)."""
         a = same if cond is None else same & cond
         b = same & ~a
@@ -305,7 +308,7 @@ class SplitStats:
         if explain is None or not outl.any():
             return
         idx = np.flatnonzero(outl)
-        env32, flip = explain(idx, rel[idx])
+        env32, flip = explain(idx, rel[idx], c[idx])
         ok = rel[idx] <= EXPLAIN_FACTOR * env32
         ok |= c[idx] & flip
         ratio = rel[idx] / np.maximum(env32, 1e-30)
@@ -372,13 +375,26 @@ def _discrete_terms(terms, kind):
     return terms[:, :0]
 
 
-def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None):
+def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None, sim=None):
     """GPU steps all n envs (auto-reset on, Philox actions); before every step the sampled
     envs' float64 state records are copied into the oracle, which steps them from the same
     state, and into two more oracle instances at PROBE_REL perturbations of it (the
     conditioning probe).  Compares obs (the terminal obs where the GPU reset an env), reward,
-    termination, contact count, contact-set signature and the discrete reward terms."""
-    env = VecEnv(env_id, n, seed=seed, autoreset=True)
+    termination, contact count, contact-set signature and the discrete reward terms.
+    sim: scene-parameter overrides (pbg_sim_params_t) given to the GPU handle and the oracle."""
+    if sim is not None:
+        sp = VecEnv.default_sim_params(env_id)
+        sp.update(sim)
+        oracle.set_sim_params(sp)
+        try:
+            return _teacher_forced_run(env_id, n, steps, sample, seed, name, sim)
+        finally:
+            oracle.set_sim_params(None)
+    return _teacher_forced_run(env_id, n, steps, sample, seed, name, None)
+
+
+def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim):
+    env = VecEnv(env_id, n, seed=seed, autoreset=True, sim_params=sim)
     env.reset()
     idx = np.arange(n) if sample is None else np.linspace(0, n - 1, sample).astype(np.int64)
     tidx = torch.from_numpy(idx).cuda()
@@ -822,3 +838,72 @@ def test_state_dict_round_trip_and_record_version():
         b.load_state_dict(dict(sd, record_version=1))
     with pytest.raises(PbgError):
         b.load_state_dict(dict(sd, env_id="AntPyBulletEnv-v0"))
+
+
+# ------------------------------------------------------------------ scene parameters
+# pbg_sim_params_t at create (scene_bases.py:8-18,58-73): each variant changes the scene of the
+# GPU handle and the oracle alike; teacher-forced parity holds to the same split bounds.
+# HopperMuJoCo at timestep 0.002 x 6 divides its potential by that Scene.dt.
+SIM_VARIANTS = [("AntPyBulletEnv-v0", {"gravity": 4.9, "solver_iterations": 8}),
+                ("HumanoidPyBulletEnv-v0", {"timestep": 0.0165 / 5, "frame_skip": 5, "contact_erp": 0.3}),
+                ("HalfCheetahPyBulletEnv-v0", {"gravity": 12.0, "joint_limit_erp": 0.4, "solver_iterations": 3}),
+                ("HumanoidFlagrunPyBulletEnv-v0", {"gravity": 9.0, "solver_iterations": 6}),
+                ("HopperMuJoCoEnv-v0", {"timestep": 0.002, "frame_skip": 6}),
+                ("InvertedPendulumPyBulletEnv-v0", {"gravity": 3.7, "timestep": 0.01})]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("env_id,over", SIM_VARIANTS)
+def test_sim_params_teacher_forced_parity(env_id, over):
+    _teacher_forced(env_id, 128, 30, sim=over, name=f"sim_params[{env_id},{over}]")
+
+
+def test_sim_params_defaults_bitwise_and_changes_trajectory():
+    """The reference's scene passed explicitly is bit-identical to pbg_create; a changed
+    gravity / sub-step count / iteration count changes the trajectory; the handle reports
+    its scene (info.substeps = frame_skip); out-of-range parameters are refused."""
+    env_id = "AntPyBulletEnv-v0"
+    base, cb = _rollout(env_id, n=128, steps=30)
+    same, cs = _rollout(env_id, n=128, steps=30, sim_params=VecEnv.default_sim_params(env_id))
+    np.testing.assert_array_equal(cb, cs)
+    np.testing.assert_array_equal(base.view(np.uint32), same.view(np.uint32))
+    for over in ({"gravity": 9.0}, {"frame_skip": 5}, {"solver_iterations": 4}):
+        other, _ = _rollout(env_id, n=128, steps=30, sim_params=over)
+        assert np.isfinite(other).all()
+        assert np.abs(other[-1] - base[-1]).max() > 1e-2, over
+    e = VecEnv(env_id, 4, sim_params={"frame_skip": 6, "gravity": 1.6})
+    assert e.info.substeps == 6 and e.sim_params.frame_skip == 6 and e.sim_params.gravity == 1.6
+    sd = e.state_dict()
+    assert sd["sim_params"]["gravity"] == 1.6
+    from pybulletgym_amd._native import PbgError
+    with pytest.raises(PbgError):
+        VecEnv(env_id, 4).load_state_dict(sd)  # a checkpoint of another scene
+    for bad in ({"frame_skip": 0}, {"timestep": -0.01}, {"solver_iterations": 0}, {"contact_erp": 1.5},
+                {"gravity": float("nan")}, {"no_such_field": 1}):
+        with pytest.raises(PbgError):
+            VecEnv(env_id, 4, sim_params=bad)
+
+
+def test_sim_params_flagrun_timeout_follows_frame_skip():
+    """HumanoidFlagrun's flag_timeout = 600 / frame_skip (robot_locomotors.py:218), counted down
+    once by the reset's calc_state: 149 at frame_skip 4, ceil(600 / 7) - 1 = 85 at 7 -- the GPU
+    aux record equal to the oracle's under the same scene."""
+    env_id, n = "HumanoidFlagrunPyBulletEnv-v0", 16
+    for fs, want in ((4, 149), (7, 85)):
+        over = {"frame_skip": fs, "timestep": 0.0165 / fs}
+        env = VecEnv(env_id, n, seed=5, autoreset=False, sim_params=over)
+        q0 = np.random.default_rng(1).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
+        env.reset(init_q=torch.from_numpy(q0))
+        _, aux = env.get_state()
+        NF = env.info.n_feet
+        aux = aux.cpu().numpy()
+        assert (aux[:, 4 + NF + 2] == want).all(), (fs, aux[:, 4 + NF + 2])
+        sp = VecEnv.default_sim_params(env_id)
+        sp.update(over)
+        oracle.set_sim_params(sp)
+        try:
+            orc = oracle.OracleEnvs(env_id, n, nthreads=4, seed=5)
+            orc.reset(q0.astype(np.float64))
+            np.testing.assert_array_equal(aux[:, 4 + NF:], orc.aux[:, 4 + NF:])
+        finally:
+            oracle.set_sim_params(None)

@@ -53,3 +53,33 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_native.PbgError):
         _native.lib()
+
+
+def test_sim_params_struct_matches_header():
+    """_native.SimParams mirrors pbg_sim_params_t field for field (types and order)."""
+    src = open(HEADER).read()
+    body = src[src.rindex("typedef struct {", 0, src.index("} pbg_sim_params_t;")):src.index("} pbg_sim_params_t;")]
+    fields = re.findall(r"\b(double|int)\s+([a-z_]+);", body)
+    ct = {"double": ctypes.c_double, "int": ctypes.c_int}
+    assert [(n, ct[t]) for t, n in fields] == list(_native.SimParams._fields_)
+
+
+@pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="libpbg_amd.so not built")
+def test_default_sim_params_are_the_reference_scenes():
+    """pbg_default_sim_params (host only) returns the scene each env builds: StadiumScene(gravity
+    9.8, timestep 0.0165/4, frame_skip 4) for the walkers (roboschool and MuJoCo
+    gym_locomotion_envs.py:18-19), SingleRobotEmptyScene(9.8, 0.0165, 1) for the pendulums
+    (gym_pendulum_envs.py:14,48), numSolverIterations 5 (scene_bases.py:65)."""
+    for env_id in _native.ROBOT_IDS:
+        p = _native.default_sim_params(env_id)
+        pend = "Pendulum" in env_id
+        assert p.gravity == 9.8 and p.solver_iterations == 5, env_id
+        assert p.frame_skip == (1 if pend else 4), env_id
+        assert p.timestep == (0.0165 if pend else 0.0165 / 4), env_id
+        assert 0.0 <= p.contact_erp <= 1.0 and 0.0 <= p.joint_limit_erp <= 1.0
+    over = _native.sim_params("AntPyBulletEnv-v0", {"gravity": 1.6, "frame_skip": 2})
+    assert (over.gravity, over.frame_skip, over.solver_iterations) == (1.6, 2, 5)
+    with pytest.raises(_native.PbgError):
+        _native.sim_params("AntPyBulletEnv-v0", {"gravty": 1.0})
+    with pytest.raises(_native.PbgError):
+        _native.default_sim_params("NoSuchEnv-v0")

@@ -212,3 +212,56 @@ def test_mca_float32_runs_bracket_ieee_float32(env_id):
     emca = rel(run(33, 7, R), np.repeat(o64, R, 0)).reshape(n, R).max(axis=1)
     assert np.median(emca) <= 10 * max(np.median(e32), 1e-7) and np.median(e32) <= 10 * max(np.median(emca), 1e-7)
     assert np.median(emca) < 1e-3
+
+
+def test_scene_parameters_enter_the_physics():
+    """pbg_oracle_set_sim_params (the oracle side of pbg_create_ex's pbg_sim_params_t): the
+    bias forces are the potential gradient under the new gravity; a changed sub-step count,
+    iteration count or ERP changes the rollout; NULL restores the reference's scene bit for bit."""
+    key = "hopper"
+    s, rng, info, t = random_state(key, 1)
+    L = _lib()
+    sp = {"gravity": 3.7, "timestep": 0.0165 / 4, "frame_skip": 4, "solver_iterations": 5,
+          "contact_erp": 0.2, "joint_limit_erp": 0.2}
+    L.pbg_oracle_set_flags(4)
+    oracle.set_sim_params(sp)
+    try:
+        _, C = oracle.dynamics(key, s)
+        d = rng.standard_normal(info.NDOF)
+        masses = [t["base_mass"]] + t["link_mass"]
+
+        def V(st):
+            _, c = frames(key, st)
+            return sum(masses[b] * 3.7 * c[b][2] for b in range(info.NL + 1))
+
+        eps = 1e-6
+        dV = (V(advance(info, s, d, eps)) - V(advance(info, s, d, -eps))) / (2 * eps)
+        assert C @ d == pytest.approx(dV, rel=1e-6, abs=1e-9)
+    finally:
+        L.pbg_oracle_set_flags(0)
+        oracle.set_sim_params(None)
+
+    def rollout(params):
+        oracle.set_sim_params(params)
+        try:
+            e = oracle.OracleEnvs("ant", 4, nthreads=4)
+            r = np.random.default_rng(5)
+            e.reset(r.uniform(-0.1, 0.1, (4, 8)))
+            for _ in range(20):
+                obs, rew, _, _ = e.step(r.uniform(-1, 1, (4, 8)).astype(np.float32))
+            return obs.copy(), rew.copy(), e.info.substeps
+        finally:
+            oracle.set_sim_params(None)
+
+    base, rb, nsub = rollout(None)
+    assert nsub == 4
+    ref = dict(sp, gravity=9.8)
+    same, rs, _ = rollout(ref)
+    np.testing.assert_array_equal(base, same)
+    np.testing.assert_array_equal(rb, rs)
+    for over in ({"frame_skip": 5}, {"solver_iterations": 3}, {"contact_erp": 0.5}, {"gravity": 9.0}):
+        other, _, ns = rollout(dict(ref, **over))
+        assert np.isfinite(other).all() and np.abs(other - base).max() > 1e-3, over
+        assert ns == ref["frame_skip"] if "frame_skip" not in over else ns == over["frame_skip"]
+    again, ra, _ = rollout(None)
+    np.testing.assert_array_equal(base, again)

@@ -1,7 +1,10 @@
 """A/B timing of two builds of libpbg_amd.so on the same GPU (dev tool): each variant runs in
 its own subprocess (the library is loaded once per process), alternating A, B, A, B; each run
 is bench-like (Philox actions, pre-roll, one HIP graph of the timed steps).
-python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST] ..."""
+python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST] ...
+LIB_A / LIB_B: a libpbg_amd.so (run with this tree's Python package) or a directory holding a
+whole tree snapshot (its pybulletgym_amd.py, pybullet-gym_amd/ and built library), for a base
+whose C-ABI predates the current package's."""
 import os
 import subprocess
 import sys
@@ -29,7 +32,9 @@ print("%.5f" % (e0.elapsed_time(e1) / K))
 
 def run(lib, env, n, gd=-1):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = CHILD.format(repo=repo, lib=os.path.abspath(lib), env=env, n=n, gd=gd)
+    if os.path.isdir(lib):
+        repo, lib = lib, os.path.join(lib, "pybullet-gym_amd", "libpbg_amd.so")
+    code = CHILD.format(repo=os.path.abspath(repo), lib=os.path.abspath(lib), env=env, n=n, gd=gd)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if out.returncode:
         raise RuntimeError(out.stderr[-2000:])

@@ -2,7 +2,8 @@
 op-counting instantiation of the oracle's physics (oracle/counted.h, pbg_oracle_count_flops):
 for each robot, 256 envs are rolled out 200 steps with Philox U(-1, 1) actions and auto-reset
 (the bench workload's state distribution), then the next step of every env is counted.
-Writes profiles/flops_per_env_step.json (read by bench.py for the flop roofline).
+Writes profiles/flops_per_env_step.json and its copy pybullet-gym_amd/perf/ (read by bench.py
+for the flop roofline).
 Test infrastructure (imports the oracle).  python tools/count_flops.py"""
 import ctypes
 import json
@@ -58,9 +59,10 @@ if __name__ == "__main__":
                           "on oracle/counted.h: +,-,*,/,sqrt,sin,cos one flop each; flops_per_env_step skips adds "
                           "and muls with an exactly-zero operand (the dense restatement's structural zeros); the "
                           "float64 observation/reward pack is not counted")
-    path = os.path.join(REPO, "profiles", "flops_per_env_step.json")
-    with open(path, "w") as f:
-        json.dump(res, f, indent=1)
+    for path in (os.path.join(REPO, "profiles", "flops_per_env_step.json"),
+                 os.path.join(REPO, "pybullet-gym_amd", "perf", "flops_per_env_step.json")):
+        with open(path, "w") as f:
+            json.dump(res, f, indent=1)
     for k, v in res.items():
         if not k.startswith("_"):
             print(f"{k:12s} {v['flops_per_env_step']:12.0f} flops/env-step (dense {v['dense_flops_per_env_step']:.0f})")

@@ -22,7 +22,7 @@ KEYS = ["contact_erp", "deep_erp", "deep_thr", "deep_mode", "limit_mode", "damp_
         "springs", "roll_mu", "spin_mu", "lim_deep_mode", "limit_cfm", "contact_cfm", "contact_thr", "margin",
         "self_collision"]
 DEFAULT = [-1.0, -1.0, -0.04, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.2, 5.0, 0.0, 0.0, 1.0, 1.0,
-           0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.02, 0.0, 1.0]
+           1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.02, 0.0, 1.0]
 VARIANTS = {
     "current": {},
     "erp0.9": {"contact_erp": 0.9},
@@ -39,7 +39,9 @@ VARIANTS = {
     "relative_sep_rows (round 1)": {"sep_abs": 0.0, "lim_sep_abs": 0.0},
     "relative_sep_limit_rows": {"lim_sep_abs": 0.0},
     # round 3: importer / solver hypotheses not scored before
-    "springs": {"springs": 1.0},  # MJCF joint stiffness as a spring to q = 0
+    # MJCF joint stiffness as a spring to q = 0 (adopted in round 3, mjcf.py B7; "no_springs" is the
+    # round-2 rule set)
+    "no_springs": {"springs": 0.0},
     "roll0.08": {"roll_mu": 0.08},  # MJCF friction[2] 0.1 x floor 0.8 (btManifoldResult rolling combine)
     "spin0.08": {"spin_mu": 0.08},  # MJCF friction[1] 0.1 x floor 0.8
     "roll+spin0.08": {"roll_mu": 0.08, "spin_mu": 0.08},
@@ -57,43 +59,6 @@ VARIANTS = {
 }
 ENVS = ["HopperPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "AntPyBulletEnv-v0",
         "HumanoidPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0"]
-
-
-# MJCF per env (the joint-stiffness table of the "springs" variant)
-XML = {"HopperPyBulletEnv-v0": "hopper.xml", "Walker2DPyBulletEnv-v0": "walker2d.xml",
-       "HalfCheetahPyBulletEnv-v0": "half_cheetah.xml", "AntPyBulletEnv-v0": "ant.xml",
-       "HumanoidPyBulletEnv-v0": "humanoid_symmetric.xml", "HumanoidFlagrunPyBulletEnv-v0": "humanoid_symmetric.xml",
-       "InvertedDoublePendulumPyBulletEnv-v0": "inverted_double_pendulum.xml"}
-ASSETS = "/root/reference/pybulletgym/envs/assets/mjcf"
-
-
-def mjcf_stiffness(path):
-    """<joint stiffness> in dof order (mjcf.py numbers dofs body by body, depth first, each body's
-    joints in document order), <default><joint stiffness> when a joint has none."""
-    import xml.etree.ElementTree as ET
-    root = ET.parse(path).getroot()
-    d = root.find("default")
-    dj = d.find("joint") if d is not None else None
-    dflt = float(dj.get("stiffness", "0")) if dj is not None else 0.0
-    out = []
-
-    def walk(b):
-        for j in b.findall("joint"):
-            out.append(float(j.get("stiffness", dflt)))
-        for c in b.findall("body"):
-            walk(c)
-    for b in root.find("worldbody").findall("body"):
-        walk(b)
-    return out
-
-
-def load_springs():
-    L = oracle.lib()
-    L.pbg_oracle_set_springs.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
-    for env_id, xml in XML.items():
-        k = np.array(mjcf_stiffness(os.path.join(ASSETS, xml)), dtype=np.float64)
-        assert len(k) == oracle.Info(oracle.robot_id(env_id)).NJ, (env_id, len(k))
-        L.pbg_oracle_set_springs(oracle.robot_id(env_id), k.ctypes.data, len(k))
 
 
 def set_physics(over):
@@ -129,7 +94,6 @@ def parse(spec):
 
 
 if __name__ == "__main__":
-    load_springs()
     specs = sys.argv[1:] or list(VARIANTS)
     short = ["Hopper", "Walker", "Cheetah", "Ant", "Humanoid", "Flagrun", "DblPend"]
     print(f"{'variant':34s}" + "".join(f"{s:>16s}" for s in short))

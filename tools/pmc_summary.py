@@ -3,8 +3,9 @@
 usage: python tools/pmc_summary.py gpurun_out/TAG ROUND ROBOT ENVS
 (PMC passes under gpurun_out/TAG/ROBOT/, the kernel trace under gpurun_out/TAG/trace/)
 writes profiles/ROUND_{kernel_stats,pmc_*}_<robot><envs/1024>k.csv copies and
-profiles/pmc_step_<robot>.json (per-launch medians of the step kernel), which bench.py
-reads for roofline.traffic and valu_roofline.
+profiles/ROUND_pmc_step_<robot>.json (per-launch medians of the step kernel) and its copy
+pybullet-gym_amd/perf/pmc_step_<robot>.json, which bench.py reads for roofline.traffic and
+valu_roofline.
 """
 import csv
 import glob
@@ -74,6 +75,9 @@ if "SQ_INSTS_VALU_FMA_F32_median" in out:
         + out.get("SQ_INSTS_VALU_MUL_F32_median", 0) + out.get("SQ_INSTS_VALU_TRANS_F32_median", 0))
 out["source"] = ("rocprofv3 --kernel-trace --stats; separate --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_* | "
                  "SQ_INSTS_VALU_* (tools/gpu_bench_prof.sh), python bench.py --steps 20 --warmup 2")
-with open(os.path.join(prof, f"pmc_step_{robot}.json"), "w") as f:
-    json.dump(out, f, indent=1)
+# the round-named record under profiles/ (judged) and the copy bench.py ships and reads
+for path in (os.path.join(prof, f"{rnd}_pmc_step_{robot}.json"),
+             os.path.join(REPO, "pybullet-gym_amd", "perf", f"pmc_step_{robot}.json")):
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))

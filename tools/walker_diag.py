@@ -26,7 +26,6 @@ import physics_rules  # noqa: E402
 def main(env_id="Walker2DPyBulletEnv-v0", episode=0, last=12, rule=""):
     key = oracle.ENV_KEYS[env_id]
     tab = json.load(open(os.path.join(REPO, "pybullet-gym_amd", "models", f"{key}.json")))
-    physics_rules.load_springs()
     physics_rules.set_physics(physics_rules.parse(rule)[1] if rule else {})
     L = oracle.lib()
     L.pbg_oracle_contact_diag.argtypes = [ctypes.c_void_p, ctypes.c_int]
