@@ -13,7 +13,9 @@ Protocol: actions U(-1, 1) from Philox4x32-10 keyed by 0
 distinct batch per step; an untimed pre-roll (--preroll, 200 steps) ages the episodes past
 their first steps so the timed window sees steady-state contact counts and auto-resets, then
 W warm-up steps, then EXACTLY K timed steps (one HIP graph of the K launches) bracketed by a
-barrier + device sync on both sides, max over ranks.
+barrier + device sync on both sides, max over ranks.  The timed windows (--windows, default 5;
+value = the median window) replay the same captured graphs, i.e. the same K action batches;
+the env state moves on between windows, so every window steps different states.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N

@@ -857,22 +857,16 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       });
     }
   };
+  // the factor L and 1 / diag(L), replicated in registers: the rows pass reads them there
+  float L[D::NNZ], Ld[N];
   if constexpr (DIST) {
     // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
     gang_dyn_mass<R, T>(s, X SUB_STAMP_PASS);
     STAMP(3)
-    // --- replicated: factorisation and the unconstrained velocity, staged for the rows ---
-    float L[D::NNZ], rhs[N], Ld[N], nu[N], u[N];
-#pragma unroll
-    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
-#pragma unroll
-    for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
-    dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
-    stage_solution(L, Ld, u);
   } else {
     // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
     {
-      float L[D::NNZ], Ld[N], nu[N], u[N];
+      float nu[N], u[N];
       dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
       STAMP(3)
       stage_solution(L, Ld, u);
@@ -1021,6 +1015,19 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   }
   PBG_GANG_SYNC
   STAMP(4)
+  if constexpr (DIST) {
+    // --- replicated: factorisation and the unconstrained velocity, staged for the PGS; after
+    // the detection, so the factor is still in registers for the rows pass --------------------
+    float rhs[N], nu[N], u[N];
+#pragma unroll
+    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+#pragma unroll
+    for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
+    dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
+    stage_solution(L, Ld, u);
+    PBG_GANG_SYNC
+    STAMP(10)
+  }
   // --- distributed: constraint rows (limits first, then 3 rows per contact) --------------
   const int njobs = NLIM + 3 * nc;
 #pragma unroll 1
@@ -1079,8 +1086,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       float tt = J[i];
 #pragma unroll
       for (int kk = 0; kk < i; kk++)
-        if (D::coupled(i, kk)) tt -= X.l[G::O_L + D::lidx(i, kk)] * y[kk];
-      y[i] = tt * X.l[G::O_LD + i];
+        if (D::coupled(i, kk)) tt -= L[D::lidx(i, kk)] * y[kk];
+      y[i] = tt * Ld[i];
       D2 += y[i] * y[i];
     }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
