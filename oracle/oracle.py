@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
              "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
-             "double_pendulum_mujoco": 14}
+             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15}
 ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
             "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
             "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d",
@@ -25,7 +25,8 @@ ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0"
             "HumanoidFlagrunPyBulletEnv-v0": "humanoid_flagrun", "HopperMuJoCoEnv-v0": "hopper_mujoco",
             "Walker2DMuJoCoEnv-v0": "walker2d_mujoco", "HalfCheetahMuJoCoEnv-v0": "halfcheetah_mujoco",
             "AntMuJoCoEnv-v0": "ant_mujoco", "HumanoidMuJoCoEnv-v0": "humanoid_mujoco",
-            "InvertedDoublePendulumMuJoCoEnv-v0": "double_pendulum_mujoco"}
+            "InvertedDoublePendulumMuJoCoEnv-v0": "double_pendulum_mujoco",
+            "HumanoidFlagrunHarderPyBulletEnv-v0": "humanoid_flagrun_harder"}
 
 _lib = None
 
@@ -52,6 +53,7 @@ def lib():
         L.pbg_oracle_set_sim_params.argtypes = [P]
         L.pbg_oracle_pack.argtypes = [ctypes.c_int, P, P]
         L.pbg_oracle_pack_flag.argtypes = [ctypes.c_int, P, P, P, P]
+        L.pbg_oracle_pack_harder.argtypes = [ctypes.c_int, P, P, P, P, P, P]
         L.pbg_oracle_set_rng.argtypes = [ctypes.c_uint64, ctypes.c_int]
         L.pbg_oracle_set_mca_seed.argtypes = [ctypes.c_uint64]
         L.pbg_oracle_set_mca_seed.restype = None
@@ -172,13 +174,15 @@ class _PackOut(ctypes.Structure):
     _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_double), ("done", ctypes.c_uint8),
                 ("potential", ctypes.c_double), ("initial_z", ctypes.c_double),
                 ("feet_out", ctypes.c_void_p), ("rewards", ctypes.c_double * 5), ("dist", ctypes.c_double),
-                ("pitch", ctypes.c_double), ("at_limit", ctypes.c_int)]
+                ("pitch", ctypes.c_double), ("at_limit", ctypes.c_int), ("body_xyz", ctypes.c_double * 3)]
 
 
 def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet_new, act,
-         potential_old, initial_z, flag=None, body_avel=None):
+         potential_old, initial_z, flag=None, body_avel=None, harder=None):
     """Run the oracle's pack on explicit inputs (golden-vector tests).  flag (HumanoidFlagrun):
-    [target x, y, flag_timeout, next draw x, y]; the result then carries flag_out."""
+    [target x, y, flag_timeout, next draw x, y]; the result then carries flag_out.  harder
+    (HumanoidFlagrunHarder, with flag): [frame, on_ground, crawl_start, crawl_ignored, launch
+    draws 5]; the result then carries harder_out (pbg_oracle_pack_harder)."""
     rid = robot_id(name)
     info = Info(rid)
     arrs = dict(part_xyz=np.ascontiguousarray(part_xyz, dtype=np.float64),
@@ -201,11 +205,17 @@ def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet
     pout.obs = _p(obs)
     pout.feet_out = _p(feet_out)
     flag_out = np.zeros(3)
+    harder_out = np.zeros(11)
     if flag is None:
         assert lib().pbg_oracle_pack(rid, ctypes.byref(pin), ctypes.byref(pout)) == 0
+    elif harder is not None:
+        fin = np.ascontiguousarray(flag, dtype=np.float64)
+        hin = np.ascontiguousarray(harder, dtype=np.float64)
+        assert lib().pbg_oracle_pack_harder(rid, ctypes.byref(pin), ctypes.byref(pout), _p(fin), _p(flag_out),
+                                            _p(hin), _p(harder_out)) == 0
     else:
         fin = np.ascontiguousarray(flag, dtype=np.float64)
         assert lib().pbg_oracle_pack_flag(rid, ctypes.byref(pin), ctypes.byref(pout), _p(fin), _p(flag_out)) == 0
     return dict(obs=obs, reward=pout.reward, done=bool(pout.done), potential=pout.potential,
                 initial_z=pout.initial_z, feet=feet_out[:info.NF].copy(), rewards=list(pout.rewards),
-                flag_out=flag_out)
+                flag_out=flag_out, harder_out=harder_out)

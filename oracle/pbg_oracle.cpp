@@ -41,7 +41,9 @@
 #define MAXD 32
 #define MAXS 32
 #define MAXPAIR 72
-#define MAXROWS (2 * MAXD + 6 * (MAXS + MAXPAIR))  // 3 rows per contact + the rule study's 3 torsional
+#define MAXCG 24
+#define MAXCAND (MAXS + MAXPAIR + 8 + MAXCG)  // collision candidates (HumanoidFlagrunHarder's cube: 8 + NCG)
+#define MAXROWS (2 * MAXD + 6 * MAXCAND)      // 3 rows per contact + the rule study's 3 torsional
 
 thread_local FlopCount g_flops;
 thread_local uint64_t g_mca_state;
@@ -105,8 +107,8 @@ int g_diag_n = 0, g_diag_cap = 0;
 // ------------------------------------------------------------------ model view
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
-      floor, max_steps, robot_body, tip_link, flagrun;
-  double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip, contact_erp;
+      floor, max_steps, robot_body, tip_link, flagrun, harder, NCG;
+  double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip, contact_erp, cube_floor_mu;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
   const double (*off_pos)[3], (*axis)[3], (*anchor)[3], (*com)[3], (*off_quat)[4], (*inertia)[6];
@@ -119,6 +121,7 @@ struct MV {
   const int* slot_link; const double (*slot_point)[3]; const double *slot_radius, *slot_mu;
   const int *pair_a, *pair_b; const double (*pa0)[3], (*pa1)[3], (*pb0)[3], (*pb1)[3];
   const double *pra, *prb, *pmu;
+  const int* cg_link; const double (*cg_p0)[3], (*cg_p1)[3]; const double *cg_r, *cg_mu;  // cube vs robot geoms
 };
 
 template <class R>
@@ -128,7 +131,8 @@ MV view() {
   m.NDOF = R::NDOF; m.NA = R::NA; m.NO = R::NO; m.NR = R::NR; m.NF = R::NF; m.NP = R::NP;
   m.NS = R::NS; m.NPAIR = R::NPAIR; m.OBS = R::OBS; m.alive = R::alive; m.substeps = R::substeps;
   m.floor = R::floor; m.max_steps = R::max_episode_steps; m.robot_body = R::robot_body; m.tip_link = R::tip_link;
-  m.flagrun = R::flagrun;
+  m.flagrun = R::flagrun; m.harder = R::harder; m.NCG = R::NCG; m.cube_floor_mu = R::cube_floor_mu;
+  m.cg_link = R::cgeom_link; m.cg_p0 = R::cgeom_p0; m.cg_p1 = R::cgeom_p1; m.cg_r = R::cgeom_r; m.cg_mu = R::cgeom_mu;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
   m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.contact_erp = R::contact_erp; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
@@ -155,15 +159,15 @@ double sim_env_dt(const MV& m) { return sim_dt(m) * sim_substeps(m); }
 int sim_flag_timeout(const MV& m) { return (600 + sim_substeps(m) - 1) / sim_substeps(m); }
 
 const MV* model(int robot) {
-  static MV views[15] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[16] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                          view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                          view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
                          view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
                          view<pbg_models::HumanoidFlagrun>(), view<pbg_models::HopperMuJoCo>(),
                          view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>(),
                          view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>(),
-                         view<pbg_models::DoublePendulumMuJoCo>()};
-  if (robot < 0 || robot > 14) return nullptr;
+                         view<pbg_models::DoublePendulumMuJoCo>(), view<pbg_models::HumanoidFlagrunHarder>()};
+  if (robot < 0 || robot > 15) return nullptr;
   return &views[robot];
 }
 
@@ -262,6 +266,62 @@ void flag_draw(int e, Flag& f) {
   f.count++;
 }
 
+// HumanoidFlagrunHarder bookkeeping (robot_locomotors.py:230-302).  crawl_start NaN = None.
+struct Harder { int frame, onground, launches; double crawl_start, crawl_ignored; };
+// potential_leak (:275-278): clip(body z, 0, 0.8) / 0.8 + 1  (NaN passes np.clip)
+double potential_leak(double z) { const double c = z < 0.0 ? 0.0 : (z > PBG_HARDER_GROUND_Z ? PBG_HARDER_GROUND_Z : z); return c / 0.8 + 1.0; }
+// calc_potential (:280-302) given Humanoid.calc_potential's value fp and body_xyz[2]; mutates
+// the crawl bookkeeping (every call does: env reset, _step, and the flag re-draw's
+// `self.potential = self.calc_potential()` in HumanoidFlagrun.calc_state, :225)
+double harder_potential(Harder& h, double fp, double bz) {
+  if (bz < PBG_HARDER_GROUND_Z) {
+    if (std::isnan(h.crawl_start)) h.crawl_start = fp - h.crawl_ignored;
+    h.crawl_ignored = fp - h.crawl_start;
+    fp = h.crawl_start;
+  } else {
+    fp -= h.crawl_ignored;
+    h.crawl_start = NAN;
+  }
+  return fp + potential_leak(bz) * 100;
+}
+// The cube launch of alive_bonus (:251-265): angle U(-3.14, 3.14), speed U(20, 30), jitter
+// U(-1, 1)^3 from np_random -- here Philox4x32-10 keyed by the seed, counter (global env, launch
+// index, 0xC0BE / 0xC0BF, 0x5EED); `draws` (nullable, golden tests) = [angle, speed, jitter 3].
+// cube: the env's cube state words (position and velocity set, orientation kept, w = 0).
+void harder_launch(int e, Harder& h, const double* body_xyz, const double* speed, double* cube, const double* draws) {
+  double d[5];
+  if (draws) {
+    for (int i = 0; i < 5; i++) d[i] = draws[i];
+  } else {
+    uint32_t c[4] = {(uint32_t)(g_env_offset + e), (uint32_t)h.launches, 0xC0BEu, 0x5EEDu};
+    uint32_t c2[4] = {(uint32_t)(g_env_offset + e), (uint32_t)h.launches, 0xC0BFu, 0x5EEDu};
+    philox(c, (uint32_t)g_seed, (uint32_t)(g_seed >> 32));
+    philox(c2, (uint32_t)g_seed, (uint32_t)(g_seed >> 32));
+    const double u[5] = {(double)(c[0] >> 8) * (1.0 / 16777216.0), (double)(c[1] >> 8) * (1.0 / 16777216.0),
+                         (double)(c[2] >> 8) * (1.0 / 16777216.0), (double)(c[3] >> 8) * (1.0 / 16777216.0),
+                         (double)(c2[0] >> 8) * (1.0 / 16777216.0)};
+    d[0] = -3.14 + (3.14 - -3.14) * u[0];
+    d[1] = 20.0 + (30.0 - 20.0) * u[1];
+    for (int i = 0; i < 3; i++) d[2 + i] = -1.0 + (1.0 - -1.0) * u[2 + i];
+  }
+  h.launches++;
+  const double ttt = PBG_HARDER_FROM_DIST / d[1];
+  double t[3], pos[3], v[3];
+  for (int i = 0; i < 3; i++) t[i] = body_xyz[i] + speed[i] * ttt;
+  pos[0] = t[0] + PBG_HARDER_FROM_DIST * cos(d[0]);
+  pos[1] = t[1] + PBG_HARDER_FROM_DIST * sin(d[0]);
+  pos[2] = t[2] + 1.0;
+  for (int i = 0; i < 3; i++) v[i] = t[i] - pos[i];
+  const double sc = d[1] / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  for (int i = 0; i < 3; i++) {
+    v[i] *= sc;
+    v[i] += d[2 + i];
+    cube[i] = pos[i];
+    cube[7 + i] = v[i];
+    cube[10 + i] = 0.0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -291,6 +351,7 @@ typedef struct {
   double dist;               // walk_target_dist
   double pitch;              // body_rpy[1]
   int at_limit;              // joints_at_limit
+  double body_xyz[3];        // robot.body_xyz (mean part x, y; robot_body z)
 } pbg_pack_out;
 
 void pbg_oracle_set_flags(int flags) { g_flags = flags; }
@@ -308,7 +369,7 @@ int pbg_oracle_set_sim_params(const double* v) {
 // Physics-rule variants (see OPT_*): v[i] for i < n replaces option i; n = 0 restores the defaults.
 int pbg_oracle_set_physics(const double* v, int n) {
   for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = (v && i < n) ? v[i] : g_opt_default[i];
-  if (g_cache && g_cache_n) memset(g_cache, 0, g_cache_n * 4 * (MAXS + MAXPAIR) * sizeof(double));
+  if (g_cache && g_cache_n) memset(g_cache, 0, g_cache_n * 4 * MAXCAND * sizeof(double));
   return OPT_COUNT;
 }
 
@@ -343,7 +404,7 @@ int pbg_oracle_info(int robot, int* out) {
   const MV* m = model(robot);
   if (!m) return -1;
   int v[] = {m->NL, m->NJ, m->NDOF, m->NA, m->NO, m->NR, m->NF, m->NP, m->NS, m->NPAIR, m->OBS,
-             PBG_BASE_WORDS + 2 * m->NJ, PBG_AUX_RECORD_WORDS(m->NF, m->flagrun), m->floating, m->kind,
+             PBG_STATE_WORDS(m->NJ, m->harder), PBG_AUX_RECORD_WORDS(m->NF, m->flagrun, m->harder), m->floating, m->kind,
              sim_substeps(*m)};
   memcpy(out, v, sizeof(v));
   return 0;
@@ -423,6 +484,7 @@ static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* ou
   out->initial_z = z0;
   out->pitch = rpy[1];
   out->at_limit = at_limit;
+  out->body_xyz[0] = bx; out->body_xyz[1] = by; out->body_xyz[2] = bz;
   double dt = sim_env_dt(m);  // scene.dt = timestep*frame_skip (scene_bases.py:17)
   out->potential = -dist / dt;         // robot_locomotors.py:79
   for (int i = 0; i < m.NF; i++) out->feet_out[i] = in->feet_prev[i];
@@ -479,7 +541,7 @@ static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* ou
 // countdown, pack against the current flag, re-draw and pack again when the target is
 // within 1 m or the timeout ran out.  `next` (nullable) replaces the draw (golden tests).
 static void flag_pack(int robot, const MV& m, pbg_pack_in* in, pbg_pack_out* out, Flag& f, int e,
-                      const double* next) {
+                      const double* next, Harder* h = nullptr) {
   if (!m.flagrun) { pbg_oracle_pack(robot, in, out); return; }
   f.timeout -= 1;
   in->target_x = f.tx; in->target_y = f.ty;
@@ -489,7 +551,43 @@ static void flag_pack(int robot, const MV& m, pbg_pack_in* in, pbg_pack_out* out
     else flag_draw(e, f);
     in->target_x = f.tx; in->target_y = f.ty;
     pbg_oracle_pack(robot, in, out);
+    if (h) (void)harder_potential(*h, out->potential, out->body_xyz[2]);  // robot.potential (:225)
   }
+}
+static Harder load_harder(const MV& m, const double* a) {
+  Harder h = {0, 0, 0, NAN, 0.0};
+  if (m.harder) { h.frame = (int)a[8 + m.NF]; h.onground = (int)a[9 + m.NF]; h.crawl_start = a[10 + m.NF];
+                  h.crawl_ignored = a[11 + m.NF]; h.launches = (int)a[12 + m.NF]; }
+  return h;
+}
+static void store_harder(const MV& m, double* a, const Harder& h) {
+  if (m.harder) { a[8 + m.NF] = h.frame; a[9 + m.NF] = h.onground; a[10 + m.NF] = h.crawl_start;
+                  a[11 + m.NF] = h.crawl_ignored; a[12 + m.NF] = h.launches; }
+}
+// The Harder half of _step after calc_state (gym_locomotion_envs.py:59-70 with
+// HumanoidFlagrunHarder.alive_bonus / calc_potential): out holds the calc_state pack with the
+// Humanoid's reward; alive, done, potential, progress and the reward are redone.  Returns 1 when
+// the cube was launched (its state words in `cube` rewritten).
+static int harder_step(const MV& m, const pbg_pack_in* in, pbg_pack_out* out, Harder& h, int e, double* cube,
+                       const double* draws) {
+  const float z = out->obs[0] + (float)m.z0fixed;  // state[0] + initial_z (float32, NEP 50)
+  int launched = 0;
+  if (h.frame % PBG_HARDER_LAUNCH_EVERY == 0 && h.frame > PBG_HARDER_LAUNCH_AFTER && h.onground == 0) {
+    harder_launch(e, h, out->body_xyz, in->body_vel, cube, draws);
+    launched = 1;
+  }
+  if (z < (float)PBG_HARDER_GROUND_Z) h.onground += 1;
+  else if (h.onground > 0) h.onground -= 1;
+  h.frame += 1;
+  const double alive = h.onground < PBG_HARDER_GROUND_FRAMES ? potential_leak(out->body_xyz[2]) : -1.0;
+  bool done = alive < 0;
+  for (int i = 0; i < m.OBS; i++) if (std::isnan(out->obs[i])) done = true;
+  out->potential = harder_potential(h, out->potential, out->body_xyz[2]);
+  const double progress = out->potential - in->potential_old;
+  out->rewards[0] = alive; out->rewards[1] = progress;
+  out->reward = ((((0.0 + alive) + progress) + out->rewards[2]) + out->rewards[3]) + 0.0;
+  out->done = done;
+  return launched;
 }
 static Flag load_flag(const MV& m, const double* a) {
   Flag f = {0.0, 0.0, 0, 0};
@@ -513,6 +611,31 @@ int pbg_oracle_pack_flag(int robot, const pbg_pack_in* in, pbg_pack_out* out, co
   Flag f = {flag_in[0], flag_in[1], (int)flag_in[2], 0};
   flag_pack(robot, *mp, &in2, out, f, 0, flag_in + 3);
   flag_out[0] = f.tx; flag_out[1] = f.ty; flag_out[2] = f.timeout;
+  return 0;
+}
+
+// HumanoidFlagrunHarder golden form: flag_in / flag_out as above; harder_in = [frame,
+// on_ground_frame_counter, crawl_start (NaN = None), crawl_ignored, launch draws: angle, speed,
+// jitter 3 (NaN: no launch recorded)]; harder_out = [frame, on_ground, crawl_start,
+// crawl_ignored, launched, cube position 3, cube velocity 3].  in->act NULL: the reset's
+// calc_state + env.potential = calc_potential() (env_bases.py:69-70).
+int pbg_oracle_pack_harder(int robot, const pbg_pack_in* in, pbg_pack_out* out, const double* flag_in,
+                           double* flag_out, const double* harder_in, double* harder_out) {
+  const MV* mp = model(robot);
+  if (!mp || !mp->harder) return -1;
+  pbg_pack_in in2 = *in;
+  Flag f = {flag_in[0], flag_in[1], (int)flag_in[2], 0};
+  Harder h = {(int)harder_in[0], (int)harder_in[1], 0, harder_in[2], harder_in[3]};
+  flag_pack(robot, *mp, &in2, out, f, 0, flag_in + 3, &h);
+  double cube[PBG_CUBE_WORDS];
+  for (int i = 0; i < PBG_CUBE_WORDS; i++) cube[i] = NAN;
+  int launched = 0;
+  if (in->act) launched = harder_step(*mp, &in2, out, h, 0, cube, harder_in + 4);
+  else out->potential = harder_potential(h, out->potential, out->body_xyz[2]);
+  flag_out[0] = f.tx; flag_out[1] = f.ty; flag_out[2] = f.timeout;
+  const double ho[5] = {(double)h.frame, (double)h.onground, h.crawl_start, h.crawl_ignored, (double)launched};
+  for (int i = 0; i < 5; i++) harder_out[i] = ho[i];
+  for (int i = 0; i < 3; i++) { harder_out[5 + i] = cube[i]; harder_out[8 + i] = cube[7 + i]; }
   return 0;
 }
 
@@ -697,15 +820,19 @@ int pbg_oracle_reset_mask(int robot, int n, double* state, double* aux, const do
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_RECORD_WORDS(m.NF, m.flagrun);
+  int SD = PBG_STATE_WORDS(m.NJ, m.harder), AD = PBG_AUX_RECORD_WORDS(m.NF, m.flagrun, m.harder);
   for (int e = 0; e < n; e++) {
     if (mask && !mask[e]) continue;
-    if (g_cache && (size_t)e < g_cache_n) memset(g_cache + (size_t)e * 4 * (MAXS + MAXPAIR), 0, sizeof(double) * 4 * (MAXS + MAXPAIR));
+    if (g_cache && (size_t)e < g_cache_n) memset(g_cache + (size_t)e * 4 * MAXCAND, 0, sizeof(double) * 4 * MAXCAND);
     double* s = state + (size_t)e * SD;
     double* a = aux + (size_t)e * AD;
     for (int i = 0; i < 3; i++) s[i] = m.base_pos[i];
     for (int i = 0; i < 4; i++) s[3 + i] = m.base_quat[i];
-    for (int i = 7; i < PBG_BASE_WORDS + 2 * m.NJ; i++) s[i] = 0.0;
+    for (int i = 7; i < SD; i++) s[i] = 0.0;
+    if (m.harder) {  // restoreState + resetBasePositionAndOrientation(cube, [-1.5, 0, 0.05], [0, 0, 0, 1]) (:241)
+      double* cs = s + PBG_BASE_WORDS + 2 * m.NJ;
+      cs[0] = PBG_CUBE_X0; cs[1] = PBG_CUBE_Y0; cs[2] = PBG_CUBE_Z0; cs[6] = 1.0;
+    }
     // robot_pendula.py:16 (swingup: 3.1415 + u)
     for (int r = 0; r < m.NR; r++) s[PBG_BASE_WORDS + m.reset_dof[r]] = m.reset_offset[r] + qinit[(size_t)e * m.NR + r];
     float* ob = obs + (size_t)e * m.OBS;
@@ -725,8 +852,15 @@ int pbg_oracle_reset_mask(int robot, int n, double* state, double* aux, const do
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);
     if (m.flagrun) flag_draw(e, fl);  // robot_specific_reset -> flag_reposition (:199-201)
-    flag_pack(robot, m, &in, &out, fl, e, nullptr);
+    // HumanoidFlagrunHarder.robot_specific_reset (:237-248): frame, counters, crawl state
+    Harder hd = load_harder(m, a);
+    hd.frame = 0; hd.onground = 0; hd.crawl_start = NAN; hd.crawl_ignored = 0.0;
+    flag_pack(robot, m, &in, &out, fl, e, nullptr, m.harder ? &hd : nullptr);
     store_flag(m, a, fl);
+    if (m.harder) {
+      out.potential = harder_potential(hd, out.potential, out.body_xyz[2]);  // env_bases.py:70
+      store_harder(m, a, hd);
+    }
     a[0] = out.potential;
     a[1] = out.initial_z;
     a[3] = 1.0;  // the floor is in robot.parts from now on
@@ -753,10 +887,10 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  int SD = PBG_BASE_WORDS + 2 * m.NJ, AD = PBG_AUX_RECORD_WORDS(m.NF, m.flagrun);
+  int SD = PBG_STATE_WORDS(m.NJ, m.harder), AD = PBG_AUX_RECORD_WORDS(m.NF, m.flagrun, m.harder);
   if (g_opt[OPT_WARM] != 0.0 && g_cache_n < (size_t)n) {  // warm-start cache (rule study only)
     free(g_cache);
-    g_cache = (double*)calloc((size_t)n * 4 * (MAXS + MAXPAIR), sizeof(double));
+    g_cache = (double*)calloc((size_t)n * 4 * MAXCAND, sizeof(double));
     g_cache_n = g_cache ? (size_t)n : 0;
   }
 #pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
@@ -766,7 +900,7 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     const float* ac = act + (size_t)e * m.NA;
     uint8_t slot_active[MAXS];
     uint32_t sig = 0;
-    double* cache = g_cache && (size_t)e < g_cache_n ? g_cache + (size_t)e * 4 * (MAXS + MAXPAIR) : nullptr;
+    double* cache = g_cache && (size_t)e < g_cache_n ? g_cache + (size_t)e * 4 * MAXCAND : nullptr;
     uint32_t as = 0;
     int nc;
     if (precision == 32) {
@@ -802,8 +936,13 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);
-    flag_pack(robot, m, &in, &out, fl, e, nullptr);
+    Harder hd = load_harder(m, a);
+    flag_pack(robot, m, &in, &out, fl, e, nullptr, m.harder ? &hd : nullptr);
     store_flag(m, a, fl);
+    if (m.harder) {
+      (void)harder_step(m, &in, &out, hd, e, s + PBG_BASE_WORDS + 2 * m.NJ, nullptr);
+      store_harder(m, a, hd);
+    }
     rew[e] = out.reward;
     done[e] = out.done;
     if (terms) memcpy(terms, out.rewards, sizeof(out.rewards));
@@ -841,7 +980,7 @@ int pbg_oracle_count_flops(int robot, int n, double* state, const float* act, ui
   const MV* mp = model(robot);
   if (!mp) return -1;
   const MV& m = *mp;
-  const int SD = PBG_BASE_WORDS + 2 * m.NJ;
+  const int SD = PBG_STATE_WORDS(m.NJ, m.harder);
   g_flops = FlopCount{0, 0, 0, 0, 0, 0, 0};
   for (int e = 0; e < n; e++) {
     uint8_t slot_active[MAXS];

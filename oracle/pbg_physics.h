@@ -82,7 +82,16 @@ template <class T> struct KinT {
   V3T<T> w[MAXL + 1], v[MAXL + 1];    // angular velocity, COM linear velocity
   V3T<T> al[MAXL + 1], ac[MAXL + 1];  // bias angular / COM linear acceleration
   V3T<T> ja[MAXD], jo[MAXD];          // per joint dof: world axis, world anchor
+  M3T<T> Rc;                          // HumanoidFlagrunHarder's cube: orientation, COM
+  V3T<T> xc;
 };
+
+// HumanoidFlagrunHarder: the attacking cube is a second free body (its state words follow the
+// robot's, sim_params.h PBG_STATE_WORDS; its 6 velocity coordinates [v, w] follow the robot's
+// in the generalized velocity).  Contact bodies: b >= 0 robot body, -1 floor, -2 cube.
+inline int cube_word(const MV& m) { return PBG_BASE_WORDS + 2 * m.NJ; }
+inline int n_total(const MV& m) { return m.NDOF + (m.harder ? 6 : 0); }
+#define CUBE_BODY (-2)
 
 // s: the env's state record in T (layout of sim_params.h)
 template <class T> void forward_kinematics(const MV& m, const T* s, KinT<T>& k) {
@@ -95,6 +104,11 @@ template <class T> void forward_kinematics(const MV& m, const T* s, KinT<T>& k) 
   k.v[0] = m.floating ? v3p(s + 7) : vzero<T>();
   k.al[0] = vzero<T>();
   k.ac[0] = vzero<T>();
+  if (m.harder) {
+    const T* cs = s + cube_word(m);
+    k.Rc = quat_to_m3(cs[3], cs[4], cs[5], cs[6]);
+    k.xc = v3p(cs);
+  }
   for (int l = 0; l < m.NL; l++) {
     int p = m.link_parent[l] + 1;
     M3T<T> Ro = quat_to_m3c<T>(m.off_quat[l]);
@@ -182,8 +196,15 @@ template <class T> void point_jacobian(const MV& m, const KinT<T>& k, int b, V3T
 
 // ------------------------------------------------------------------ dynamics
 // M (NDOF x NDOF) and bias C (Coriolis/centrifugal/gyroscopic + gravity + body damping).
-template <class T> void mass_and_bias(const MV& m, const KinT<T>& k, T M[MAXD][MAXD], T* C) {
+template <class T> void mass_and_bias(const MV& m, const KinT<T>& k, T M[MAXD][MAXD], T* C, const T* s = nullptr) {
   int n = m.NDOF;
+  if (m.harder) {  // the cube's block: diag(m, m, m, I, I, I) (isotropic inertia), decoupled
+    const int n6 = n_total(m);
+    for (int i = n; i < n6; i++) {
+      C[i] = T(0);
+      for (int j = 0; j < n6; j++) M[i][j] = M[j][i] = T(0);
+    }
+  }
   for (int i = 0; i < n; i++) {
     C[i] = T(0);
     for (int j = 0; j < n; j++) M[i][j] = T(0);
@@ -218,6 +239,18 @@ template <class T> void mass_and_bias(const MV& m, const KinT<T>& k, T M[MAXD][M
     }
   }
   for (int d = 0; d < m.NJ; d++) M[gidx(m, d)][gidx(m, d)] = M[gidx(m, d)][gidx(m, d)] + T(m.armature[d]);
+  if (m.harder && s) {
+    // free-body bias as for the robot's base (ac = al = 0): f = m (-g) + m (k1 + k2 |v|) v,
+    // tq = w x (I w) + (k1 + k2 |w|) I w, whose gyroscopic term vanishes for the isotropic cube
+    const T* cs = s + cube_word(m);
+    const T mc(PBG_CUBE_MASS), Ic(PBG_CUBE_INERTIA);
+    const V3T<T> v = v3p(cs + 7), w = v3p(cs + 10);
+    const V3T<T> f = mc * (vzero<T>() - g) + (mc * (kd_lin + kd_lin * norm(v))) * v;
+    const V3T<T> tq = ((kd_ang + kd_ang * norm(w)) * Ic) * w;
+    const int c0 = m.NDOF;
+    for (int i = 0; i < 3; i++) { M[c0 + i][c0 + i] = mc; M[c0 + 3 + i][c0 + 3 + i] = Ic; }
+    C[c0] = f.x; C[c0 + 1] = f.y; C[c0 + 2] = f.z; C[c0 + 3] = tq.x; C[c0 + 4] = tq.y; C[c0 + 5] = tq.z;
+  }
 }
 
 // in-place Cholesky M = L L^T (lower)
@@ -297,6 +330,96 @@ template <class T> struct ContactT {
   T dist, mu;
 };
 
+// HumanoidFlagrunHarder's cube (a box of half extent h) against the floor and the robot's
+// geoms.  Candidates after the floor slots and self pairs: NS + NPAIR + k for cube corner k
+// (k bit 0/1/2: -/+ h along the cube's x/y/z), NS + NPAIR + 8 + g for robot geom g
+// (cgeom_*).  [EXT] Bullet's box-plane algorithm keeps the deepest vertices of the box in its
+// manifold (up to 4 with the multipoint iterations pybullet enables) -- here every corner
+// within the contact threshold is a point, normal +z.  Box-capsule: Bullet's GJK/EPA returns
+// the closest (or deepest) points of the two convex shapes; here the same points are found
+// on the capsule's segment by minimising the box's signed distance function along it (convex
+// in the segment parameter: golden-section search, CUBE_GS_ITERS fixed rounds, then the box
+// point and normal of the minimiser).  Normal from the cube (B) into the robot link (A).
+#define CUBE_GS_ITERS 24
+template <class T> inline T box_sd(V3T<T> p, T h) {  // signed distance of a box-local point
+  const T qx = fabs(p.x) - h, qy = fabs(p.y) - h, qz = fabs(p.z) - h;
+  const T ox = tmax(qx, T(0)), oy = tmax(qy, T(0)), oz = tmax(qz, T(0));
+  return sqrt(ox * ox + oy * oy + oz * oz) + tmin(tmax(qx, tmax(qy, qz)), T(0));
+}
+template <class T>
+int detect_cube_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, int nc, int sub, uint32_t* sig) {
+  const T thr(g_opt[OPT_CONTACT_THR]), h(PBG_CUBE_HALF);
+  const M3T<T>& Rc = k.Rc;
+  const V3T<T> xc = k.xc;
+  for (int c = 0; c < 8; c++) {  // corners vs floor
+    const V3T<T> lc = v3((c & 1) ? h : T(0) - h, (c & 2) ? h : T(0) - h, (c & 4) ? h : T(0) - h);
+    const V3T<T> p = xc + mul(Rc, lc);
+    if (!(p.z < thr)) continue;
+    if (sig) *sig += pbg_contact_hash((uint32_t)sub, (uint32_t)(m.NS + m.NPAIR + c));
+    ContactT<T>& ct = out[nc++];
+    ct.cand = m.NS + m.NPAIR + c;
+    ct.body_a = CUBE_BODY; ct.body_b = -1;
+    ct.pa = p; ct.pb = v3(p.x, p.y, T(0));
+    ct.n = v3(T(0), T(0), T(1)); ct.dist = p.z; ct.mu = T(m.cube_floor_mu);
+  }
+  // R^T: robot geom endpoints into the cube frame
+  M3T<T> Rt;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) Rt.m[i][j] = Rc.m[j][i];
+  const T bound(0.5 * 1.7320508075688772 * 2.0 * PBG_CUBE_HALF);  // cube circumradius
+  for (int g = 0; g < m.NCG; g++) {
+    const int b = m.cg_link[g] + 1;
+    const V3T<T> e0 = k.x[b] + mul(k.R[b], v3c<T>(m.cg_p0[g])), e1 = k.x[b] + mul(k.R[b], v3c<T>(m.cg_p1[g]));
+    const T r(m.cg_r[g]);
+    // broad phase: the segment's distance to the cube centre vs circumradius + radius + threshold
+    const V3T<T> p0 = mul(Rt, e0 - xc), p1 = mul(Rt, e1 - xc), d = p1 - p0;
+    const T dd = dot(d, d);
+    T t0 = dd > T(1e-12) ? tmin(tmax((T(0) - dot(p0, d)) / dd, T(0)), T(1)) : T(0);
+    const V3T<T> pc = p0 + t0 * d;
+    if (!(norm(pc) < bound + r + thr)) continue;
+    T t = T(0);
+    if (dd > T(1e-12)) {  // golden-section minimisation of box_sd(p0 + t d) over [0, 1]
+      const T phi(0.6180339887498949);
+      T a(0), bb(1);
+      T x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
+      T f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
+      for (int it = 0; it < CUBE_GS_ITERS; it++) {
+        if (f1 <= f2) { bb = x2; x2 = x1; f2 = f1; x1 = bb - phi * (bb - a); f1 = box_sd(p0 + x1 * d, h); }
+        else { a = x1; x1 = x2; f1 = f2; x2 = a + phi * (bb - a); f2 = box_sd(p0 + x2 * d, h); }
+      }
+      t = T(0.5) * (a + bb);
+    }
+    const V3T<T> ps = p0 + t * d;
+    const T sd = box_sd(ps, h);
+    const T dist = sd - r;
+    if (!(dist < thr)) continue;
+    // box point and outward normal (cube frame)
+    V3T<T> nb, qb;
+    const T qx = fabs(ps.x) - h, qy = fabs(ps.y) - h, qz = fabs(ps.z) - h;
+    if (tmax(qx, tmax(qy, qz)) > T(0)) {  // outside: the nearest point of the box
+      qb = v3(tmin(tmax(ps.x, T(0) - h), h), tmin(tmax(ps.y, T(0) - h), h), tmin(tmax(ps.z, T(0) - h), h));
+      const V3T<T> dv = ps - qb;
+      const T l = norm(dv);
+      nb = l > T(1e-9) ? (T(1) / l) * dv : v3(T(0), T(0), T(1));
+    } else {  // inside: through the nearest face
+      const int ax = (qx >= qy && qx >= qz) ? 0 : (qy >= qz ? 1 : 2);
+      const T c = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
+      const T sg = c < T(0) ? T(-1) : T(1);
+      nb = v3(ax == 0 ? sg : T(0), ax == 1 ? sg : T(0), ax == 2 ? sg : T(0));
+      qb = v3(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
+    }
+    const V3T<T> n = mul(Rc, nb);
+    if (sig) *sig += pbg_contact_hash((uint32_t)sub, (uint32_t)(m.NS + m.NPAIR + 8 + g));
+    ContactT<T>& ct = out[nc++];
+    ct.cand = m.NS + m.NPAIR + 8 + g;
+    ct.body_a = b; ct.body_b = CUBE_BODY;
+    ct.pa = xc + mul(Rc, ps) - r * n;
+    ct.pb = xc + mul(Rc, qb);
+    ct.n = n; ct.dist = dist; ct.mu = T(m.cg_mu[g]);
+  }
+  return nc;
+}
+
 // sig (nullable): adds pbg_contact_hash(sub, candidate) of every active candidate
 template <class T>
 int detect_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, uint8_t* slot_active, int sub, uint32_t* sig) {
@@ -340,14 +463,31 @@ int detect_contacts(const MV& m, const KinT<T>& k, ContactT<T>* out, uint8_t* sl
       ct.n = n; ct.dist = dist; ct.mu = T(m.pmu[p]);
     }
   }
+  if (m.harder) nc = detect_cube_contacts(m, k, out, nc, sub, sig);
   return nc;
 }
 
+// the cube's columns of a row along dir at world point P (v . dir + w . (r x dir)), scaled by sg
+template <class T> void cube_row_jacobian(const MV& m, const KinT<T>& k, V3T<T> P, V3T<T> dir, T sg, T* J) {
+  const V3T<T> rx = cross(P - k.xc, dir);
+  const int c0 = m.NDOF;
+  J[c0] = sg * dir.x; J[c0 + 1] = sg * dir.y; J[c0 + 2] = sg * dir.z;
+  J[c0 + 3] = sg * rx.x; J[c0 + 4] = sg * rx.y; J[c0 + 5] = sg * rx.z;
+}
 template <class T> void contact_row_jacobian(const MV& m, const KinT<T>& k, const ContactT<T>& c, V3T<T> dir, T* J) {
   T Jv[3][MAXD], Jw[3][MAXD];
+  if (m.harder)
+    for (int j = m.NDOF; j < n_total(m); j++) J[j] = T(0);
+  if (c.body_a == CUBE_BODY) {  // cube vs floor
+    for (int j = 0; j < m.NDOF; j++) J[j] = T(0);
+    cube_row_jacobian(m, k, c.pa, dir, T(1), J);
+    return;
+  }
   point_jacobian(m, k, c.body_a, c.pa, Jv, Jw);
   for (int j = 0; j < m.NDOF; j++) J[j] = dir.x * Jv[0][j] + dir.y * Jv[1][j] + dir.z * Jv[2][j];
-  if (c.body_b >= 0) {
+  if (c.body_b == CUBE_BODY) {
+    cube_row_jacobian(m, k, c.pb, dir, T(-1), J);
+  } else if (c.body_b >= 0) {
     point_jacobian(m, k, c.body_b, c.pb, Jv, Jw);
     for (int j = 0; j < m.NDOF; j++) J[j] = J[j] - (dir.x * Jv[0][j] + dir.y * Jv[1][j] + dir.z * Jv[2][j]);
   }
@@ -409,6 +549,30 @@ template <class T> inline T clampv(T v) {
   return v > mx ? mx : (v < T(0) - mx ? T(0) - mx : v);
 }
 
+// Free body (the floating base, the cube): record words [pos 3 | quat 4 | v 3 | w 3] from its
+// generalized velocity nu = [v, w]; semi-implicit Euler, exponential-map quaternion update
+// with the world angular velocity  [EXT] btMultiBody pQuatUpdateFun
+template <class T> void integrate_free_body(T* s, const T* nu, T dt) {
+  for (int i = 0; i < 3; i++) { s[7 + i] = nu[i]; s[10 + i] = nu[3 + i]; s[i] = s[i] + dt * nu[i]; }
+  V3T<T> w = v3p(s + 10);
+  T ang = norm(w);
+  const T thr(PBG_ANGULAR_MOTION_THRESHOLD), half(0.5);
+  if (ang * dt > thr) ang = thr / dt;
+  V3T<T> ax;
+  if (ang < T(0.001)) ax = (half * dt - (dt * dt * dt) * T(0.020833333333) * ang * ang) * w;
+  else ax = (sin(half * ang * dt) / ang) * w;
+  T dw = cos(half * ang * dt);
+  T* qt = s + 3;
+  T x = qt[0], y = qt[1], z = qt[2], ww = qt[3];
+  // dq * q (Hamilton, xyzw)
+  T nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+  T ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+  T nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+  T nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+  T inv = T(1) / sqrt(nx * nx + ny * ny + nz * nz + nw * nw);
+  qt[0] = nx * inv; qt[1] = ny * inv; qt[2] = nz * inv; qt[3] = nw * inv;
+}
+
 // ------------------------------------------------------------------ one sub-step
 // s: the env's state record in T.  tau: motor torque on joint dofs, held over the env step
 // (robot_locomotors.py:26-29).  qd_step: joint velocities at the start of the env step
@@ -419,14 +583,14 @@ template <class T>
 int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint32_t* sig, double* cache,
             const T* qd_step, uint32_t* asig) {
   const T dt(sim_dt(m));
-  const int n = m.NDOF;
+  const int n = n_total(m);  // the robot's generalized velocity (+ the cube's 6)
   static thread_local KinT<T> k;
   static thread_local T M[MAXD][MAXD];
   static thread_local RowT<T> rows[MAXROWS];
-  static thread_local ContactT<T> cts[MAXS + MAXPAIR];
+  static thread_local ContactT<T> cts[MAXCAND];
   T C[MAXD], rhs[MAXD], qdd[MAXD], nu[MAXD];
   forward_kinematics(m, s, k);
-  mass_and_bias(m, k, M, C);
+  mass_and_bias(m, k, M, C, s);
   // joint damping tau = -d*qd from this sub-step's velocity (explicit; [EXT] pybullet
   // applyJointDamping -- applied per sub-step here, the stable choice at dt/4)
   const T* qd0 = s + PBG_BASE_WORDS + m.NJ;
@@ -449,6 +613,9 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     for (int i = 0; i < 3; i++) { nu[i] = s[7 + i]; nu[3 + i] = s[10 + i]; }
   }
   for (int d = 0; d < m.NJ; d++) nu[gidx(m, d)] = qd[d];
+  T* cs = s + cube_word(m);  // HumanoidFlagrunHarder's cube (n_total)
+  if (m.harder)
+    for (int i = 0; i < 3; i++) { nu[m.NDOF + i] = cs[7 + i]; nu[m.NDOF + 3 + i] = cs[10 + i]; }
   for (int i = 0; i < n; i++) nu[i] = clampv(nu[i] + dt * qdd[i]);
 
   // constraint rows, Bullet order: joint limits, contact normals, frictions
@@ -471,7 +638,7 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   int nc = detect_contacts(m, k, cts, slot_active, sub, sig);
   if (g_flags & 2) nc = 0;
   // contact -> collision candidate (the warm-start cache key): slots in order, then pairs
-  int cand[MAXS + MAXPAIR];
+  int cand[MAXCAND];
   for (int c = 0; c < nc; c++) cand[c] = cts[c].cand;
   if (g_opt[OPT_SEP_MODE] != 0.0) {  // drop separated contacts (no speculative rows)
     int w = 0;
@@ -593,7 +760,7 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     }
   }
   if (cache) {
-    for (int i = 0; i < (m.NS + m.NPAIR); i++) cache[4 * i + 3] = 0.0;
+    for (int i = 0; i < MAXCAND; i++) cache[4 * i + 3] = 0.0;
     for (int c = 0; c < nc; c++) {
       if (cand[c] < 0) continue;
       double* cc = cache + 4 * cand[c];
@@ -610,27 +777,8 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     qd[d] = nu[gidx(m, d)];
     q[d] = q[d] + dt * qd[d];
   }
-  if (m.floating) {
-    for (int i = 0; i < 3; i++) { s[7 + i] = nu[i]; s[10 + i] = nu[3 + i]; s[i] = s[i] + dt * nu[i]; }
-    // exponential-map quaternion update with world angular velocity  [EXT] pQuatUpdateFun
-    V3T<T> w = v3p(s + 10);
-    T ang = norm(w);
-    const T thr(PBG_ANGULAR_MOTION_THRESHOLD), half(0.5);
-    if (ang * dt > thr) ang = thr / dt;
-    V3T<T> ax;
-    if (ang < T(0.001)) ax = (half * dt - (dt * dt * dt) * T(0.020833333333) * ang * ang) * w;
-    else ax = (sin(half * ang * dt) / ang) * w;
-    T dw = cos(half * ang * dt);
-    T* qt = s + 3;
-    T x = qt[0], y = qt[1], z = qt[2], ww = qt[3];
-    // dq * q (Hamilton, xyzw)
-    T nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
-    T ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
-    T nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
-    T nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-    T inv = T(1) / sqrt(nx * nx + ny * ny + nz * nz + nw * nw);
-    qt[0] = nx * inv; qt[1] = ny * inv; qt[2] = nz * inv; qt[3] = nw * inv;
-  }
+  if (m.floating) integrate_free_body(s, nu, dt);
+  if (m.harder) integrate_free_body(cs, nu + m.NDOF, dt);
   return nc;
 }
 
@@ -640,8 +788,8 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
 template <class T>
 int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_active, uint32_t* sig, double* cache,
                  uint32_t* asig = nullptr) {
-  T s[PBG_BASE_WORDS + 2 * MAXD], tau[MAXD], qd_step[MAXD];
-  const int SD = PBG_BASE_WORDS + 2 * m.NJ;
+  T s[PBG_BASE_WORDS + 2 * MAXD + PBG_CUBE_WORDS], tau[MAXD], qd_step[MAXD];
+  const int SD = PBG_STATE_WORDS(m.NJ, m.harder);
   for (int i = 0; i < SD; i++) s[i] = T(state[i]);
   for (int d = 0; d < m.NJ; d++) tau[d] = T(0);
   for (int i = 0; i < m.NA; i++) {  // robot_locomotors.py:26-29

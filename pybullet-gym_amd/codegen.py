@@ -80,6 +80,11 @@ def _chain_links(model: mjcf.RobotModel, li: int) -> List[int]:
     return out[::-1]
 
 
+# HumanoidFlagrunHarder's cube: cube_small.urdf <lateral_friction value="1.0"/> (pybullet_data;
+# envs/assets/things/cube_small.urdf), combined with the other body's friction by product [EXT]
+CUBE_FRICTION = 1.0
+
+
 def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None) -> Dict:
     ov = ov or {}
     floor_mu = apply_overrides(model, ov)
@@ -196,6 +201,16 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
     pair_ga = [gid(p[0], p[1]) for p in pairs]
     pair_gb = [gid(p[2], p[3]) for p in pairs]
 
+    # HumanoidFlagrunHarder: every collision geom of the robot against the cube (a separate
+    # body: pybullet's default collision filter lets it hit all links), sphere p0 == p1
+    cgeoms = []
+    if spec.harder:
+        for li, geoms in [(-1, model.base_geoms)] + [(li, l.geoms) for li, l in enumerate(links)]:
+            for g in geoms:
+                if g.contype == 0 and g.conaffinity == 0:
+                    continue
+                cgeoms.append((li, g))
+
     feet = [model.link_index(f) for f in spec.foot_list]
     inertia6 = lambda I: [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
     t = dict(
@@ -237,6 +252,10 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
         NG=len(pgeoms), geom_link=[g[0] for g in pgeoms], geom_p0=[list(g[1].p0) for g in pgeoms],
         geom_p1=[list(g[1].p1) for g in pgeoms], geom_r=[g[1].radius for g in pgeoms],
         pair_ga=pair_ga, pair_gb=pair_gb,
+        harder=int(spec.harder), NCG=len(cgeoms), cgeom_link=[g[0] for g in cgeoms],
+        cgeom_p0=[list(g[1].p0) for g in cgeoms], cgeom_p1=[list(g[1].p1) for g in cgeoms],
+        cgeom_r=[g[1].radius for g in cgeoms], cgeom_mu=[g[1].friction * CUBE_FRICTION for g in cgeoms],
+        cube_floor_mu=(CUBE_FRICTION * floor_mu if spec.harder else 0.0),
         contact_erp=float(ov.get("contact_erp", CONTACT_ERP_DEFAULT)),
     )
     return t
@@ -290,10 +309,10 @@ def emit_struct(t: Dict) -> str:
          f"  static constexpr int kind = {t['kind']};",
          f"  static constexpr bool floating = {'true' if t['floating'] else 'false'};"]
     for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "NG", "OBS", "alive", "substeps",
-              "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun"):
+              "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun", "harder", "NCG"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
-              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp"):
+              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp", "cube_floor_mu"):
         L.append(f"  static constexpr double {k} = {_num(t[k])};")
     L.append(_arr1("base_inertia", "double", t["base_inertia"]))
     L.append(_arr1("base_pos", "double", t["base_pos"]))
@@ -335,6 +354,11 @@ def emit_struct(t: Dict) -> str:
     L.append(_arr2("geom_p0", "double", t["geom_p0"], 3))
     L.append(_arr2("geom_p1", "double", t["geom_p1"], 3))
     L.append(_arr1("geom_r", "double", t["geom_r"]))
+    L.append(_arr1("cgeom_link", "int", t["cgeom_link"]))
+    L.append(_arr2("cgeom_p0", "double", t["cgeom_p0"], 3))
+    L.append(_arr2("cgeom_p1", "double", t["cgeom_p1"], 3))
+    L.append(_arr1("cgeom_r", "double", t["cgeom_r"]))
+    L.append(_arr1("cgeom_mu", "double", t["cgeom_mu"]))
     L.append("};")
     return "\n".join(L)
 
@@ -342,13 +366,13 @@ def emit_struct(t: Dict) -> str:
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
              "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
-             "double_pendulum_mujoco": 14}
+             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
            "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun",
            "hopper_mujoco": "HopperMuJoCo", "walker2d_mujoco": "Walker2DMuJoCo",
            "halfcheetah_mujoco": "HalfCheetahMuJoCo", "ant_mujoco": "AntMuJoCo", "humanoid_mujoco": "HumanoidMuJoCo",
-           "double_pendulum_mujoco": "DoublePendulumMuJoCo"}
+           "double_pendulum_mujoco": "DoublePendulumMuJoCo", "humanoid_flagrun_harder": "HumanoidFlagrunHarder"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -30,21 +30,47 @@
 #define PBG_OBS_CLIP 5.0                // robot_locomotors.py:64 np.clip(..., -5, +5)
 #define PBG_JOINT_AT_LIMIT 0.99f        // robot_locomotors.py:36 (float32 compare)
 
+// HumanoidFlagrunHarder's attacking cube (robot_locomotors.py:230-302; gym_utils.py:9-15
+// get_cube: pybullet_data cube_small.urdf -- envs/assets/things/cube_small.urdf holds the same
+// file: box .05, lateral_friction 1.0 (codegen.py CUBE_FRICTION -> cgeom_mu, cube_floor_mu) -- loaded at (-1.5, 0, 0.05), changeDynamics(mass=1.2)).
+// [EXT] changeDynamics(mass) recomputes the base inertia from the collision shape
+// (btBoxShape::calculateLocalInertia: m/12 (ly^2 + lz^2), isotropic for a cube).
+#define PBG_CUBE_HALF 0.025
+#define PBG_CUBE_MASS 1.2
+#define PBG_CUBE_INERTIA (PBG_CUBE_MASS * (2.0 * PBG_CUBE_HALF) * (2.0 * PBG_CUBE_HALF) / 6.0)
+#define PBG_CUBE_X0 (-1.5)              // robot_locomotors.py:242,244
+#define PBG_CUBE_Y0 0.0
+#define PBG_CUBE_Z0 0.05
+#define PBG_CUBE_WORDS 13               // pos 3 | quat 4 | lin vel 3 | ang vel 3
+// alive_bonus (robot_locomotors.py:250-273): a launch every 30 frames after frame 100 while the
+// robot is up, from 4 m away at U(20, 30) m/s towards its predicted position; U(+-1) jitter
+#define PBG_HARDER_LAUNCH_EVERY 30
+#define PBG_HARDER_LAUNCH_AFTER 100
+#define PBG_HARDER_GROUND_Z 0.8         // z < 0.8: on the ground (:267, :291), potential_leak clip (:277)
+#define PBG_HARDER_GROUND_FRAMES 170    // :273 (alive -1 once the counter reaches it)
+#define PBG_HARDER_FROM_DIST 4.0        // :255
+
 // Per-env physical state record (float64 at the C-ABI, float32 inside the kernel):
 //   [0..2] base COM position  [3..6] base quaternion (x,y,z,w)
 //   [7..9] base COM linear velocity (world)  [10..12] base angular velocity (world)
 //   [13 .. 13+NJ)  joint positions q   [13+NJ .. 13+2NJ)  joint velocities qd
+//   HumanoidFlagrunHarder only: [13+2NJ .. 13+2NJ+13) the cube (PBG_CUBE_WORDS, same layout
+//   as the base words)
 // Fixed-base robots keep the 13 base words at their load values.
 #define PBG_BASE_WORDS 13
+#define PBG_STATE_WORDS(NJ, harder) (PBG_BASE_WORDS + 2 * (NJ) + ((harder) ? PBG_CUBE_WORDS : 0))
 
 // Per-env bookkeeping record (float64):
 //   [0] potential  [1] initial_z  [2] elapsed steps  [3] floor-in-parts flag
 //   [4 .. 4+NF) feet_contact (as written into the observation)
-//   HumanoidFlagrun only: [4+NF .. 4+NF+4) walk target x, y, flag_timeout, flag draws so far
+//   HumanoidFlagrun(Harder): [4+NF .. 4+NF+4) walk target x, y, flag_timeout, flag draws so far
+//   HumanoidFlagrunHarder: [8+NF .. 8+NF+5) frame, on_ground_frame_counter,
+//     crawl_start_potential (NaN = None), crawl_ignored_potential, cube launches so far
 //   last word: episodes started so far (the Philox counter of the next reset's noise), so a
 //   checkpoint restored into a fresh handle continues the same reset stream
 #define PBG_AUX_WORDS 4
-#define PBG_AUX_RECORD_WORDS(NF, flagrun) (PBG_AUX_WORDS + (NF) + ((flagrun) ? 4 : 0) + 1)
+#define PBG_AUX_RECORD_WORDS(NF, flagrun, harder) \
+  (PBG_AUX_WORDS + (NF) + ((flagrun) ? 4 : 0) + ((harder) ? 5 : 0) + 1)
 
 // Contact-set signature (parity tests): the term of active collision candidate `id` (floor
 // slots 0..NS-1, self-collision pairs NS + p) in sub-step `sub` is murmur3's fmix32 of

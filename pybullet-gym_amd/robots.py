@@ -56,6 +56,7 @@ class RobotSpec:
     self_collision: bool = True
     reset_offset: float = 0.0                                    # swingup hinge 3.1415 + u
     flagrun: bool = False                                        # HumanoidFlagrun walk target
+    harder: bool = False                                         # HumanoidFlagrunHarder attacking cube
     power_cost: float = 0.0                                      # MuJoCo planar: coef of sum(a^2)
     qvel_clip: float = 0.0                                       # MuJoCo planar: obs qvel clip (0: none)
 
@@ -156,6 +157,18 @@ _add(RobotSpec("HumanoidMuJoCoEnv-v0", "humanoid_mujoco", "humanoid_symmetric.xm
                power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8))
 
 ENV_IDS = {s.env_id: s for s in SPECS.values()}
+
+
+# HumanoidFlagrunHarder: robot_locomotors.py:230-302 (the attacking cube of gym_utils.py:9-15,
+# alive_bonus / potential_leak / crawl-disabling calc_potential), gym_locomotion_envs.py:167-178,
+# envs/__init__.py:93-97.  The env's `self.electricity_cost /= 4` (:172) runs before
+# HumanoidBulletEnv.__init__ sets electricity_cost = 4.25 * -2.0 (:150), which overwrites it: the
+# Humanoid's costs stand (pinned by tests/golden/pack_humanoid_flagrun_harder.npz).
+_add(RobotSpec("HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder", "humanoid_symmetric.xml", "torso",
+               action_dim=17, obs_dim=44, kind=KIND_WALKER, power=0.41, foot_list=["right_foot", "left_foot"],
+               alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
+               power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8,
+               electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1, flagrun=True, harder=True))
 
 
 def spec_for(name: str) -> RobotSpec:

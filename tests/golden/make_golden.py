@@ -53,7 +53,9 @@ ROBOTS = {
     "ant_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "AntMuJoCoEnv"),
     "humanoid_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HumanoidMuJoCoEnv"),
     "double_pendulum_mujoco": ("pybulletgym.envs.mujoco.gym_pendulum_envs", "InvertedDoublePendulumMuJoCoEnv"),
+    "humanoid_flagrun_harder": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidFlagrunHarderBulletEnv"),
 }
+CUBE_UID = 6
 
 
 # ----------------------------------------------------------------------------- stubs
@@ -165,6 +167,9 @@ class FakeClient:
         self.qd = np.zeros(self.L)
         self.saved = None
         self.target_hook = None
+        self.z_hook = None       # HumanoidFlagrunHarder: scripted torso height (up / crawling)
+        self.cube_pose = ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+        self.cube_events = []    # (kind, value) of every cube reset call
         self.new_state(initial=True)
 
     # --- state script
@@ -173,6 +178,8 @@ class FakeClient:
         big = rng.random() < 0.1
         self.base_pos = (float(rng.uniform(-3, 3) if not big else rng.choice([-2000.0, 1500.0, 999.5])),
                          float(rng.uniform(-3, 3)), float(rng.uniform(0.05, 1.6)))
+        if self.z_hook is not None:
+            self.base_pos = (self.base_pos[0], self.base_pos[1], float(self.z_hook(rng)))
         self.base_orn = rand_quat(rng, 0.9 if rng.random() < 0.3 else 0.2)
         vs = 30.0 if rng.random() < 0.1 else 2.0
         self.base_lin = tuple(float(v) for v in rng.normal(0, vs, 3))
@@ -210,8 +217,21 @@ class FakeClient:
     def setJointMotorControl2(self, *a, **k): pass
     def loadSDF(self, path): return (self.floor_uid,)
     def loadMJCF(self, path, flags=0): return (self.robot_uid,)
-    def loadURDF(self, path, pos=None, *a, **k): return 5  # HumanoidFlagrun's flag sphere (no collision)
-    def resetBasePositionAndOrientation(self, *a, **k): pass
+    def loadURDF(self, path, pos=None, *a, **k):
+        if "cube" in str(path):  # HumanoidFlagrunHarder's attacking cube (gym_utils.get_cube)
+            self.cube_pose = (tuple(float(v) for v in pos), (0.0, 0.0, 0.0, 1.0))
+            return CUBE_UID
+        return 5  # HumanoidFlagrun's flag sphere (no collision)
+
+    def resetBasePositionAndOrientation(self, uid, pos, orn):
+        if uid == CUBE_UID:
+            self.cube_pose = (tuple(float(v) for v in pos), tuple(float(v) for v in orn))
+            self.cube_events.append(("pose", self.cube_pose[0]))
+
+    def resetBaseVelocity(self, uid, linearVelocity=(0, 0, 0), angularVelocity=(0, 0, 0)):
+        if uid == CUBE_UID:
+            self.cube_events.append(("vel", tuple(float(v) for v in linearVelocity),
+                                     tuple(float(v) for v in angularVelocity)))
     def saveState(self): return 3
     def restoreState(self, sid): self.q[:] = 0.0; self.qd[:] = 0.0
     def stepSimulation(self): self.new_state()
@@ -220,6 +240,8 @@ class FakeClient:
         return self.L if uid == self.robot_uid else 0
 
     def getBodyInfo(self, uid):
+        if uid == CUBE_UID:
+            return (b"baseLink", b"cube.urdf")
         return (b"floor", b"floor_obj") if uid == self.floor_uid else (b"base", self.t["key"].encode())
 
     def getJointInfo(self, uid, j):
@@ -238,6 +260,8 @@ class FakeClient:
     def getBasePositionAndOrientation(self, uid):
         if uid == self.floor_uid:
             return ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+        if uid == CUBE_UID:
+            return self.cube_pose
         return (self.base_pos, self.base_orn)
 
     def getBaseVelocity(self, uid):
@@ -296,7 +320,7 @@ def generate(key, episodes=3, steps=40, seed=1234):
     rec = {k: [] for k in ("kind", "part_xyz", "n_parts", "body_quat", "body_pos", "body_vel", "jq", "jqd",
                            "feet_prev", "feet_new", "act", "potential_old", "initial_z_in", "obs", "reward",
                            "done", "potential", "feet_out", "initial_z_out", "rewards", "flag_in", "flag_out",
-                           "body_avel")}
+                           "body_avel", "harder_in", "harder_out")}
     part_names = []
     captured = {}
     calc_cls = type(robot)
@@ -329,6 +353,10 @@ def generate(key, episodes=3, steps=40, seed=1234):
             if t.get("flagrun"):  # walk target and flag_timeout before HumanoidFlagrun.calc_state
                 captured["flag_before"] = (float(self.walk_target_x), float(self.walk_target_y),
                                            float(self.flag_timeout))
+            if t.get("harder"):  # HumanoidFlagrunHarder bookkeeping before this calc_state
+                cs = self.crawl_start_potential
+                captured["harder_before"] = [float(self.frame), float(self.on_ground_frame_counter),
+                                             np.nan if cs is None else float(cs), float(self.crawl_ignored_potential)]
         else:
             js = [self.j1, self.j2, self.slider] if hasattr(self, "j2") else [self.j1, self.slider]
             captured["jq"] = np.array([j.get_state()[0] for j in js])
@@ -338,6 +366,30 @@ def generate(key, episodes=3, steps=40, seed=1234):
         return orig_calc(self)
 
     calc_cls.calc_state = spy_calc_state
+    orig_alive = calc_cls.alive_bonus
+    if t.get("harder"):
+        def spy_alive_bonus(self, z, pitch):
+            # the launch draws of np_random.uniform inside alive_bonus, and the cube resets it makes
+            rs = self.np_random
+            draws = []
+
+            class Recorder:  # delegates to the env's RandomState, recording uniform() values
+                def uniform(self, *a, **k):
+                    v = rs.uniform(*a, **k)
+                    draws.extend(np.atleast_1d(v).astype(np.float64).tolist())
+                    return v
+
+                def __getattr__(self, name):
+                    return getattr(rs, name)
+            self.np_random = Recorder()
+            fake.cube_events.clear()
+            try:
+                return orig_alive(self, z, pitch)
+            finally:
+                self.np_random = rs
+                captured["launch_draws"] = draws
+                captured["launch_events"] = list(fake.cube_events)
+        calc_cls.alive_bonus = spy_alive_bonus
     if t["kind"] == 2:
         calc_cls.calc_potential = spy_calc_potential
     NPMAX = t["NP"] + 1
@@ -370,6 +422,18 @@ def generate(key, episodes=3, steps=40, seed=1234):
                 # the draw a reposition took (NaN: none happened during this calc_state)
                 rec["flag_in"].append([bx, by, bt, after[0] if moved else np.nan, after[1] if moved else np.nan])
                 rec["flag_out"].append(list(after))
+            if t.get("harder"):
+                dr = captured.pop("launch_draws", []) if kind == 1 else []
+                ev = captured.pop("launch_events", []) if kind == 1 else []
+                assert len(dr) in (0, 5), dr
+                rec["harder_in"].append(captured["harder_before"] + (dr if dr else [np.nan] * 5))
+                cs = robot.crawl_start_potential
+                pos = [e[1] for e in ev if e[0] == "pose"]
+                vel = [e[1] for e in ev if e[0] == "vel"]
+                assert len(pos) == len(vel) == (1 if dr else 0), ev
+                rec["harder_out"].append([float(robot.frame), float(robot.on_ground_frame_counter),
+                                          np.nan if cs is None else float(cs), float(robot.crawl_ignored_potential),
+                                          1.0 if dr else 0.0] + (list(pos[0]) + list(vel[0]) if dr else [np.nan] * 6))
             rec["initial_z_out"].append(float(robot.initial_z))
             part_names.append(captured["part_names"])
         elif t["kind"] == 2:
@@ -388,7 +452,15 @@ def generate(key, episodes=3, steps=40, seed=1234):
         rec["rewards"].append(rr)
 
     arng = np.random.default_rng(seed + 1)
+    if t.get("harder"):
+        # up (no crawl, cube launches every 30 frames after frame 100) most of the time, on the
+        # ground in bursts; the last episode stays down until the 170-frame counter ends it
+        state = {"ep": 0}
+        fake.z_hook = lambda r: (r.uniform(0.05, 0.79) if state["ep"] == episodes - 1 or r.random() < 0.25
+                                 else r.uniform(0.81, 1.5))
     for ep in range(episodes):
+        if t.get("harder"):
+            state["ep"] = ep
         obs = env.reset()
         push(0, None, np.nan, obs, 0.0, False)
         for s in range(steps):
@@ -401,6 +473,7 @@ def generate(key, episodes=3, steps=40, seed=1234):
             push(1, a, pot_old, obs, float(r), done)
     calc_cls.calc_state = orig_calc
     calc_cls.calc_potential = orig_pot
+    calc_cls.alive_bonus = orig_alive
     out = {k: np.array(v) for k, v in rec.items() if len(v)}
     out["part_names"] = np.array(["|".join(p) for p in part_names]) if part_names else np.array([])
     out["numpy_version"] = np.array(np.__version__)
@@ -412,7 +485,12 @@ def main():
     sys.path.insert(0, REF)
     for key in (sys.argv[1:] or ROBOTS):
         # flagrun: long enough for flag_timeout (150 calc_states) to run out
-        data = generate(key, episodes=2, steps=170) if key == "humanoid_flagrun" else generate(key)
+        if key == "humanoid_flagrun":
+            data = generate(key, episodes=2, steps=170)
+        elif key == "humanoid_flagrun_harder":  # launches from frame 120; the 170-frame ground limit
+            data = generate(key, episodes=3, steps=200)
+        else:
+            data = generate(key)
         path = os.path.join(HERE, f"pack_{key}.npz")
         np.savez_compressed(path, **data)
         print(key, "calls", len(data["kind"]), "->", os.path.relpath(path, REPO))

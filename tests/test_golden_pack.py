@@ -9,7 +9,7 @@ import oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d", "humanoid_flagrun", "ant_mujoco",
-           "humanoid_mujoco"]
+           "humanoid_mujoco", "humanoid_flagrun_harder"]
 
 
 def load(key):
@@ -39,10 +39,17 @@ def test_oracle_pack_bit_exact(key):
                           g["feet_new"][i] if step else None, g["act"][i] if step else None,
                           g["potential_old"][i], g["initial_z_in"][i],
                           flag=g["flag_in"][i] if "flag_in" in g.files else None,
-                          body_avel=g["body_avel"][i] if "body_avel" in g.files else None)
+                          body_avel=g["body_avel"][i] if "body_avel" in g.files else None,
+                          harder=g["harder_in"][i] if "harder_in" in g.files else None)
         ref_obs = g["obs"][i].astype(np.float32)
         if "flag_out" in g.files:  # HumanoidFlagrun: target and flag_timeout after calc_state
             np.testing.assert_array_equal(out["flag_out"], g["flag_out"][i], err_msg=f"call {i}")
+        if "harder_out" in g.files:  # HumanoidFlagrunHarder: frame, counters, crawl state, cube launch
+            ho, ref = out["harder_out"], g["harder_out"][i]
+            np.testing.assert_array_equal(ho[[0, 1, 4]], ref[[0, 1, 4]], err_msg=f"call {i}")
+            np.testing.assert_allclose(ho[[2, 3]], ref[[2, 3]], rtol=1e-13, atol=1e-9, equal_nan=True, err_msg=f"call {i}")
+            # cube position / velocity of a launch: float64, np.linalg.norm's BLAS dot ordering
+            np.testing.assert_allclose(ho[5:], ref[5:], rtol=1e-13, atol=1e-12, equal_nan=True, err_msg=f"call {i}")
         assert out["obs"].dtype == np.float32
         np.testing.assert_array_equal(out["obs"].view(np.uint32), ref_obs.view(np.uint32), err_msg=f"call {i}")
         assert out["potential"] == pytest.approx(g["potential"][i], abs=1e-9, rel=0)
