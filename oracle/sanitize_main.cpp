@@ -29,7 +29,7 @@ int main(int argc, char** argv) {
     return (double)(x >> 11) * (2.0 / 9007199254740992.0) - 1.0;
   };
   const double variants[][2] = {{-1, 0}, {7, 0.85}, {6, 1}, {6, 2}, {4, 1}, {5, 1}, {11, 1}};
-  for (int robot = 0; robot < 15; robot++) {
+  for (int robot = 0; robot < 16; robot++) {
     int info[16];
     if (pbg_oracle_info(robot, info) != 0) return 2;
     const int NA = info[3], NR = info[5], OBS = info[10], SD = info[11], AD = info[12];
@@ -51,6 +51,8 @@ int main(int argc, char** argv) {
       std::vector<uint32_t> sig(n);
       for (auto& v : q) v = 0.1 * rnd();
       if (pbg_oracle_reset(robot, n, st.data(), aux.data(), q.data(), obs.data()) != 0) return 3;
+      if (robot == 15)  // HumanoidFlagrunHarder: frame 120, so the first step launches the cube
+        for (int e = 0; e < n; e++) aux[(size_t)e * AD + 8 + info[6]] = 120.0;
       for (int t = 0; t < steps; t++) {
         for (auto& v : act) v = (float)rnd();
         if (t == steps / 2) act[0] = NAN;  // non-finite action path

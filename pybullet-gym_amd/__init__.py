@@ -1,6 +1,7 @@
 """pybulletgym_amd: MI355X-native batched stepper for the roboschool locomotion envs of
 josiahls/pybullet-gym (InvertedPendulum, InvertedPendulumSwingup, InvertedDoublePendulum,
-Hopper, HalfCheetah, Ant, Humanoid, HumanoidFlagrun, Walker2D ``*PyBulletEnv-v0``).  Import as ``import pybulletgym_amd``.
+Hopper, HalfCheetah, Ant, Humanoid, HumanoidFlagrun, HumanoidFlagrunHarder, Walker2D
+``*PyBulletEnv-v0``, and the MuJoCo-observation variants).  Import as ``import pybulletgym_amd``.
 
     from pybulletgym_amd import VecEnv, make
     envs = VecEnv("AntPyBulletEnv-v0", 16384)      # device-resident batch, one launch per step
@@ -10,7 +11,8 @@ ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheeta
            "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
            "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
            "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0",
-           "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0")
+           "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0",
+           "HumanoidFlagrunHarderPyBulletEnv-v0")
 
 
 def __getattr__(name):

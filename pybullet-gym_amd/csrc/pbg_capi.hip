@@ -27,7 +27,7 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[15][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[16][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
@@ -41,8 +41,9 @@ int env_robot_id(const char* env_id) {
                                   {"HalfCheetahMuJoCoEnv-v0", "halfcheetah_mujoco"},
                                   {"AntMuJoCoEnv-v0", "ant_mujoco"},
                                   {"HumanoidMuJoCoEnv-v0", "humanoid_mujoco"},
-                                  {"InvertedDoublePendulumMuJoCoEnv-v0", "double_pendulum_mujoco"}};
-  for (int i = 0; i < 15; i++)
+                                  {"InvertedDoublePendulumMuJoCoEnv-v0", "double_pendulum_mujoco"},
+                                  {"HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder"}};
+  for (int i = 0; i < 16; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -103,12 +104,13 @@ int check_sim_params(const pbg_sim_params_t& p) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT, defaults_of<pbg_models::NAME>()}
 
 const Ops* ops(int rid) {
-  static const Ops table[15] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+  static const Ops table[16] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
                                 PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5), PBG_OPS(PendulumSwingup, 6),
                                 PBG_OPS(DoublePendulum, 7), PBG_OPS(HumanoidFlagrun, 8), PBG_OPS(HopperMuJoCo, 9),
                                 PBG_OPS(Walker2DMuJoCo, 10), PBG_OPS(HalfCheetahMuJoCo, 11), PBG_OPS(AntMuJoCo, 12),
-                                PBG_OPS(HumanoidMuJoCo, 13), PBG_OPS(DoublePendulumMuJoCo, 14)};
-  return (rid >= 0 && rid < 15) ? &table[rid] : nullptr;
+                                PBG_OPS(HumanoidMuJoCo, 13), PBG_OPS(DoublePendulumMuJoCo, 14),
+                                PBG_OPS(HumanoidFlagrunHarder, 15)};
+  return (rid >= 0 && rid < 16) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {
@@ -220,6 +222,8 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   e |= hip_check(hipMalloc(&B.episode, sizeof(uint32_t) * n), "hipMalloc episode");
   e |= hip_check(hipMalloc(&B.tgt, sizeof(double) * 2 * n), "hipMalloc walk target");
   e |= hip_check(hipMalloc(&B.ftm, sizeof(int32_t) * 2 * n), "hipMalloc flag counters");
+  e |= hip_check(hipMalloc(&B.hkd, sizeof(double) * 2 * n), "hipMalloc crawl potentials");
+  e |= hip_check(hipMalloc(&B.hki, sizeof(int32_t) * 3 * n), "hipMalloc cube counters");
   e |= hip_check(hipMalloc(&h->scratch, sizeof(float) * n * h->geo.scratch_words_per_env), "hipMalloc scratch");
   if (!e) {
     e |= hip_check(hipMemset(B.st, 0, sizeof(float) * n * h->info.state_words), "hipMemset");
@@ -230,6 +234,8 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
     e |= hip_check(hipMemset(B.episode, 0, sizeof(uint32_t) * n), "hipMemset");
     e |= hip_check(hipMemset(B.tgt, 0, sizeof(double) * 2 * n), "hipMemset");
     e |= hip_check(hipMemset(B.ftm, 0, sizeof(int32_t) * 2 * n), "hipMemset");
+    e |= hip_check(hipMemset(B.hkd, 0, sizeof(double) * 2 * n), "hipMemset");
+    e |= hip_check(hipMemset(B.hki, 0, sizeof(int32_t) * 3 * n), "hipMemset");
     e |= hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   }
   if (e) {
@@ -243,7 +249,8 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
 void pbg_destroy(pbg_handle* h) {
   if (!h) return;
   DeviceGuard dg(h->device);
-  void* bufs[] = {h->B.st, h->B.pot, h->B.z0, h->B.elapsed, h->B.flags, h->B.episode, h->B.tgt, h->B.ftm, h->scratch};
+  void* bufs[] = {h->B.st, h->B.pot, h->B.z0, h->B.elapsed, h->B.flags, h->B.episode, h->B.tgt, h->B.ftm,
+                  h->B.hkd, h->B.hki, h->scratch};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   delete h;

@@ -49,4 +49,5 @@ PBG_DECLARE_ROBOT(HalfCheetahMuJoCo)
 PBG_DECLARE_ROBOT(AntMuJoCo)
 PBG_DECLARE_ROBOT(HumanoidMuJoCo)
 PBG_DECLARE_ROBOT(DoublePendulumMuJoCo)
+PBG_DECLARE_ROBOT(HumanoidFlagrunHarder)
 }  // namespace pbg

@@ -81,7 +81,7 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
 // + 3 rows), contacts past the capacity spill to the device workspace.
 template <class RR>
 static int plan_gang(int n_envs, int cus, Geometry* g) {
-  if constexpr (RR::kind == 0 || RR::kind >= 2) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
     using G = Gang<RR, 16>;
     constexpr int EPB = PBG_GANG_BLOCK / 16;  // envs per workgroup
     const int wgs = (n_envs + EPB - 1) / EPB;
@@ -114,7 +114,7 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
 }
 template <class RR>
 static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
-  if constexpr (RR::kind == 0 || RR::kind >= 2) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
     if (g.team != 16) return false;
     const dim3 grid(blocks(B.n, PBG_GANG_BLOCK / 16)), blk(PBG_GANG_BLOCK);
     if (g.gang_dist)
@@ -129,10 +129,11 @@ static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, cons
 }
 
 // mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers);
-// 2 = gang for every walker (parity tests of the gang kernel on Ant)
+// 2 = gang for every walker (parity tests of the gang kernel on Ant).  HumanoidFlagrunHarder
+// (a second free body per env) runs on the lane kernel only.
 int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
-  if (R::kind != 1 && mode >= 1) return plan_gang<R>(n_envs, cus, g);
+  if (R::kind != 1 && !R::harder && mode >= 1) return plan_gang<R>(n_envs, cus, g);
   g->team = 1;
   g->env_words = 0;
   const int per_cu = (n_envs + cus - 1) / cus;

@@ -21,6 +21,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "models_gen.h"
 #include "pbg_math.h"
 #include "pbg_records.h"
@@ -77,8 +79,11 @@ constexpr bool has_springs() {
 template <class R>
 struct Dims {
   static constexpr int NL = R::NL, NJ = R::NJ, NB = R::NL + 1, NDOF = R::NDOF;
-  static constexpr int SD = PBG_BASE_WORDS + 2 * R::NJ;
-  static constexpr int NC = R::NS + R::NPAIR;  // contact capacity
+  static constexpr int SD = PBG_STATE_WORDS(R::NJ, R::harder);
+  // contact capacity: floor slots, self pairs (+ HumanoidFlagrunHarder's cube: 8 corners, NCG geoms)
+  static constexpr int NC = R::NS + R::NPAIR + (R::harder ? 8 + R::NCG : 0);
+  // constraint-row length: the robot's generalized velocity (+ the cube's 6 in u-space)
+  static constexpr int NY = R::NDOF + (R::harder ? 6 : 0);
   static constexpr int count_limited() {
     int c = 0;
     for (int d = 0; d < R::NJ; d++) c += R::dof_limited[d];
@@ -231,10 +236,16 @@ struct Dims {
 };
 
 // ------------------------------------------------------------------ state record in registers
+// HumanoidFlagrunHarder's cube: a second free body (words after the robot's, sim_params.h)
+struct CubeState {
+  float p[3], q[4], v[3], w[3];
+};
+struct NoCube {};
 template <class R>
 struct State {
   float bp[3], bq[4], bv[3], bw[3];
   float q[R::NJ > 0 ? R::NJ : 1], qd[R::NJ > 0 ? R::NJ : 1];
+  std::conditional_t<(R::harder != 0), CubeState, NoCube> cube;
 };
 
 template <class R>
@@ -251,6 +262,17 @@ PBG_DEV void load_state(State<R>& s, const float* __restrict__ st, int n, int e)
   for (int d = 0; d < R::NJ; d++) s.q[d] = st[(size_t)(PBG_BASE_WORDS + d) * n + e];
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) s.qd[d] = st[(size_t)(PBG_BASE_WORDS + R::NJ + d) * n + e];
+  if constexpr (R::harder) {
+    constexpr int c0 = PBG_BASE_WORDS + 2 * R::NJ;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      s.cube.p[i] = st[(size_t)(c0 + i) * n + e];
+      s.cube.v[i] = st[(size_t)(c0 + 7 + i) * n + e];
+      s.cube.w[i] = st[(size_t)(c0 + 10 + i) * n + e];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) s.cube.q[i] = st[(size_t)(c0 + 3 + i) * n + e];
+  }
 }
 template <class R>
 PBG_DEV void store_state(const State<R>& s, float* __restrict__ st, int n, int e) {
@@ -266,6 +288,17 @@ PBG_DEV void store_state(const State<R>& s, float* __restrict__ st, int n, int e
   for (int d = 0; d < R::NJ; d++) st[(size_t)(PBG_BASE_WORDS + d) * n + e] = s.q[d];
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) st[(size_t)(PBG_BASE_WORDS + R::NJ + d) * n + e] = s.qd[d];
+  if constexpr (R::harder) {
+    constexpr int c0 = PBG_BASE_WORDS + 2 * R::NJ;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      st[(size_t)(c0 + i) * n + e] = s.cube.p[i];
+      st[(size_t)(c0 + 7 + i) * n + e] = s.cube.v[i];
+      st[(size_t)(c0 + 10 + i) * n + e] = s.cube.w[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) st[(size_t)(c0 + 3 + i) * n + e] = s.cube.q[i];
+  }
 }
 
 // Stores of a value replicated over T cooperating lanes (gang / quad kernels), dealt over
@@ -299,6 +332,12 @@ PBG_DEV void snapshot_state(State<R>& s) {
   for (int i = 0; i < 3; i++) { s.bv[i] = 0.f; s.bw[i] = 0.f; }
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) { s.q[d] = 0.f; s.qd[d] = 0.f; }
+  if constexpr (R::harder) {  // restoreState + resetBasePositionAndOrientation(cube, (-1.5, 0, 0.05)) (:241)
+    s.cube.p[0] = (float)PBG_CUBE_X0; s.cube.p[1] = (float)PBG_CUBE_Y0; s.cube.p[2] = (float)PBG_CUBE_Z0;
+    s.cube.q[0] = 0.f; s.cube.q[1] = 0.f; s.cube.q[2] = 0.f; s.cube.q[3] = 1.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) { s.cube.v[i] = 0.f; s.cube.w[i] = 0.f; }
+  }
 }
 
 // ------------------------------------------------------------------ kinematics
@@ -374,7 +413,7 @@ typedef __attribute__((address_space(3))) float lds_float;  // explicit LDS poin
 template <class R, int LS = 64>
 struct Rows {
   using D = Dims<R>;
-  static constexpr int N = R::NDOF, W = N + 3;  // contact row: y | meff | target | lambda
+  static constexpr int N = D::NY, W = N + 3;  // contact row: y | meff | target | lambda (N: robot [+ cube])
   static constexpr int MR = 3 * D::NC > 0 ? 3 * D::NC : 1;
   static constexpr int NC = D::NC > 0 ? D::NC : 1;
   static constexpr int WORDS = MR * W;  // global workspace words per env
@@ -718,6 +757,77 @@ PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, 
   dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
 }
 
+// exponential-map quaternion update of a free body (the floating base, the cube) with its
+// world angular velocity  [EXT] btMultiBody pQuatUpdateFun
+PBG_DEV void free_body_quat(float* q, f3 wv, const SimP& P) {
+  const float dt = P.dt;
+  float ang = norm3(wv);
+  if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
+  float sh, dw;
+  sincos_fast(0.5f * ang * dt, &sh, &dw);
+  f3 ax;
+  if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
+  else ax = (sh / ang) * wv;
+  const float x = q[0], y = q[1], z = q[2], ww = q[3];
+  const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+  const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+  const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+  const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+  const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+  q[0] = nx * inv; q[1] = ny * inv; q[2] = nz * inv; q[3] = nw * inv;
+}
+
+// HumanoidFlagrunHarder's cube (a free body with isotropic inertia, block-diagonal to the robot):
+// its Cholesky factor is diag(sqrt m x3, sqrt I x3), so u_c = L_c^T nu_c and y_c = L_c^-1 J_c are
+// plain scalings.  Unconstrained velocity: the free-body bias of the oracle's mass_and_bias
+// (f = m (-g) + m (k1 + k2 |v|) v, tq = (k1 + k2 |w|) I w; the gyroscopic term of an isotropic
+// body vanishes), nu_c = clamp(nu_c - dt M_c^-1 (f, tq)), then u_c.
+struct CubeK {
+  static PBG_DEV float sm() { return sqrtf((float)PBG_CUBE_MASS); }
+  static PBG_DEV float sI() { return sqrtf((float)PBG_CUBE_INERTIA); }
+};
+template <class R>
+PBG_DEV void cube_unconstrained(const State<R>& s, float* uc, const SimP& P) {
+  if constexpr (R::harder) {
+    const f3 v = mk3(s.cube.v[0], s.cube.v[1], s.cube.v[2]), w = mk3(s.cube.w[0], s.cube.w[1], s.cube.w[2]);
+    const float kl = (float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v);
+    const float ka = (float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w);
+    const float vmax = (float)PBG_MAX_COORD_VELOCITY;
+    const float vv[3] = {v.x, v.y, v.z}, wv[3] = {w.x, w.y, w.z};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const float acc = -(kl * vv[i]) - (i == 2 ? P.gravity : 0.f);
+      uc[i] = CubeK::sm() * clampf(vv[i] + P.dt * acc, -vmax, vmax);
+      uc[3 + i] = CubeK::sI() * clampf(wv[i] + P.dt * (-(ka * wv[i])), -vmax, vmax);
+    }
+  } else {
+    (void)s; (void)uc; (void)P;
+  }
+}
+// nu_c = L_c^-T u_c, clamp, semi-implicit Euler
+template <class R>
+PBG_DEV void cube_integrate(State<R>& s, const float* uc, const SimP& P) {
+  if constexpr (R::harder) {
+    const float vmax = (float)PBG_MAX_COORD_VELOCITY;
+    const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      s.cube.v[i] = clampf(uc[i] * rm, -vmax, vmax);
+      s.cube.w[i] = clampf(uc[3 + i] * rI, -vmax, vmax);
+      s.cube.p[i] += P.dt * s.cube.v[i];
+    }
+    free_body_quat(s.cube.q, mk3(s.cube.w[0], s.cube.w[1], s.cube.w[2]), P);
+  } else {
+    (void)s; (void)uc; (void)P;
+  }
+}
+// signed distance of a cube-local point to the box of half extent h (oracle box_sd)
+PBG_DEV float box_sd(f3 p, float h) {
+  const float qx = fabsf(p.x) - h, qy = fabsf(p.y) - h, qz = fabsf(p.z) - h;
+  const float ox = fmaxf(qx, 0.f), oy = fmaxf(qy, 0.f), oz = fmaxf(qz, 0.f);
+  return sqrtf(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.f);
+}
+
 // nu = L^-T u, clamp, semi-implicit Euler (exponential-map base rotation).  nu: scratch.
 template <class R>
 PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float* u, float* nu, const SimP& P) {
@@ -747,23 +857,145 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
       s.bw[i] = nu[NJ + 3 + i];
       s.bp[i] += dt * s.bv[i];
     }
-    // exponential-map quaternion update with the world angular velocity  [EXT]
-    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
-    float ang = norm3(wv);
-    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
-    float sh, dw;
-    sincos_fast(0.5f * ang * dt, &sh, &dw);
-    f3 ax;
-    if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
-    else ax = (sh / ang) * wv;
-    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
-    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
-    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
-    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
-    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
-    s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
+    free_body_quat(s.bq, mk3(s.bw[0], s.bw[1], s.bw[2]), P);
   }
+}
+
+// HumanoidFlagrunHarder's cube against the floor and the robot (oracle detect_cube_contacts):
+// candidates NS + NPAIR + corner (8), then NS + NPAIR + 8 + geom; a corner within the contact
+// threshold of the floor is a point (normal +z, cube = body A), a robot geom against the box
+// takes the minimiser of the box's signed distance along its segment (golden section,
+// PBG_CUBE_GS_ITERS rounds; robot link = A, cube = B).  Rows: the robot part y_h = L^-1 J_h as
+// for the self pairs, the cube part y_c = +-(n / sqrt m, (r x n) / sqrt I).  Returns nc.
+#define PBG_CUBE_GS_ITERS 24
+template <class R, int LS>
+PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const f3* sw, const f3* sv, f3 O, const float* L,
+                          const float* Ld, const Rows<R, LS>& rw, uint32_t sub, uint32_t& csig, const SimP& P, int nc) {
+  using D = Dims<R>;
+  constexpr int N = R::NDOF, NY = D::NY;
+  const float h = (float)PBG_CUBE_HALF, thr = (float)PBG_CONTACT_THRESHOLD;
+  const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+  const m3 Rc = quat_to_m3(s.cube.q[0], s.cube.q[1], s.cube.q[2], s.cube.q[3]);
+  const f3 xc = mk3(s.cube.p[0], s.cube.p[1], s.cube.p[2]);
+  // --- corners vs floor
+  static_for<0, 8>([&](auto c_c) {
+    constexpr int c = decltype(c_c)::value;
+    const f3 lc = mk3((c & 1) ? h : -h, (c & 2) ? h : -h, (c & 4) ? h : -h);
+    const f3 p = xc + mul(Rc, lc);
+    if (!(p.z < thr)) return;
+    csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + c));
+    const f3 rc = p - xc;
+#pragma unroll
+    for (int dir = 0; dir < 3; dir++) {
+      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 mm = cross3(rc, nd);
+      float y[NY];
+#pragma unroll
+      for (int i = 0; i < N; i++) y[i] = 0.f;
+      y[N] = nd.x * rm; y[N + 1] = nd.y * rm; y[N + 2] = nd.z * rm;
+      y[N + 3] = mm.x * rI; y[N + 4] = mm.y * rI; y[N + 5] = mm.z * rI;
+      float D2 = 0.f;
+#pragma unroll
+      for (int i = N; i < NY; i++) D2 += y[i] * y[i];
+      rw.put(3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f, dir == 0 ? pos_target(p.z, P.k_contact, P.k_sep) : 0.f);
+    }
+    rw.mu(nc) = (float)R::cube_floor_mu;
+    nc++;
+  });
+  // --- robot geoms vs the box
+  f3 G0[R::NCG], G1[R::NCG];
+#pragma unroll
+  for (int g = 0; g < R::NCG; g++) {
+    const int b = R::cgeom_link[g] + 1;
+    G0[g] = k.x[b] + mulc(k.Rm[b], (float)R::cgeom_p0[g][0], (float)R::cgeom_p0[g][1], (float)R::cgeom_p0[g][2]);
+    G1[g] = k.x[b] + mulc(k.Rm[b], (float)R::cgeom_p1[g][0], (float)R::cgeom_p1[g][1], (float)R::cgeom_p1[g][2]);
+  }
+  m3 Rt;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) Rt.m[3 * i + j] = Rc.m[3 * j + i];
+  const float bound = (float)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
+#pragma unroll 1
+  for (int g = 0; g < R::NCG; g++) {
+    const float r = (float)R::cgeom_r[g];
+    const f3 p0 = mul(Rt, G0[g] - xc), p1 = mul(Rt, G1[g] - xc), d = p1 - p0;
+    const float dd = dot3(d, d);
+    const float t0 = dd > 1e-12f ? fminf(fmaxf(-dot3(p0, d) / dd, 0.f), 1.f) : 0.f;
+    if (!(norm3(p0 + t0 * d) < bound + r + thr)) continue;
+    float t = 0.f;
+    if (dd > 1e-12f) {
+      const float phi = 0.6180339887498949f;
+      float a = 0.f, bb = 1.f;
+      float x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
+      float f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
+#pragma unroll 1
+      for (int it = 0; it < PBG_CUBE_GS_ITERS; it++) {
+        if (f1 <= f2) { bb = x2; x2 = x1; f2 = f1; x1 = bb - phi * (bb - a); f1 = box_sd(p0 + x1 * d, h); }
+        else { a = x1; x1 = x2; f1 = f2; x2 = a + phi * (bb - a); f2 = box_sd(p0 + x2 * d, h); }
+      }
+      t = 0.5f * (a + bb);
+    }
+    const f3 ps = p0 + t * d;
+    const float dist = box_sd(ps, h) - r;
+    if (!(dist < thr)) continue;
+    f3 nb, qb;
+    const float qx = fabsf(ps.x) - h, qy = fabsf(ps.y) - h, qz = fabsf(ps.z) - h;
+    if (fmaxf(qx, fmaxf(qy, qz)) > 0.f) {
+      qb = mk3(fminf(fmaxf(ps.x, -h), h), fminf(fmaxf(ps.y, -h), h), fminf(fmaxf(ps.z, -h), h));
+      const f3 dv = ps - qb;
+      const float l = norm3(dv);
+      nb = l > 1e-9f ? (1.f / l) * dv : mk3(0, 0, 1);
+    } else {
+      const int ax = (qx >= qy && qx >= qz) ? 0 : (qy >= qz ? 1 : 2);
+      const float cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
+      const float sg = cc < 0.f ? -1.f : 1.f;
+      nb = mk3(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
+      qb = mk3(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
+    }
+    csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + 8 + g));
+    const f3 nrm = mul(Rc, nb);
+    const f3 PA = xc + mul(Rc, ps) - r * nrm, PB = xc + mul(Rc, qb);
+    f3 t1, t2;  // btPlaneSpace1(nrm)
+    if (fabsf(nrm.z) > 0.7071067811865476f) {
+      const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
+      t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
+      t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+    } else {
+      const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
+      t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
+      t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+    }
+    const int lnk = R::cgeom_link[g];
+    const uint32_t ma = lnk >= 0 ? R::link_chain_mask[lnk] : 0u;
+    const f3 rA = PA - O, rB = PB - xc;
+#pragma unroll 1
+    for (int dir = 0; dir < 3; dir++) {
+      const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
+      const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
+      float y[NY];
+      float D2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int di = D::dof_of(i);
+        const bool inA = di < 0 || ((ma >> di) & 1u);
+        float tt = inA ? dot3(nd, sv[i]) + dot3(mA, sw[i]) : 0.f;
+#pragma unroll
+        for (int kk = 0; kk < i; kk++)
+          if (D::coupled(i, kk)) tt -= L[D::lidx(i, kk)] * y[kk];
+        y[i] = tt * Ld[i];
+        D2 += y[i] * y[i];
+      }
+      y[N] = -nd.x * rm; y[N + 1] = -nd.y * rm; y[N + 2] = -nd.z * rm;
+      y[N + 3] = -mB.x * rI; y[N + 4] = -mB.y * rI; y[N + 5] = -mB.z * rI;
+#pragma unroll
+      for (int i = N; i < NY; i++) D2 += y[i] * y[i];
+      rw.put(3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f, dir == 0 ? pos_target(dist, P.k_contact, P.k_sep) : 0.f);
+    }
+    rw.mu(nc) = (float)R::cgeom_mu[g];
+    nc++;
+  }
+  return nc;
 }
 
 template <class R, int LS>
@@ -771,9 +1003,11 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
                     uint32_t& csig, const SimP& P SUB_STAMP_ARGS) {
   using D = Dims<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
+  constexpr int NY = D::NY;  // rows and u: the robot's N (+ HumanoidFlagrunHarder's cube 6)
   float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
-  float Ld[N], nu[N], u[N];
+  float Ld[N], nu[N], u[NY];
   dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
+  cube_unconstrained<R>(s, u + N, P);
   f3 O;
   STAMP(2)
   // --- constraint rows: joint limits, contact normals, frictions (Bullet order) ---------
@@ -841,7 +1075,9 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       float Jr[N];
 #pragma unroll
       for (int i = 0; i < N; i++) Jr[i] = D::in_chain(i, lnk) ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : 0.f;
-      float y[N];
+      float y[NY];
+#pragma unroll
+      for (int i = N; i < NY; i++) y[i] = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) {
         if (!D::in_chain(i, lnk)) { y[i] = 0.f; continue; }
@@ -920,7 +1156,9 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       for (int dir = 0; dir < 3; dir++) {
         const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
         const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
-        float y[N];
+        float y[NY];
+#pragma unroll
+        for (int i = N; i < NY; i++) y[i] = 0.f;
         float D2 = 0.f;
 #pragma unroll
         for (int i = 0; i < N; i++) {
@@ -943,6 +1181,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       nc++;
     }
   }
+  if constexpr (R::harder) nc = cube_contacts<R, LS>(s, k, sw, sv, O, L, Ld, rw, sub, csig, P, nc);
 
   STAMP(4)
   // --- PGS: 5 sweeps in u-space (gym_locomotion_envs -> scene_bases.py:65 numSolverIterations=5)
@@ -988,6 +1227,7 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 
   STAMP(5)
   integrate<R>(s, L, Ld, u, nu, P);
+  cube_integrate<R>(s, u + N, P);
   STAMP(6)
   return nc;
 }
@@ -1056,6 +1296,7 @@ struct PackOut {
   int at_limit;                               // joints_at_limit
   uint32_t feet_out;  // bitmask
   bool done;
+  double body_xyz[3];                         // robot.body_xyz (HumanoidFlagrunHarder)
 };
 
 // robot_locomotors.py:31-64 calc_state + gym_locomotion_envs.py:59-114 reward/done.
@@ -1157,6 +1398,7 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   out.dist = dist;
   out.pitch = pitch;
   out.at_limit = at_limit;
+  out.body_xyz[0] = bx; out.body_xyz[1] = by; out.body_xyz[2] = bz;
   out.potential = -dist / in.env_dt;  // robot_locomotors.py:79; scene_bases.py:17
   uint32_t fb = 0;
 #pragma unroll
@@ -1217,8 +1459,33 @@ PBG_DEV void flag_draw(const Buffers& B, int e, Flag& f) {
 // calc_state with HumanoidFlagrun's bookkeeping (:219-226): count the timeout down, pack
 // against the current flag, and if the target is within 1 m or the timeout ran out, re-draw
 // (`redraw(f)`) and pack again against the new flag.  Other robots: plain walker_pack.
+// HumanoidFlagrunHarder bookkeeping (robot_locomotors.py:230-302); crawl_start NaN = None.
+struct HarderBk {
+  int frame, onground, launches;
+  double crawl_start, crawl_ignored;
+};
+// potential_leak (:275-278): clip(body z, 0, 0.8) / 0.8 + 1 (NaN passes np.clip)
+PBG_DEV double potential_leak(double z) {
+  const double c = z < 0.0 ? 0.0 : (z > PBG_HARDER_GROUND_Z ? PBG_HARDER_GROUND_Z : z);
+  return c / 0.8 + 1.0;
+}
+// calc_potential (:280-302) from Humanoid.calc_potential's fp and body_xyz[2]; every call
+// updates the crawl bookkeeping (env reset, _step, and the flag re-draw's robot.potential)
+PBG_DEV double harder_potential(HarderBk& h, double fp, double bz) {
+  if (bz < PBG_HARDER_GROUND_Z) {
+    if (isnan(h.crawl_start)) h.crawl_start = fp - h.crawl_ignored;
+    h.crawl_ignored = fp - h.crawl_start;
+    fp = h.crawl_start;
+  } else {
+    fp -= h.crawl_ignored;
+    h.crawl_start = __builtin_nan("");
+  }
+  return fp + potential_leak(bz) * 100;
+}
+
 template <class R, int Q = 1, class Redraw>
-PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po, Flag& f, Redraw&& redraw, int lane = 0) {
+PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po, Flag& f, Redraw&& redraw, int lane = 0,
+                       HarderBk* hb = nullptr) {
   if constexpr (R::flagrun) {
     f.timeout -= 1;
     in.target_x = f.tx; in.target_y = f.ty;
@@ -1227,8 +1494,11 @@ PBG_DEV void flag_pack(PackIn<R>& in, const float* act, float* obs, PackOut& po,
       redraw(f);
       in.target_x = f.tx; in.target_y = f.ty;
       walker_pack<R, false, Q>(in, act, obs, po, lane);
+      if constexpr (R::harder)  // self.potential = self.calc_potential() (:225) on the robot
+        if (hb) (void)harder_potential(*hb, po.potential, po.body_xyz[2]);
     }
   } else {
+    (void)hb;
     (void)f; (void)redraw;
     walker_pack<R, false, Q>(in, act, obs, po, lane);
   }
@@ -1242,6 +1512,86 @@ PBG_DEV Flag load_flag(const Buffers& B, int e) {
 template <class R>
 PBG_DEV void store_flag(const Buffers& B, int e, const Flag& f) {
   if constexpr (R::flagrun) { B.tgt[e] = f.tx; B.tgt[B.n + e] = f.ty; B.ftm[e] = f.timeout; B.ftm[B.n + e] = f.count; }
+}
+template <class R>
+PBG_DEV HarderBk load_harder(const Buffers& B, int e) {
+  HarderBk h = {0, 0, 0, 0.0, 0.0};
+  if constexpr (R::harder) {
+    h.frame = B.hki[e]; h.onground = B.hki[B.n + e]; h.launches = B.hki[2 * B.n + e];
+    h.crawl_start = B.hkd[e]; h.crawl_ignored = B.hkd[B.n + e];
+  }
+  return h;
+}
+template <class R>
+PBG_DEV void store_harder(const Buffers& B, int e, const HarderBk& h) {
+  if constexpr (R::harder) {
+    B.hki[e] = h.frame; B.hki[B.n + e] = h.onground; B.hki[2 * B.n + e] = h.launches;
+    B.hkd[e] = h.crawl_start; B.hkd[B.n + e] = h.crawl_ignored;
+  }
+}
+// The cube launch of alive_bonus (:251-265) in float64: angle U(-3.14, 3.14), speed U(20, 30),
+// jitter U(-1, 1)^3 (np_random there; Philox4x32-10 here, keyed by the seed, counter (global
+// env, launch index, 0xC0BE / 0xC0BF, 0x5EED)); d (nullable) = recorded draws (golden tests).
+// Writes the cube's position and velocity (orientation kept, angular velocity 0).
+PBG_DEV void harder_launch(const Buffers& B, int e, HarderBk& h, const double* body_xyz, const double* speed,
+                           double* pos, double* vel, const double* draws) {
+  double d[5];
+  if (draws) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) d[i] = draws[i];
+  } else {
+    u4 c = {(uint32_t)(B.env_offset + e), (uint32_t)h.launches, 0xC0BEu, 0x5EEDu};
+    u4 c2 = {(uint32_t)(B.env_offset + e), (uint32_t)h.launches, 0xC0BFu, 0x5EEDu};
+    const u4 r = philox4x32_10(c, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
+    const u4 r2 = philox4x32_10(c2, (uint32_t)B.seed, (uint32_t)(B.seed >> 32));
+    d[0] = -3.14 + (3.14 - -3.14) * (double)u01(r.x);
+    d[1] = 20.0 + (30.0 - 20.0) * (double)u01(r.y);
+    d[2] = -1.0 + (1.0 - -1.0) * (double)u01(r.z);
+    d[3] = -1.0 + (1.0 - -1.0) * (double)u01(r.w);
+    d[4] = -1.0 + (1.0 - -1.0) * (double)u01(r2.x);
+  }
+  h.launches++;
+  const double ttt = PBG_HARDER_FROM_DIST / d[1];
+  double t[3], v[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) t[i] = body_xyz[i] + speed[i] * ttt;
+  pos[0] = t[0] + PBG_HARDER_FROM_DIST * cos(d[0]);
+  pos[1] = t[1] + PBG_HARDER_FROM_DIST * sin(d[0]);
+  pos[2] = t[2] + 1.0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) v[i] = t[i] - pos[i];
+  const double sc = d[1] / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    v[i] *= sc;
+    vel[i] = v[i] + d[2 + i];
+  }
+}
+// The Harder half of _step after calc_state (gym_locomotion_envs.py:59-70 with alive_bonus
+// :250-273 and calc_potential :280-302): alive, done, potential, progress and the reward of po
+// are redone.  Returns true when the cube was launched (pos / vel written).
+template <class R>
+PBG_DEV bool harder_step(const Buffers& B, int e, const PackIn<R>& in, const float* obs, PackOut& po, HarderBk& h,
+                         double* pos, double* vel, const double* draws) {
+  const float z = obs[0] + (float)R::initial_z_fixed;  // state[0] + initial_z (float32, NEP 50)
+  bool launched = false;
+  if (h.frame % PBG_HARDER_LAUNCH_EVERY == 0 && h.frame > PBG_HARDER_LAUNCH_AFTER && h.onground == 0) {
+    harder_launch(B, e, h, po.body_xyz, in.vel, pos, vel, draws);
+    launched = true;
+  }
+  if (z < (float)PBG_HARDER_GROUND_Z) h.onground += 1;
+  else if (h.onground > 0) h.onground -= 1;
+  h.frame += 1;
+  const double alive = h.onground < PBG_HARDER_GROUND_FRAMES ? potential_leak(po.body_xyz[2]) : -1.0;
+  bool done = alive < 0;
+#pragma unroll
+  for (int i = 0; i < R::OBS; i++) done |= isnan(obs[i]);
+  po.potential = harder_potential(h, po.potential, po.body_xyz[2]);
+  const double progress = po.potential - in.potential_old;
+  po.terms[0] = alive; po.terms[1] = progress;
+  po.reward = ((((0.0 + alive) + progress) + po.terms[2]) + po.terms[3]) + 0.0;
+  po.done = done;
+  return launched;
 }
 
 // MuJoCo-observation planar walkers (envs/mujoco, add_ignored_joints=True):
@@ -1497,7 +1847,7 @@ PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
 // epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e]
 template <class R>
 PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                           double& pot, float& z0, uint32_t epi, Flag& fl) {
+                           double& pot, float& z0, uint32_t epi, Flag& fl, HarderBk* hb = nullptr) {
   snapshot_state<R>(s);
   if (init_q) {
 #pragma unroll
@@ -1538,8 +1888,12 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
   in.initial_z = R::initial_z_fixed;
   auto draw = [&](Flag& f) { flag_draw(B, e, f); };
   if constexpr (R::flagrun) draw(fl);  // robot_specific_reset -> flag_reposition (:199-201)
+  if constexpr (R::harder) {  // HumanoidFlagrunHarder.robot_specific_reset (:237-248)
+    hb->frame = 0; hb->onground = 0; hb->crawl_start = __builtin_nan(""); hb->crawl_ignored = 0.0;
+  }
   if constexpr (R::kind == 3) mujoco3d_pack<R>(in, nullptr, obs, po);
-  else flag_pack<R>(in, nullptr, obs, po, fl, draw);
+  else flag_pack<R>(in, nullptr, obs, po, fl, draw, 0, hb);
+  if constexpr (R::harder) po.potential = harder_potential(*hb, po.potential, po.body_xyz[2]);  // env_bases.py:70
   pot = po.potential;
   z0 = (float)po.initial_z;
   has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
@@ -1552,8 +1906,10 @@ PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q
   const uint32_t epi = B.episode[e];
   B.episode[e] = epi + 1;
   Flag fl = load_flag<R>(B, e);
-  reset_env_epi<R>(B, e, s, init_q, obs, has_floor, pot, z0, epi, fl);
+  HarderBk hb = load_harder<R>(B, e);
+  reset_env_epi<R>(B, e, s, init_q, obs, has_floor, pot, z0, epi, fl, &hb);
   store_flag<R>(B, e, fl);
+  store_harder<R>(B, e, hb);
 }
 
 template <class R>
@@ -1637,8 +1993,17 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     in.potential_old = B.pot[e];
     in.initial_z = B.z0[e];
     Flag fl = load_flag<R>(B, e);
+    HarderBk hb = load_harder<R>(B, e);
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
-    else flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); });
+    else flag_pack<R>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, 0, &hb);
+    if constexpr (R::harder) {
+      double pos[3], vel[3];
+      if (harder_step<R>(B, e, in, obs, po, hb, pos, vel, nullptr)) {  // resetBasePosition / Velocity
+#pragma unroll
+        for (int i = 0; i < 3; i++) { s.cube.p[i] = (float)pos[i]; s.cube.v[i] = (float)vel[i]; s.cube.w[i] = 0.f; }
+      }
+      store_harder<R>(B, e, hb);
+    }
     store_flag<R>(B, e, fl);
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
@@ -1729,12 +2094,31 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
       // [target x, y | flag_timeout | next target x, y]: the reposition takes the recorded draw
       const int o_f = o_pot + 3;
       Flag f = {r[o_f], r[o_f + 1], (int)r[o_f + 2], 0};
+      // HumanoidFlagrunHarder: [frame | on_ground | crawl_start | crawl_ignored | launch draws 5]
+      const int o_h = o_f + 5;
+      HarderBk hb = {0, 0, 0, 0.0, 0.0};
+      if constexpr (R::harder) hb = HarderBk{(int)r[o_h], (int)r[o_h + 1], 0, r[o_h + 2], r[o_h + 3]};
       flag_pack<R>(in, is_step ? act : nullptr, obs, po, f, [&](Flag& g) {
         g.tx = r[o_f + 3]; g.ty = r[o_f + 4]; g.timeout = PBG_FLAG_TIMEOUT; g.count++;
-      });
+      }, 0, &hb);
       w[R::OBS + 4 + R::NF] = f.tx;
       w[R::OBS + 4 + R::NF + 1] = f.ty;
       w[R::OBS + 4 + R::NF + 2] = f.timeout;
+      if constexpr (R::harder) {
+        // out: [frame | on_ground | crawl_start | crawl_ignored | launched | cube position 3 | velocity 3]
+        double pos[3] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan("")}, vel[3] = {pos[0], pos[1], pos[2]};
+        bool launched = false;
+        if (is_step) {
+          Buffers Bz{};
+          launched = harder_step<R>(Bz, e, in, obs, po, hb, pos, vel, r + o_h + 4);
+        } else {
+          po.potential = harder_potential(hb, po.potential, po.body_xyz[2]);
+        }
+        double* ho = w + R::OBS + 4 + R::NF + 3;
+        ho[0] = hb.frame; ho[1] = hb.onground; ho[2] = hb.crawl_start; ho[3] = hb.crawl_ignored; ho[4] = launched ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; i++) { ho[5 + i] = pos[i]; ho[8 + i] = vel[i]; }
+      }
     } else if (in.n_parts == R::NP || in.n_parts == R::NP + 1) {
       // the step's part counts take the kernels' compile-time path (what this test pins)
       walker_pack<R>(in, is_step ? act : nullptr, obs, po);
@@ -1770,6 +2154,11 @@ __global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __rest
     const Flag fl = load_flag<R>(B, e);
     a[4 + R::NF] = fl.tx; a[5 + R::NF] = fl.ty; a[6 + R::NF] = fl.timeout; a[7 + R::NF] = fl.count;
   }
+  if constexpr (R::harder) {
+    const HarderBk h = load_harder<R>(B, e);
+    a[8 + R::NF] = h.frame; a[9 + R::NF] = h.onground; a[10 + R::NF] = h.crawl_start;
+    a[11 + R::NF] = h.crawl_ignored; a[12 + R::NF] = h.launches;
+  }
   a[AD - 1] = (double)B.episode[e];  // the reset-noise Philox counter
 }
 template <class R>
@@ -1788,6 +2177,8 @@ __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* 
     B.flags[e] = fl;
     if constexpr (R::flagrun)
       store_flag<R>(B, e, Flag{a[4 + R::NF], a[5 + R::NF], (int)a[6 + R::NF], (int)a[7 + R::NF]});
+    if constexpr (R::harder)
+      store_harder<R>(B, e, HarderBk{(int)a[8 + R::NF], (int)a[9 + R::NF], (int)a[12 + R::NF], a[10 + R::NF], a[11 + R::NF]});
     B.episode[e] = (uint32_t)a[AD - 1];
   }
 }

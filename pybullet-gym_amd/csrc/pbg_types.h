@@ -49,6 +49,8 @@ struct Buffers {
   uint32_t* episode;       // [n] resets so far (RNG counter)
   double* tgt;             // [2][n] walk target x, y (HumanoidFlagrun)
   int32_t* ftm;            // [2][n] flag_timeout, flag draws so far (HumanoidFlagrun RNG counter)
+  double* hkd;             // [2][n] crawl_start_potential (NaN = None), crawl_ignored_potential (Harder)
+  int32_t* hki;            // [3][n] frame, on_ground_frame_counter, cube launches so far (Harder)
   uint64_t seed;
   int env_offset;          // global id of env 0 (multi-GPU sharding)
   SimP sp;                 // the handle's scene parameters (kernel arguments)

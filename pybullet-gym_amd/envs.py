@@ -109,6 +109,7 @@ HalfCheetah = _robot_class("halfcheetah", "HalfCheetah")     # :109-127
 Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
 HumanoidFlagrun = _robot_class("humanoid_flagrun", "HumanoidFlagrun")  # :195-226
+HumanoidFlagrunHarder = _robot_class("humanoid_flagrun_harder", "HumanoidFlagrunHarder")  # :229-302
 HopperMuJoCo = _robot_class("hopper_mujoco", "Hopper")                # mujoco/robot_locomotors.py:82-121
 Walker2DMuJoCo = _robot_class("walker2d_mujoco", "Walker2D")          # :124-164
 HalfCheetahMuJoCo = _robot_class("halfcheetah_mujoco", "HalfCheetah")  # :167-207
@@ -139,6 +140,8 @@ Walker2D.alive_bonus = _alive_bonus_hopper  # robot_locomotors.py:100-101 (same 
 Ant.alive_bonus = _alive_bonus_ant
 Humanoid.alive_bonus = _alive_bonus_humanoid
 HumanoidFlagrun.alive_bonus = _alive_bonus_humanoid
+# HumanoidFlagrunHarder.alive_bonus (robot_locomotors.py:250-273) moves the cube and counts
+# frames; it runs inside the step kernel (the per-env bookkeeping lives in the aux record)
 
 
 # ----------------------------------------------------------------------------- envs
@@ -292,6 +295,21 @@ class HumanoidFlagrunBulletEnv(HumanoidBulletEnv):
         HumanoidBulletEnv.__init__(self, HumanoidFlagrun(), render, device)
 
 
+class HumanoidFlagrunHarderBulletEnv(HumanoidBulletEnv):
+    """gym_locomotion_envs.py:167-178: HumanoidFlagrun plus an attacking 1.2 kg, 5 cm cube
+    (gym_utils.get_cube) launched at the robot every 30 frames after frame 100 while it is up,
+    an alive bonus / potential that leak with the torso height, crawl disabled, and the episode
+    ended after 170 frames on the ground (robot_locomotors.py:229-302).  The cube is a second
+    free body of the env's physics state; its launches are Philox draws (not np_random).
+    The env's ``electricity_cost /= 4`` (:172) is overwritten by HumanoidBulletEnv.__init__
+    (:150), so the Humanoid's costs stand, as in the reference."""
+    env_id = "HumanoidFlagrunHarderPyBulletEnv-v0"
+    random_lean = True  # :168 (a class attribute of the env; the robot never reads it)
+
+    def __init__(self, render=False, device="cuda:0"):
+        HumanoidBulletEnv.__init__(self, HumanoidFlagrunHarder(), render, device)
+
+
 class WalkerBaseMuJoCoEnv(WalkerBaseBulletEnv):
     """envs/mujoco/gym_locomotion_envs.py:8-118 (MuJoCo-style observations on the same
     pybullet physics)."""
@@ -417,6 +435,7 @@ ENV_CLASSES = {
     "AntPyBulletEnv-v0": AntBulletEnv,
     "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
     "HumanoidFlagrunPyBulletEnv-v0": HumanoidFlagrunBulletEnv,
+    "HumanoidFlagrunHarderPyBulletEnv-v0": HumanoidFlagrunHarderBulletEnv,
     "HopperMuJoCoEnv-v0": HopperMuJoCoEnv,
     "Walker2DMuJoCoEnv-v0": Walker2DMuJoCoEnv,
     "HalfCheetahMuJoCoEnv-v0": HalfCheetahMuJoCoEnv,

@@ -156,9 +156,6 @@ _add(RobotSpec("HumanoidMuJoCoEnv-v0", "humanoid_mujoco", "humanoid_symmetric.xm
                alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
                power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8))
 
-ENV_IDS = {s.env_id: s for s in SPECS.values()}
-
-
 # HumanoidFlagrunHarder: robot_locomotors.py:230-302 (the attacking cube of gym_utils.py:9-15,
 # alive_bonus / potential_leak / crawl-disabling calc_potential), gym_locomotion_envs.py:167-178,
 # envs/__init__.py:93-97.  The env's `self.electricity_cost /= 4` (:172) runs before
@@ -169,6 +166,8 @@ _add(RobotSpec("HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder",
                alive=ALIVE_HUMANOID, motor_order=SPECS["humanoid"].motor_order,
                power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8,
                electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1, flagrun=True, harder=True))
+
+ENV_IDS = {s.env_id: s for s in SPECS.values()}
 
 
 def spec_for(name: str) -> RobotSpec:

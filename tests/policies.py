@@ -33,6 +33,7 @@ POLICY_FILES = {
     "AntPyBulletEnv-v0": "policy_ant.npz",
     "HumanoidPyBulletEnv-v0": "policy_humanoid.npz",
     "HumanoidFlagrunPyBulletEnv-v0": "policy_humanoidflagrun.npz",
+    "HumanoidFlagrunHarderPyBulletEnv-v0": "policy_humanoidflagrunharder.npz",
 }
 MAX_STEPS = 1000  # TimeLimit (envs/__init__.py max_episode_steps)
 

@@ -29,7 +29,8 @@ ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPy
         "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0",
         "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
         "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0",
-        "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0"]
+        "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0",
+        "HumanoidFlagrunHarderPyBulletEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -79,6 +80,8 @@ def test_device_pack_matches_reference_golden(env_id):
         rec[i, o + 2] = float(g["kind"][i] == 1)
         if "flag_in" in g.files:  # HumanoidFlagrun: target, flag_timeout, the recorded re-draw
             rec[i, o + 3:o + 8] = g["flag_in"][i]
+        if "harder_in" in g.files:  # HumanoidFlagrunHarder: bookkeeping + the recorded launch draws
+            rec[i, o + 8:o + 17] = g["harder_in"][i]
         if "body_avel" in g.files:  # MuJoCo Ant / Humanoid: torso angular velocity
             rec[i, o + 3:o + 6] = g["body_avel"][i]
     out = pack(env_id, torch.from_numpy(rec).cuda()).cpu().numpy()
@@ -95,7 +98,13 @@ def test_device_pack_matches_reference_golden(env_id):
         np.testing.assert_array_equal(out[:, info.OBS + 3], g["initial_z_out"])
         np.testing.assert_array_equal(out[:, info.OBS + 4:info.OBS + 4 + info.NF], g["feet_out"][:, : info.NF])
     if "flag_out" in g.files:
-        np.testing.assert_array_equal(out[:, info.OBS + 4 + info.NF:], g["flag_out"])
+        np.testing.assert_array_equal(out[:, info.OBS + 4 + info.NF:info.OBS + 7 + info.NF], g["flag_out"])
+    if "harder_out" in g.files:  # frame, on_ground, launched exact; crawl potentials / cube launch float64
+        ho, ref = out[:, info.OBS + 7 + info.NF:], g["harder_out"]
+        np.testing.assert_array_equal(ho[:, [0, 1, 4]], ref[:, [0, 1, 4]])
+        np.testing.assert_allclose(ho[:, [2, 3]], ref[:, [2, 3]], rtol=1e-13, atol=1e-9, equal_nan=True)
+        np.testing.assert_allclose(ho[:, 5:], ref[:, 5:], rtol=1e-12, atol=1e-12, equal_nan=True)
+        assert (ref[:, 4] == 1).sum() >= 3  # the vectors hold cube launches
 
 
 # ------------------------------------------------------------------ reset
@@ -198,7 +207,8 @@ COND_FRAC_ENV = {"InvertedPendulumPyBulletEnv-v0": 0.05, "InvertedPendulumSwingu
                  "HopperPyBulletEnv-v0": 0.67, "HalfCheetahPyBulletEnv-v0": 0.26, "AntPyBulletEnv-v0": 0.51,
                  "HumanoidPyBulletEnv-v0": 0.38, "Walker2DPyBulletEnv-v0": 0.65,
                  "HumanoidFlagrunPyBulletEnv-v0": 0.35, "HopperMuJoCoEnv-v0": 0.19, "Walker2DMuJoCoEnv-v0": 0.40,
-                 "HalfCheetahMuJoCoEnv-v0": 0.64, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.85}
+                 "HalfCheetahMuJoCoEnv-v0": 0.64, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.85,
+                 "HumanoidFlagrunHarderPyBulletEnv-v0": 0.6}
 
 
 def _probe_state(state, rng):
@@ -367,7 +377,11 @@ class SplitStats:
 
 
 def _discrete_terms(terms, kind):
-    """Columns of the reward terms that are discrete (alive bonus, joints-at-limit penalty)."""
+    """Columns of the reward terms that are discrete (alive bonus, joints-at-limit penalty).
+    HumanoidFlagrunHarder's alive bonus is potential_leak (continuous in the torso height) or -1
+    after 170 frames on the ground (robot_locomotors.py:273): its discrete part is the sign."""
+    if kind == "harder":
+        return np.stack([terms[:, 0] < 0, terms[:, 3]], axis=1)
     if kind == 0:
         return terms[:, [0, 3]]  # alive, joints_at_limit (gym_locomotion_envs.py:99-105)
     if kind == 3:
@@ -375,7 +389,7 @@ def _discrete_terms(terms, kind):
     return terms[:, :0]
 
 
-def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None, sim=None):
+def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None, sim=None, init=None):
     """GPU steps all n envs (auto-reset on, Philox actions); before every step the sampled
     envs' float64 state records are copied into the oracle, which steps them from the same
     state, and into two more oracle instances at PROBE_REL perturbations of it (the
@@ -387,22 +401,26 @@ def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None, sim=None):
         sp.update(sim)
         oracle.set_sim_params(sp)
         try:
-            return _teacher_forced_run(env_id, n, steps, sample, seed, name, sim)
+            return _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init)
         finally:
             oracle.set_sim_params(None)
-    return _teacher_forced_run(env_id, n, steps, sample, seed, name, None)
+    return _teacher_forced_run(env_id, n, steps, sample, seed, name, None, init)
 
 
-def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim):
+def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init=None):
     env = VecEnv(env_id, n, seed=seed, autoreset=True, sim_params=sim)
     env.reset()
+    if init is not None:  # rewrite the reset state records (phys, aux) before the first step
+        phys, aux = env.get_state()
+        init(phys, aux)
+        env.set_state(phys, aux)
     idx = np.arange(n) if sample is None else np.linspace(0, n - 1, sample).astype(np.int64)
     tidx = torch.from_numpy(idx).cuda()
     th = min(16, os.cpu_count() or 1)
     orc = oracle.OracleEnvs(env_id, len(idx), nthreads=th, seed=seed)
     prb = [oracle.OracleEnvs(env_id, len(idx), nthreads=th, seed=seed) for _ in range(N_PROBES)]
     pert = np.random.default_rng(seed)
-    kind = orc.info.kind
+    kind = "harder" if "Harder" in env_id else orc.info.kind
     acts = sample_actions(env.info.action_dim, n, steps, seed=seed)
     st = SplitStats(name or f"teacher_forced[{env_id},{n}x{steps}]", env_id)
     for t in range(steps):
@@ -746,7 +764,7 @@ def test_reward_terms_match_oracle_and_sum(env_id):
         # class A env-steps (same contact set, well conditioned; see SplitStats)
         same = (env.contact_sig.cpu().numpy().view(np.uint32) == orc.csig) & (prb.csig == orc.csig)
         same &= _rel(op, oo) <= COND_EPS
-        kind = orc.info.kind
+        kind = "harder" if "Harder" in env_id else orc.info.kind
         same &= (_discrete_terms(terms, kind) == _discrete_terms(orc.terms, kind)).all(axis=1)
         np.testing.assert_allclose(terms[same], orc.terms[same], rtol=1e-3, atol=1e-3)
         compared += int(same.sum())
@@ -816,6 +834,57 @@ def test_flagrun_redraws_match_oracle():
     assert redraws >= n  # every env's flag timed out at least once
     e = np.concatenate(errs)
     assert np.median(e) <= 1e-4 and np.percentile(e, 99) <= 1e-2
+
+
+# ------------------------------------------------------------------ HumanoidFlagrunHarder
+HARDER = "HumanoidFlagrunHarderPyBulletEnv-v0"
+
+
+def _harder_launch_now(phys, aux):
+    """Every env at frame 120 with the on-ground counter at 0: the next alive_bonus launches
+    the cube (robot_locomotors.py:251), so the parity run covers flights and impacts."""
+    nf = 2
+    aux[:, 8 + nf] = 120.0
+    aux[:, 9 + nf] = 0.0
+
+
+def test_harder_cube_launch_and_impact_teacher_forced():
+    """The attacking cube (robot_locomotors.py:229-302): launched at every env on the first
+    step, teacher-forced for 40 steps through its flight, its impacts on the humanoid's geoms
+    and its landing -- the same class / outlier machinery as every other parity test.  A
+    GPU-only rollout of the same start then checks that the cube did hit (its velocity turned
+    by an impact in mid air) in a good share of the envs, and that the bookkeeping words
+    (frame, on-ground counter, launches) follow the oracle's exactly."""
+    n, steps = 256, 40
+    _teacher_forced(HARDER, n, steps, seed=11, name=f"harder_launch[{n}x{steps}]", init=_harder_launch_now)
+    env = VecEnv(HARDER, n, seed=11, autoreset=False)
+    env.reset()
+    phys, aux = env.get_state()
+    _harder_launch_now(phys, aux)
+    env.set_state(phys, aux)
+    orc = oracle.OracleEnvs(HARDER, n, nthreads=8, seed=11)
+    acts = sample_actions(17, n, steps, seed=11)
+    c0 = 13 + 2 * 17
+    hit = np.zeros(n, bool)
+    prev_v = None
+    for t in range(steps):
+        phys, aux = env.get_state()
+        orc.state[:] = phys.cpu().numpy()
+        orc.aux[:] = aux.cpu().numpy()
+        env.step(acts[t])
+        orc.step(acts[t].cpu().numpy())
+        phys2, aux2 = env.get_state()
+        # frame, on_ground, launches exact (crawl potentials within the step tolerance)
+        np.testing.assert_array_equal(aux2.cpu().numpy()[:, [10, 11, 14]], orc.aux[:, [10, 11, 14]])
+        cs = phys2.cpu().numpy()[:, c0:c0 + 13]
+        v = cs[:, 7:10]
+        if t == 0:
+            assert (orc.aux[:, 14] == 1).all() and (np.linalg.norm(v, axis=1) > 15).all()  # launched
+        elif prev_v is not None:
+            dv = np.linalg.norm(v - prev_v, axis=1)
+            hit |= (dv > 3.0) & (cs[:, 2] > 0.2)  # gravity alone changes v by 0.16 m/s per step
+        prev_v = v
+    assert hit.mean() >= 0.1, hit.mean()
 
 
 def test_state_dict_round_trip_and_record_version():

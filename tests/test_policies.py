@@ -18,7 +18,8 @@ import policies
 # Humanoid / HumanoidFlagrun: the policies fall after ~60 steps here (they walk on pybullet);
 # the band pins what they do now -- a positive return where random actions score ~ -28, and
 # episodes of >= 45 steps (random: ~30) -- so a dynamics regression on the hardest robot shows.
-MIN_LEN = {"HumanoidPyBulletEnv-v0": 45, "HumanoidFlagrunPyBulletEnv-v0": 45, "HalfCheetahPyBulletEnv-v0": 900}
+MIN_LEN = {"HumanoidPyBulletEnv-v0": 45, "HumanoidFlagrunPyBulletEnv-v0": 45, "HalfCheetahPyBulletEnv-v0": 900,
+           "HumanoidFlagrunHarderPyBulletEnv-v0": 220}
 BANDS = {
     "InvertedPendulumPyBulletEnv-v0": (8, 999.0, 10.0),
     "InvertedPendulumSwingupPyBulletEnv-v0": (8, 700.0, None),  # swings up and balances (random: -920)
@@ -29,6 +30,11 @@ BANDS = {
     "AntPyBulletEnv-v0": (8, 650.0, 1.15),  # walks forward at ~0.7 m/s; random actions mostly stand (alive +1)
     "HumanoidPyBulletEnv-v0": (8, 0.0, None),
     "HumanoidFlagrunPyBulletEnv-v0": (8, 10.0, None),
+    # HumanoidFlagrunHarder: the policy (trained to get up and run on pybullet) falls here too; it
+    # then lies until the 170-frame ground counter ends the episode (robot_locomotors.py:273).
+    # Band: mean return -268 over 8 oracle episodes (-211 over 64; random actions -314), length
+    # ~260 steps.
+    "HumanoidFlagrunHarderPyBulletEnv-v0": (8, -290.0, None),
 }
 
 
