@@ -43,7 +43,8 @@ typedef struct {
   int robot_id;          /* 0 pendulum, 1 hopper, 2 halfcheetah, 3 ant, 4 humanoid, 5 walker2d,
                             6 pendulum_swingup, 7 double_pendulum, 8 humanoid_flagrun,
                             9 hopper_mujoco, 10 walker2d_mujoco, 11 halfcheetah_mujoco,
-                            12 ant_mujoco, 13 humanoid_mujoco, 14 double_pendulum_mujoco */
+                            12 ant_mujoco, 13 humanoid_mujoco, 14 double_pendulum_mujoco,
+                            15 humanoid_flagrun_harder */
   int n_envs;
   int action_dim;        /* action_space.shape[0]   (robot_bases.py:24-25) */
   int obs_dim;           /* observation_space.shape[0] (robot_bases.py:26-27) */
@@ -85,8 +86,9 @@ typedef struct {
                          [alive,] power_cost; pendulums: their rewards list */
   uint32_t* csig;     /* nullable [n] contact-set signature of the env step: the sum mod 2^32 of
                          fmix32((substep << 16) + candidate + 0x9E3779B9) over every active collision
-                         candidate (floor slots 0..NS-1, self pairs NS + p) of every sub-step
-                         (sim_params.h pbg_contact_hash; for parity tests) */
+                         candidate (floor slots 0..NS-1, self pairs NS + p; HumanoidFlagrunHarder's
+                         cube corners NS + NPAIR + k, cube vs robot geom NS + NPAIR + 8 + g) of every
+                         sub-step (sim_params.h pbg_contact_hash; for parity tests) */
 } pbg_step_io_t;
 
 /* Test / diagnostic launch options (pbg_create_debug).  -1 = the default everywhere. */
@@ -125,7 +127,8 @@ int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out);
  * "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "InvertedPendulumSwingupPyBulletEnv-v0",
  * "InvertedDoublePendulumPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0",
  * "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0",
- * "InvertedDoublePendulumMuJoCoEnv-v0" (the short robot names are accepted too). */
+ * "InvertedDoublePendulumMuJoCoEnv-v0", "HumanoidFlagrunHarderPyBulletEnv-v0" (the short robot
+ * names are accepted too). */
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out);
 /* pbg_create with test / diagnostic launch options (opts NULL = pbg_create). */
 int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
@@ -158,10 +161,14 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
 /* pybullet saveState/restoreState (gym_locomotion_envs.py:25,36) generalised to trace
  * replay / teacher forcing / checkpoints.  phys: [n, state_words] float64 records
  *   [0..2] base COM pos, [3..6] base quat (x,y,z,w), [7..9] base COM lin vel (world),
- *   [10..12] base ang vel (world), then q[n_joints], qd[n_joints];
+ *   [10..12] base ang vel (world), then q[n_joints], qd[n_joints], (HumanoidFlagrunHarder: the
+ *   cube's 13 words in the base's layout);
  * aux: [n, aux_words] float64 = [potential, initial_z, elapsed_steps, floor_in_parts,
- *   feet_contact[n_feet], (HumanoidFlagrun: walk target x, y, flag_timeout, flag draws),
- *   episodes started (the reset-noise RNG counter)], layout PBG_RECORD_VERSION.
+ *   feet_contact[n_feet], (HumanoidFlagrun / Harder: walk target x, y, flag_timeout, flag draws),
+ *   (HumanoidFlagrunHarder: frame, on_ground_frame_counter, crawl_start_potential (NaN = None),
+ *   crawl_ignored_potential, cube launches), episodes started (the reset-noise RNG counter)],
+ *   layout PBG_RECORD_VERSION (the Harder words are new robot-specific words, not a change of
+ *   any existing robot's layout).
  * set_state with aux == NULL replaces the physical state only: the handle keeps its own
  * bookkeeping -- potential, initial_z, elapsed steps, feet flags and the episode counter --
  * so later resets continue that handle's reset-noise stream, not the checkpoint's. */
