@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libpbg_oracle.so")
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
              "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
-             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15}
+             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15, "atlas": 16}
 ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
             "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
             "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d",
@@ -26,7 +26,7 @@ ENV_KEYS = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0"
             "Walker2DMuJoCoEnv-v0": "walker2d_mujoco", "HalfCheetahMuJoCoEnv-v0": "halfcheetah_mujoco",
             "AntMuJoCoEnv-v0": "ant_mujoco", "HumanoidMuJoCoEnv-v0": "humanoid_mujoco",
             "InvertedDoublePendulumMuJoCoEnv-v0": "double_pendulum_mujoco",
-            "HumanoidFlagrunHarderPyBulletEnv-v0": "humanoid_flagrun_harder"}
+            "HumanoidFlagrunHarderPyBulletEnv-v0": "humanoid_flagrun_harder", "AtlasPyBulletEnv-v0": "atlas"}
 
 _lib = None
 
@@ -40,6 +40,7 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
+        os.environ.setdefault("OMP_STACKSIZE", "16M")  # Atlas-sized per-env frames on worker threads
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.pbg_oracle_info.argtypes = [ctypes.c_int, P]
@@ -167,7 +168,7 @@ class _PackIn(ctypes.Structure):
                 ("feet_prev", ctypes.c_void_p), ("feet_new", ctypes.c_void_p), ("act", ctypes.c_void_p),
                 ("potential_old", ctypes.c_double), ("initial_z", ctypes.c_double),
                 ("target_x", ctypes.c_double), ("target_y", ctypes.c_double),
-                ("body_avel", ctypes.c_void_p)]
+                ("body_avel", ctypes.c_void_p), ("head_z", ctypes.c_double)]
 
 
 class _PackOut(ctypes.Structure):
@@ -178,7 +179,7 @@ class _PackOut(ctypes.Structure):
 
 
 def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet_new, act,
-         potential_old, initial_z, flag=None, body_avel=None, harder=None):
+         potential_old, initial_z, flag=None, body_avel=None, harder=None, head_z=0.0):
     """Run the oracle's pack on explicit inputs (golden-vector tests).  flag (HumanoidFlagrun):
     [target x, y, flag_timeout, next draw x, y]; the result then carries flag_out.  harder
     (HumanoidFlagrunHarder, with flag): [frame, on_ground, crawl_start, crawl_ignored, launch
@@ -195,7 +196,7 @@ def pack(name, part_xyz, body_quat, body_pos, body_vel, jq, jqd, feet_prev, feet
     ac = None if act is None else np.ascontiguousarray(act, dtype=np.float32)
     pin = _PackIn(_p(arrs["part_xyz"]), len(arrs["part_xyz"]), _p(arrs["body_quat"]), _p(arrs["body_pos"]),
                   _p(arrs["body_vel"]), _p(arrs["jq"]), _p(arrs["jqd"]), _p(arrs["feet_prev"]), _p(fn),
-                  _p(ac), float(potential_old), float(initial_z), 1e3, 0.0, None)
+                  _p(ac), float(potential_old), float(initial_z), 1e3, 0.0, None, float(head_z))
     if body_avel is not None:
         arrs["body_avel"] = np.ascontiguousarray(body_avel, dtype=np.float64)
         pin.body_avel = _p(arrs["body_avel"])

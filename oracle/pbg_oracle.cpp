@@ -37,9 +37,9 @@
 
 #include <cmath>
 
-#define MAXL 24
-#define MAXD 32
-#define MAXS 32
+#define MAXL 32
+#define MAXD 40
+#define MAXS 1024
 #define MAXPAIR 72
 #define MAXCG 24
 #define MAXCAND (MAXS + MAXPAIR + 8 + MAXCG)  // collision candidates (HumanoidFlagrunHarder's cube: 8 + NCG)
@@ -107,7 +107,7 @@ int g_diag_n = 0, g_diag_cap = 0;
 // ------------------------------------------------------------------ model view
 struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
-      floor, max_steps, robot_body, tip_link, flagrun, harder, NCG;
+      floor, max_steps, robot_body, tip_link, flagrun, harder, NCG, head_link;
   double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip, contact_erp, cube_floor_mu;
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
@@ -117,7 +117,7 @@ struct MV {
   const int *limited, *dof_jtype;
   const int* act_dof; const double* act_gain;
   const int* obs_dof; const double* obs_vel_scale; const int* reset_dof; const double* reset_offset;
-  const int* part_link; const int* foot_link;
+  const int* part_link; const int* foot_link; const int* knee_obs;
   const int* slot_link; const double (*slot_point)[3]; const double *slot_radius, *slot_mu;
   const int *pair_a, *pair_b; const double (*pa0)[3], (*pa1)[3], (*pb0)[3], (*pb1)[3];
   const double *pra, *prb, *pmu;
@@ -131,6 +131,7 @@ MV view() {
   m.NDOF = R::NDOF; m.NA = R::NA; m.NO = R::NO; m.NR = R::NR; m.NF = R::NF; m.NP = R::NP;
   m.NS = R::NS; m.NPAIR = R::NPAIR; m.OBS = R::OBS; m.alive = R::alive; m.substeps = R::substeps;
   m.floor = R::floor; m.max_steps = R::max_episode_steps; m.robot_body = R::robot_body; m.tip_link = R::tip_link;
+  m.head_link = R::head_link; m.knee_obs = R::knee_obs;
   m.flagrun = R::flagrun; m.harder = R::harder; m.NCG = R::NCG; m.cube_floor_mu = R::cube_floor_mu;
   m.cg_link = R::cgeom_link; m.cg_p0 = R::cgeom_p0; m.cg_p1 = R::cgeom_p1; m.cg_r = R::cgeom_r; m.cg_mu = R::cgeom_mu;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
@@ -159,15 +160,16 @@ double sim_env_dt(const MV& m) { return sim_dt(m) * sim_substeps(m); }
 int sim_flag_timeout(const MV& m) { return (600 + sim_substeps(m) - 1) / sim_substeps(m); }
 
 const MV* model(int robot) {
-  static MV views[16] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
+  static MV views[17] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                          view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                          view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
                          view<pbg_models::PendulumSwingup>(), view<pbg_models::DoublePendulum>(),
                          view<pbg_models::HumanoidFlagrun>(), view<pbg_models::HopperMuJoCo>(),
                          view<pbg_models::Walker2DMuJoCo>(), view<pbg_models::HalfCheetahMuJoCo>(),
                          view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>(),
-                         view<pbg_models::DoublePendulumMuJoCo>(), view<pbg_models::HumanoidFlagrunHarder>()};
-  if (robot < 0 || robot > 15) return nullptr;
+                         view<pbg_models::DoublePendulumMuJoCo>(), view<pbg_models::HumanoidFlagrunHarder>(),
+                         view<pbg_models::Atlas>()};
+  if (robot < 0 || robot > 16) return nullptr;
   return &views[robot];
 }
 
@@ -342,6 +344,7 @@ typedef struct {
   double initial_z;          // NaN: take it from this calc_state (robot_locomotors.py:44-45)
   double target_x, target_y; // robot.walk_target_x / _y (1e3, 0 except HumanoidFlagrun)
   const double* body_avel;   // base angular velocity (MuJoCo-observation Ant / Humanoid; nullable)
+  double head_z;             // Atlas: the head part's height (alive_bonus, robot_locomotors.py:319)
 } pbg_pack_in;
 
 typedef struct {
@@ -509,6 +512,12 @@ static int walker_pack_body(const MV& m, const pbg_pack_in* in, pbg_pack_out* ou
     case 2: {  // Ant: z > 0.26
       double z = (double)s0 + z0;
       alive = z > 0.26 ? 1.0 : -1.0;
+      break;
+    }
+    case 13: {  // Atlas (robot_locomotors.py:313-324): +4 - knees at limit if head z > 1.3 else -1
+      int knees = 0;
+      for (int k = 0; k < 2; k++) knees += fabsf(j[2 * m.knee_obs[k]]) > PBG_JOINT_AT_LIMIT;
+      alive = in->head_z > 1.3 ? (double)(4 - knees) : -1.0;
       break;
     }
     default: {  // Humanoid: np.float32 + python 0.8 stays float32 (NEP 50); z > 0.78 in f32
@@ -789,8 +798,10 @@ static double mujoco_planar_pack(const MV& m, const double* s, double x_before, 
 
 // Gather the pack inputs from a physical state.
 static void gather(const MV& m, const double* s, const double* aux, Kin& k, double* part_xyz,
-                   int& n_parts, double* quat, double* pos, double* vel, double* jq, double* jqd) {
+                   int& n_parts, double* quat, double* pos, double* vel, double* jq, double* jqd,
+                   double* head_z = nullptr) {
   forward_kinematics(m, s, k);
+  if (head_z) *head_z = m.head_link >= 0 ? k.c[m.head_link + 1].z : 0.0;
   n_parts = 0;
   for (int p = 0; p < m.NP; p++) {
     V3 c = k.c[m.part_link[p] + 1];
@@ -844,10 +855,11 @@ int pbg_oracle_reset_mask(int robot, int n, double* state, double* aux, const do
     static thread_local Kin k;
     double part_xyz[3 * (MAXL + 2)], quat[4], pos[3], vel[3], jq[MAXD], jqd[MAXD];
     int n_parts;
-    gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd);
+    double head_z;
+    gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd, &head_z);
     float feet_prev[8] = {0}, feet_out[8];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, nullptr, nullptr, 0.0,
-                      m.z0fixed, PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10};
+                      m.z0fixed, PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10, head_z};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);
@@ -928,11 +940,12 @@ int pbg_oracle_step_ex(int robot, int n, double* state, double* aux, const float
     static thread_local Kin k;
     double part_xyz[3 * (MAXL + 2)], quat[4], pos[3], vel[3], jq[MAXD], jqd[MAXD];
     int n_parts;
-    gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd);
+    double head_z;
+    gather(m, s, a, k, part_xyz, n_parts, quat, pos, vel, jq, jqd, &head_z);
     float feet_prev[8], feet_out[8];
     for (int f = 0; f < m.NF; f++) feet_prev[f] = (float)a[4 + f];
     pbg_pack_in in = {part_xyz, n_parts, quat, pos, vel, jq, jqd, feet_prev, feet_new, ac,
-                      a[0], a[1], PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10};
+                      a[0], a[1], PBG_WALK_TARGET_X, PBG_WALK_TARGET_Y, s + 10, head_z};
     pbg_pack_out out;
     out.obs = ob; out.feet_out = feet_out;
     Flag fl = load_flag(m, a);

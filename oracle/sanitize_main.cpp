@@ -29,7 +29,7 @@ int main(int argc, char** argv) {
     return (double)(x >> 11) * (2.0 / 9007199254740992.0) - 1.0;
   };
   const double variants[][2] = {{-1, 0}, {7, 0.85}, {6, 1}, {6, 2}, {4, 1}, {5, 1}, {11, 1}};
-  for (int robot = 0; robot < 16; robot++) {
+  for (int robot = 0; robot < 17; robot++) {
     int info[16];
     if (pbg_oracle_info(robot, info) != 0) return 2;
     const int NA = info[3], NR = info[5], OBS = info[10], SD = info[11], AD = info[12];

@@ -1,6 +1,6 @@
 """pybulletgym_amd: MI355X-native batched stepper for the roboschool locomotion envs of
 josiahls/pybullet-gym (InvertedPendulum, InvertedPendulumSwingup, InvertedDoublePendulum,
-Hopper, HalfCheetah, Ant, Humanoid, HumanoidFlagrun, HumanoidFlagrunHarder, Walker2D
+Hopper, HalfCheetah, Ant, Humanoid, HumanoidFlagrun, HumanoidFlagrunHarder, Walker2D, Atlas
 ``*PyBulletEnv-v0``, and the MuJoCo-observation variants).  Import as ``import pybulletgym_amd``.
 
     from pybulletgym_amd import VecEnv, make
@@ -12,7 +12,7 @@ ENV_IDS = ("InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheeta
            "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
            "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0",
            "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0",
-           "HumanoidFlagrunHarderPyBulletEnv-v0")
+           "HumanoidFlagrunHarderPyBulletEnv-v0", "AtlasPyBulletEnv-v0")
 
 
 def __getattr__(name):

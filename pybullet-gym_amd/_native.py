@@ -16,7 +16,8 @@ ROBOT_IDS = {"InvertedPendulumPyBulletEnv-v0": 0, "HopperPyBulletEnv-v0": 1, "Ha
              "InvertedPendulumSwingupPyBulletEnv-v0": 6, "InvertedDoublePendulumPyBulletEnv-v0": 7,
              "HumanoidFlagrunPyBulletEnv-v0": 8, "HopperMuJoCoEnv-v0": 9, "Walker2DMuJoCoEnv-v0": 10,
              "HalfCheetahMuJoCoEnv-v0": 11, "AntMuJoCoEnv-v0": 12, "HumanoidMuJoCoEnv-v0": 13,
-             "InvertedDoublePendulumMuJoCoEnv-v0": 14, "HumanoidFlagrunHarderPyBulletEnv-v0": 15}
+             "InvertedDoublePendulumMuJoCoEnv-v0": 14, "HumanoidFlagrunHarderPyBulletEnv-v0": 15,
+             "AtlasPyBulletEnv-v0": 16}
 
 
 class PbgError(RuntimeError):

@@ -133,7 +133,9 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
     act_dof = [links[i].dof for i in act_links]
     obs_dof = [links[i].dof for i in obs_links]
     # joint observation scaling (robot_bases.py:306-321): MJCF joints report maxVelocity 0
-    vel_scale = [0.1 if links[i].jtype == mjcf.JOINT_REVOLUTE else 0.5 for i in obs_links]
+    # (x0.1 revolute, x0.5 prismatic); URDF joints their <limit velocity> (urdf.py U5): 1 / maxVel
+    vel_scale = [1.0 / links[i].max_velocity if links[i].max_velocity > 0 else
+                 (0.1 if links[i].jtype == mjcf.JOINT_REVOLUTE else 0.5) for i in obs_links]
 
     dof_link = model.dof_link()
     dof = dict(
@@ -170,12 +172,22 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
                 mu = g.friction * floor_mu
                 if g.kind == mjcf.GEOM_SPHERE:
                     slots.append((li, g.p0, g.radius, mu))
-                else:
+                elif g.kind == mjcf.GEOM_CAPSULE:
                     slots.append((li, g.p0, g.radius, mu))
                     slots.append((li, g.p1, g.radius, mu))
+                else:  # URDF box corners / cylinder rim points (urdf.py U4)
+                    from . import urdf
+                    for p, r in urdf.geom_contact_points(g):
+                        slots.append((li, p, r, mu))
         add_slots(-1, model.base_geoms)
         for li, l in enumerate(links):
             add_slots(li, l.geoms)
+        if len(slots) > 64:
+            # the gang kernel reports floor contact of the first 64 slots to the feet test: the
+            # feet's slots go first (the candidate order is this compiler's choice)
+            fl = {model.link_index(f) for f in spec.foot_list}
+            slots = [x for x in slots if x[0] in fl] + [x for x in slots if x[0] not in fl]
+            assert sum(1 for x in slots if x[0] in fl) <= 64
     # self-collision pairs (Humanoid): non-ancestor link pairs, MuJoCo contype/conaffinity rule
     pairs = []
     if spec.self_collision and spec.floor:
@@ -212,6 +224,10 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
                 cgeoms.append((li, g))
 
     feet = [model.link_index(f) for f in spec.foot_list]
+    # Atlas alive_bonus (robot_locomotors.py:313-324): the head part's height and the knees'
+    # relative positions (their obs joint indices)
+    head_link = model.link_index(spec.head) if spec.head else -1
+    knee_obs = [ordered_names.index(k) for k in spec.knees] if spec.knees else [-1, -1]
     inertia6 = lambda I: [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
     t = dict(
         key=spec.key, env_id=spec.env_id, kind=spec.kind, floating=int(model.floating),
@@ -239,6 +255,7 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
         act_dof=act_dof, act_gain=act_gain, obs_dof=obs_dof, obs_vel_scale=vel_scale,
         reset_dof=reset_dof, reset_offset=[spec.reset_offset if i == 0 else 0.0 for i in range(len(reset_dof))],
         tip_link=tip_link, flagrun=int(spec.flagrun), power_cost=spec.power_cost, qvel_clip=spec.qvel_clip,
+        head_link=head_link, knee_obs=knee_obs, link_max_velocity=[l.max_velocity for l in links],
         act_joint_names=ordered_names,
         part_names=list(parts.keys()), part_link=list(parts.values()), robot_body=robot_body,
         foot_link=feet,
@@ -267,7 +284,7 @@ def compile_all(asset_dir: str = None, overrides: Dict = None) -> Dict[str, Dict
     overrides = load_overrides() if overrides is None else overrides
     out = {}
     for key, spec in robots.SPECS.items():
-        model = mjcf.compile_mjcf(os.path.join(asset_dir, spec.mjcf), key)
+        model = robots.compile_model(spec, asset_dir)
         out[key] = build_tables(spec, model, overrides.get(key))
     return out
 
@@ -309,7 +326,7 @@ def emit_struct(t: Dict) -> str:
          f"  static constexpr int kind = {t['kind']};",
          f"  static constexpr bool floating = {'true' if t['floating'] else 'false'};"]
     for k in ("NL", "NJ", "NDOF", "NA", "NO", "NR", "NF", "NP", "NS", "NPAIR", "NG", "OBS", "alive", "substeps",
-              "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun", "harder", "NCG"):
+              "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun", "harder", "NCG", "head_link"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
               "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp", "cube_floor_mu"):
@@ -338,6 +355,7 @@ def emit_struct(t: Dict) -> str:
     L.append(_arr1("reset_offset", "double", t["reset_offset"]))
     L.append(_arr1("part_link", "int", t["part_link"]))
     L.append(_arr1("foot_link", "int", t["foot_link"]))
+    L.append(_arr1("knee_obs", "int", t["knee_obs"]))
     L.append(_arr1("slot_link", "int", t["slot_link"]))
     L.append(_arr2("slot_point", "double", t["slot_point"], 3))
     L.append(_arr1("slot_radius", "double", t["slot_radius"]))
@@ -366,13 +384,14 @@ def emit_struct(t: Dict) -> str:
 ROBOT_IDS = {"pendulum": 0, "hopper": 1, "halfcheetah": 2, "ant": 3, "humanoid": 4, "walker2d": 5,
              "pendulum_swingup": 6, "double_pendulum": 7, "humanoid_flagrun": 8, "hopper_mujoco": 9,
              "walker2d_mujoco": 10, "halfcheetah_mujoco": 11, "ant_mujoco": 12, "humanoid_mujoco": 13,
-             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15}
+             "double_pendulum_mujoco": 14, "humanoid_flagrun_harder": 15, "atlas": 16}
 STRUCTS = {"pendulum": "Pendulum", "hopper": "Hopper", "halfcheetah": "HalfCheetah", "ant": "Ant",
            "humanoid": "Humanoid", "walker2d": "Walker2D", "pendulum_swingup": "PendulumSwingup",
            "double_pendulum": "DoublePendulum", "humanoid_flagrun": "HumanoidFlagrun",
            "hopper_mujoco": "HopperMuJoCo", "walker2d_mujoco": "Walker2DMuJoCo",
            "halfcheetah_mujoco": "HalfCheetahMuJoCo", "ant_mujoco": "AntMuJoCo", "humanoid_mujoco": "HumanoidMuJoCo",
-           "double_pendulum_mujoco": "DoublePendulumMuJoCo", "humanoid_flagrun_harder": "HumanoidFlagrunHarder"}
+           "double_pendulum_mujoco": "DoublePendulumMuJoCo", "humanoid_flagrun_harder": "HumanoidFlagrunHarder",
+           "atlas": "Atlas"}
 
 
 def emit_header(tables: Dict[str, Dict]) -> str:

@@ -27,7 +27,7 @@ int fail(int code, const char* fmt, const char* a = "", long b = 0) {
 
 int env_robot_id(const char* env_id) {
   if (!env_id) return -1;
-  static const char* ids[16][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
+  static const char* ids[17][2] = {{"InvertedPendulumPyBulletEnv-v0", "pendulum"},
                                   {"HopperPyBulletEnv-v0", "hopper"},
                                   {"HalfCheetahPyBulletEnv-v0", "halfcheetah"},
                                   {"AntPyBulletEnv-v0", "ant"},
@@ -42,8 +42,9 @@ int env_robot_id(const char* env_id) {
                                   {"AntMuJoCoEnv-v0", "ant_mujoco"},
                                   {"HumanoidMuJoCoEnv-v0", "humanoid_mujoco"},
                                   {"InvertedDoublePendulumMuJoCoEnv-v0", "double_pendulum_mujoco"},
-                                  {"HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder"}};
-  for (int i = 0; i < 16; i++)
+                                  {"HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder"},
+                                  {"AtlasPyBulletEnv-v0", "atlas"}};
+  for (int i = 0; i < 17; i++)
     if (!strcmp(env_id, ids[i][0]) || !strcmp(env_id, ids[i][1])) return i;
   return -1;
 }
@@ -104,13 +105,13 @@ int check_sim_params(const pbg_sim_params_t& p) {
       pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT, defaults_of<pbg_models::NAME>()}
 
 const Ops* ops(int rid) {
-  static const Ops table[16] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
+  static const Ops table[17] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
                                 PBG_OPS(Humanoid, 4), PBG_OPS(Walker2D, 5), PBG_OPS(PendulumSwingup, 6),
                                 PBG_OPS(DoublePendulum, 7), PBG_OPS(HumanoidFlagrun, 8), PBG_OPS(HopperMuJoCo, 9),
                                 PBG_OPS(Walker2DMuJoCo, 10), PBG_OPS(HalfCheetahMuJoCo, 11), PBG_OPS(AntMuJoCo, 12),
                                 PBG_OPS(HumanoidMuJoCo, 13), PBG_OPS(DoublePendulumMuJoCo, 14),
-                                PBG_OPS(HumanoidFlagrunHarder, 15)};
-  return (rid >= 0 && rid < 16) ? &table[rid] : nullptr;
+                                PBG_OPS(HumanoidFlagrunHarder, 15), PBG_OPS(Atlas, 16)};
+  return (rid >= 0 && rid < 17) ? &table[rid] : nullptr;
 }
 
 struct DeviceGuard {

@@ -39,6 +39,10 @@
 namespace pbg {
 
 #define PBG_GANG_BLOCK 256  // lanes per gang workgroup (4 waves)
+// Atlas (886 floor-contact candidates, 36 dofs): a one-wave workgroup of 4 envs -- 16 envs'
+// regions and the model tables would exceed the 160 KiB of LDS
+template <class R>
+constexpr int gang_block() { return R::NS > 128 ? 64 : PBG_GANG_BLOCK; }
 
 // bound_ctrl set: every permutation used here reads a valid lane, and with it the
 // compiler folds `x + mov_dpp(x)` into one v_add_f32_dpp (no mov, no DPP hazard nop).
@@ -470,7 +474,25 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
   // HalfCheetah: one word; Humanoid: three), set and walked branch-free (selects over the
   // words) -- the 64-bit mask with a branch per word cost 6-8 % of the step.
   constexpr int NW = (G::MAXC + 31) / 32;
-  static_assert(NW <= 4, "positive-normal mask holds 128 contacts");
+  if constexpr (NW > 4) {
+    // more than 128 contact candidates (Atlas): the plain order -- every normal, then the two
+    // friction rows of each contact whose normal impulse came out positive, a load-then-test
+    for (int c = 0; c < nc; c++) {
+      Row A;
+      gang_load_row<R, T, LDS>(X, c, 0, A);
+      gang_set_lam<R, T, LDS>(X, c, 0, gang_update<R, T>(A, us, 0.f, 3.0e38f));
+    }
+    for (int c = 0; c < nc; c++) {
+      const float lim = gang_fric_limit<R, T, LDS>(X, c);
+      if (!(lim > 0.f)) continue;  // mu * lambda_n: lambda_n > 0 (mu > 0)
+      Row A1, A2;
+      gang_load_row<R, T, LDS>(X, c, 1, A1);
+      gang_set_lam<R, T, LDS>(X, c, 1, gang_update<R, T>(A1, us, -lim, lim));
+      gang_load_row<R, T, LDS>(X, c, 2, A2);
+      gang_set_lam<R, T, LDS>(X, c, 2, gang_update<R, T>(A2, us, -lim, lim));
+    }
+    return;
+  }
   uint32_t pw0 = 0u, pw1 = 0u, pw2 = 0u, pw3 = 0u;
   auto pwr = [&](auto w_c) -> uint32_t& {
     constexpr int w = decltype(w_c)::value;
@@ -947,7 +969,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     }
     const uint64_t bal = __ballot(act);
     const uint64_t mine = bal & gang_mask;
-    sb |= (mine >> (X.le * T)) << (r * T);
+    if constexpr (r * T < 64) sb |= (mine >> (X.le * T)) << (r * T);  // the feet's slots come first
     if (act) {
       csig += pbg_contact_hash(sub, (uint32_t)sl);  // this lane's share of the signature
       const int c = nc + __popcll(bal & gang_mask & below);
@@ -1198,19 +1220,20 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
 }
 
 template <class R, int T, bool DIST>
-__global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
+__global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
   extern __shared__ float lds_dyn[];
   using G = Gang<R, T>;
   using TT = GangTabs<R>;
-  constexpr int EPB = PBG_GANG_BLOCK / T;  // envs per workgroup
+  constexpr int BLK = gang_block<R>();
+  constexpr int EPB = BLK / T;  // envs per workgroup
   lds_float* lds = (lds_float*)lds_dyn;
   {
     const uint32_t* src0 = (const uint32_t*)&g_gang_tab<R>;
     const uint32_t* src1 = (const uint32_t*)&g_gang_dyn<R>;
     __attribute__((address_space(3))) uint32_t* dst = (__attribute__((address_space(3))) uint32_t*)lds;
-    for (int i = threadIdx.x; i < (int)(sizeof(GangTab<R>) / 4); i += PBG_GANG_BLOCK) dst[i] = src0[i];
-    for (int i = threadIdx.x; i < (int)(sizeof(GangDynTab<R>) / 4); i += PBG_GANG_BLOCK) dst[TT::TAB_WORDS + i] = src1[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(GangTab<R>) / 4); i += BLK) dst[i] = src0[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(GangDynTab<R>) / 4); i += BLK) dst[TT::TAB_WORDS + i] = src1[i];
   }
   __syncthreads();
   GangCtx X;
@@ -1265,6 +1288,7 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   PackOut po;
   double pot_new = 0.0;
   Flag fl = load_flag<R>(B, e);
+  STAMPX(13)
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
   } else if constexpr (R::kind == 2) {
@@ -1273,14 +1297,14 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
   } else {
     PackIn<R> in;
     in.env_dt = B.sp.env_dt;
-    gather<R>(s, flags & 1u, in);
+    gather<R>(s, flags & 1u, in, [&](auto c) { STAMPX(decltype(c)::value) });
     STAMPX(12)
     uint32_t fnew = 0;
 #pragma unroll
     for (int f = 0; f < R::NF; f++) {
       uint64_t fm = 0;
 #pragma unroll
-      for (int sl = 0; sl < R::NS; sl++)
+      for (int sl = 0; sl < (R::NS < 64 ? R::NS : 64); sl++)
         if (R::slot_link[sl] == R::foot_link[f]) fm |= 1ull << sl;
       fnew |= ((slot_bits & fm) ? 1u : 0u) << f;
       in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
@@ -1314,7 +1338,9 @@ __global__ __launch_bounds__(PBG_GANG_BLOCK) void gang_step_kernel(Buffers B, St
     // every lane reads the episode counter (one load instruction) before the writer bumps it
     const uint32_t epi = B.episode[e];
     if (w0) B.episode[e] = epi + 1;
-    reset_env_epi<R>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl);
+    // the reset's pack deals its transcendentals over the quad as the step's does (the gang's
+    // 16 lanes take the branch together): Hopper, Walker2D and HalfCheetah reset often
+    reset_env_epi<R, 4>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl, nullptr, X.t);
     if (w0) {
       B.pot[e] = pot;
       B.z0[e] = z0;

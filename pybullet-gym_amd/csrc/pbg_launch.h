@@ -50,4 +50,5 @@ PBG_DECLARE_ROBOT(AntMuJoCo)
 PBG_DECLARE_ROBOT(HumanoidMuJoCo)
 PBG_DECLARE_ROBOT(DoublePendulumMuJoCo)
 PBG_DECLARE_ROBOT(HumanoidFlagrunHarder)
+PBG_DECLARE_ROBOT(Atlas)
 }  // namespace pbg

@@ -12,11 +12,11 @@ namespace pbg {
 // HumanoidFlagrunHarder appends to the input [frame | on_ground | crawl_start | crawl_ignored |
 // launch draws: angle, speed, jitter 3] and to the output [frame | on_ground | crawl_start |
 // crawl_ignored | launched | cube position 3 | cube velocity 3].  The MuJoCo-observation Ant /
-// Humanoid append the base angular velocity (3) to the input.
+// Humanoid append the base angular velocity (3) to the input, Atlas the head part's height.
 template <class R>
 struct PackRec {
   static constexpr int IN = (R::NP + 1) * 3 + 1 + 4 + 3 + 3 + 2 * R::NO + 2 * R::NF + R::NA + 3 + (R::flagrun ? 5 : 0) +
-                            (R::harder ? 9 : 0) + (R::kind == 3 ? 3 : 0);
+                            (R::harder ? 9 : 0) + (R::kind == 3 ? 3 : 0) + (R::alive == 13 ? 1 : 0);
   static constexpr int OUT = R::OBS + 4 + R::NF + (R::flagrun ? 3 : 0) + (R::harder ? 11 : 0);
 };
 template <class R>

@@ -83,7 +83,7 @@ template <class RR>
 static int plan_gang(int n_envs, int cus, Geometry* g) {
   if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
     using G = Gang<RR, 16>;
-    constexpr int EPB = PBG_GANG_BLOCK / 16;  // envs per workgroup
+    constexpr int EPB = gang_block<RR>() / 16;  // envs per workgroup
     const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
     // signed: with many workgroups per CU the share can be smaller than the model tables
@@ -98,7 +98,7 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     g->gang_dist = RR::NDOF >= 8 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
     if (g->force_dist == 0 || g->force_dist == 1) g->gang_dist = g->force_dist;  // pbg_create_debug
     g->team = 16;
-    g->block = PBG_GANG_BLOCK;
+    g->block = gang_block<RR>();
     g->lds_rows = cap;
     g->env_words = G::FIXED + (cap * G::PERC > G::MIN_CONTACT_WORDS ? cap * G::PERC : G::MIN_CONTACT_WORDS);
     g->env_words += g->env_words & 1;  // even: every env region 8-byte aligned (b64 row loads)
@@ -116,7 +116,7 @@ template <class RR>
 static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
     if (g.team != 16) return false;
-    const dim3 grid(blocks(B.n, PBG_GANG_BLOCK / 16)), blk(PBG_GANG_BLOCK);
+    const dim3 grid(blocks(B.n, gang_block<RR>() / 16)), blk(gang_block<RR>());
     if (g.gang_dist)
       hipLaunchKernelGGL((gang_step_kernel<RR, 16, true>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
     else
@@ -128,42 +128,66 @@ static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, cons
   }
 }
 
+// Atlas (886 floor-contact candidates) has no lane kernel: its unrolled per-slot rows would not
+// fit an instruction cache; the debug `kernel = 0` option gives it the gang kernel too.  (The
+// lane kernel is only instantiated inside these templates, behind `if constexpr`.)
+template <class RR>
+constexpr bool lane_ok() { return RR::NS <= 128; }
+template <class RR>
+static int plan_lane(int n_envs, int cus, Geometry* g) {
+  if constexpr (lane_ok<RR>()) {
+    g->team = 1;
+    g->env_words = 0;
+    const int per_cu = (n_envs + cus - 1) / cus;
+    int b = 16;
+    while (b < per_cu && b < 64) b *= 2;
+    const int wgs = (n_envs + b - 1) / b;
+    const int wpc = (wgs + cus - 1) / cus;
+    const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
+    using RW = Rows<RR, 64>;
+    long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC - RW::LIMW;
+    int cap = (int)(words / RW::W);
+    if (cap > RW::MR) cap = RW::MR;
+    if (cap < 0) cap = 0;
+    g->block = b;
+    g->lds_rows = cap;
+    g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
+    g->scratch_words_per_env = RW::WORDS;
+    const void* fn = b == 64 ? (const void*)step_kernel<RR, 64> : (b == 32 ? (const void*)step_kernel<RR, 32> : (const void*)step_kernel<RR, 16>);
+    const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
+    return e ? e : kernel_attrs(fn, g);
+  } else {
+    (void)n_envs; (void)cus; (void)g;
+    return (int)hipErrorInvalidValue;
+  }
+}
+template <class RR>
+static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if constexpr (lane_ok<RR>()) {
+    const dim3 grid(blocks(B.n, g.block)), blk(g.block);
+    if (g.block == 64) hipLaunchKernelGGL((step_kernel<RR, 64>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+    else if (g.block == 32) hipLaunchKernelGGL((step_kernel<RR, 32>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+    else hipLaunchKernelGGL((step_kernel<RR, 16>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
+    return (int)hipGetLastError();
+  } else {
+    (void)B; (void)io; (void)scratch; (void)g; (void)s;
+    return (int)hipErrorInvalidValue;
+  }
+}
+
 // mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers);
 // 2 = gang for every walker (parity tests of the gang kernel on Ant).  HumanoidFlagrunHarder
 // (a second free body per env) runs on the lane kernel only.
 int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
-  if (R::kind != 1 && !R::harder && mode >= 1) return plan_gang<R>(n_envs, cus, g);
-  g->team = 1;
-  g->env_words = 0;
-  const int per_cu = (n_envs + cus - 1) / cus;
-  int b = 16;
-  while (b < per_cu && b < 64) b *= 2;
-  const int wgs = (n_envs + b - 1) / b;
-  const int wpc = (wgs + cus - 1) / cus;
-  const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
-  using RW = Rows<R, 64>;
-  long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC - RW::LIMW;
-  int cap = (int)(words / RW::W);
-  if (cap > RW::MR) cap = RW::MR;
-  if (cap < 0) cap = 0;
-  g->block = b;
-  g->lds_rows = cap;
-  g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
-  g->scratch_words_per_env = RW::WORDS;
-  const void* fn = b == 64 ? (const void*)step_kernel<R, 64> : (b == 32 ? (const void*)step_kernel<R, 32> : (const void*)step_kernel<R, 16>);
-  const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
-  return e ? e : kernel_attrs(fn, g);
+  if (R::kind != 1 && !R::harder && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g);
+  return plan_lane<R>(n_envs, cus, g);
 }
 
 int PBG_FN(launch_step_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if (launch_team<R>(B, io, scratch, g, s)) return (int)hipGetLastError();
   if (launch_gang<R>(B, io, scratch, g, s)) return (int)hipGetLastError();
-  const dim3 grid(blocks(B.n, g.block)), blk(g.block);
-  if (g.block == 64) hipLaunchKernelGGL((step_kernel<R, 64>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
-  else if (g.block == 32) hipLaunchKernelGGL((step_kernel<R, 32>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
-  else hipLaunchKernelGGL((step_kernel<R, 16>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows);
-  return (int)hipGetLastError();
+  return launch_lane<R>(B, io, scratch, g, s);
 }
 
 int PBG_FN(launch_reset_)(const Buffers& B, const ResetIO& io, hipStream_t s) {

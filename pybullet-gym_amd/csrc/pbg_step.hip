@@ -1287,6 +1287,7 @@ struct PackIn {
   double potential_old, initial_z;  // initial_z NaN: take from this calc_state
   double target_x = PBG_WALK_TARGET_X, target_y = PBG_WALK_TARGET_Y;  // robot.walk_target_x/y
   double avel[3] = {0.0, 0.0, 0.0};  // base angular velocity (MuJoCo-observation walkers)
+  double head_z = 0.0;               // Atlas: the head part's height (alive_bonus)
   double env_dt = R::dt_sub * R::substeps;  // Scene.dt (SimP::env_dt; the pack kernel: defaults)
 };
 struct PackOut {
@@ -1418,6 +1419,11 @@ PBG_DEV void walker_pack(const PackIn<R>& in, const float* act, float* obs, Pack
   } else if constexpr (R::alive == 2) {  // Ant :137-138
     const double z = (double)s0 + z0;
     alive = z > 0.26 ? 1.0 : -1.0;
+  } else if constexpr (R::alive == 13) {  // Atlas :313-324: +4 - knees at limit if head z > 1.3
+    int knees = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) knees += fabsf(j[2 * R::knee_obs[k]]) > PBG_JOINT_AT_LIMIT;
+    alive = in.head_z > 1.3 ? (double)(4 - knees) : -1.0;
   } else {  // Humanoid :191-192; np.float32 + 0.8 stays float32 (NEP 50)
     const float z = s0 + (float)z0;
     alive = z > 0.78f ? 2.0 : -1.0;
@@ -1744,32 +1750,42 @@ PBG_DEV void pendulum_obs(const double* jq, const double* jqd, const double* tip
 }
 #pragma clang fp contract(on)
 
-// M3 -> quaternion (x,y,z,w) in float64
-PBG_DEV void m3_to_quat_d(const m3& mf, double* q) {
-  double m[9];
-#pragma unroll
-  for (int i = 0; i < 9; i++) m[i] = mf.m[i];
-  const double t = m[0] + m[4] + m[8];
-  if (t > 0) {
-    const double s = sqrt(t + 1.0) * 2;
-    q[3] = 0.25 * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+
+// M3 -> quaternion (x,y,z,w): the float32 rotation matrix converted in float32 (one IEEE
+// reciprocal per branch) and widened.  The matrix carries float32 rounding already, so the float64
+// conversion (round 2: float64, four branches) bought no accuracy; the float64 sqrt and four float64 divisions per
+// branch were 8-34 % of the gang walkers' step (r03 stamps).
+PBG_DEV void m3_to_quat_f(const m3& mf, double* q) {
+  const float* m = mf.m;
+  const float t = m[0] + m[4] + m[8];
+  float x, y, z, w;
+  if (t > 0.f) {
+    const float s = sqrtf(t + 1.f) * 2.f, r = 1.f / s;
+    w = 0.25f * s; x = (m[7] - m[5]) * r; y = (m[2] - m[6]) * r; z = (m[3] - m[1]) * r;
   } else if (m[0] > m[4] && m[0] > m[8]) {
-    const double s = sqrt(1.0 + m[0] - m[4] - m[8]) * 2;
-    q[3] = (m[7] - m[5]) / s; q[0] = 0.25 * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+    const float s = sqrtf(1.f + m[0] - m[4] - m[8]) * 2.f, r = 1.f / s;
+    w = (m[7] - m[5]) * r; x = 0.25f * s; y = (m[1] + m[3]) * r; z = (m[2] + m[6]) * r;
   } else if (m[4] > m[8]) {
-    const double s = sqrt(1.0 + m[4] - m[0] - m[8]) * 2;
-    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = 0.25 * s; q[2] = (m[5] + m[7]) / s;
+    const float s = sqrtf(1.f + m[4] - m[0] - m[8]) * 2.f, r = 1.f / s;
+    w = (m[2] - m[6]) * r; x = (m[1] + m[3]) * r; y = 0.25f * s; z = (m[5] + m[7]) * r;
   } else {
-    const double s = sqrt(1.0 + m[8] - m[0] - m[4]) * 2;
-    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = 0.25 * s;
+    const float s = sqrtf(1.f + m[8] - m[0] - m[4]) * 2.f, r = 1.f / s;
+    w = (m[3] - m[1]) * r; x = (m[2] + m[6]) * r; y = (m[5] + m[7]) * r; z = 0.25f * s;
   }
+  q[0] = x; q[1] = y; q[2] = z; q[3] = w;
 }
 
 // Gather pack inputs from the physical state (what pybullet's queries would return).
-template <class R>
-PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
+// st(integral_constant<int, i>): diagnostic phase stamps between the parts (no-op by default)
+struct NoStamp {
+  template <class C>
+  PBG_DEV void operator()(C) const {}
+};
+template <class R, class St = NoStamp>
+PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in, St st = St()) {
   Kin<R> k;
   fk_pos<R>(s, k);
+  st(std::integral_constant<int, 14>{});
   int np = 0;
 #pragma unroll
   for (int p = 0; p < R::NP; p++) {
@@ -1785,9 +1801,11 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in) {
 #pragma unroll
     for (int i = 0; i < 4; i++) in.quat[i] = s.bq[i];
   } else {
-    m3_to_quat_d(k.Rm[b], in.quat);
+    m3_to_quat_f(k.Rm[b], in.quat);
   }
+  st(std::integral_constant<int, 15>{});
   in.pos[0] = k.c[b].x; in.pos[1] = k.c[b].y; in.pos[2] = k.c[b].z;
+  if constexpr (R::head_link >= 0) in.head_z = k.c[R::head_link + 1].z;
   // robot_body COM velocity
   f3 vel;
   if constexpr (b == 0) {
@@ -1844,10 +1862,11 @@ PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
   pendulum_obs<R>(jq, jqd, tip, obs, po);
 }
 
-// epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e]
-template <class R>
+// epi: resets of env e so far (the Philox counter); the caller bumps B.episode[e].
+// Q = 4: the pack's transcendentals dealt over a DPP quad (quad / gang kernels, `lane`).
+template <class R, int Q = 1>
 PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                           double& pot, float& z0, uint32_t epi, Flag& fl, HarderBk* hb = nullptr) {
+                           double& pot, float& z0, uint32_t epi, Flag& fl, HarderBk* hb = nullptr, int lane = 0) {
   snapshot_state<R>(s);
   if (init_q) {
 #pragma unroll
@@ -1892,7 +1911,7 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
     hb->frame = 0; hb->onground = 0; hb->crawl_start = __builtin_nan(""); hb->crawl_ignored = 0.0;
   }
   if constexpr (R::kind == 3) mujoco3d_pack<R>(in, nullptr, obs, po);
-  else flag_pack<R>(in, nullptr, obs, po, fl, draw, 0, hb);
+  else flag_pack<R, Q>(in, nullptr, obs, po, fl, draw, lane, hb);
   if constexpr (R::harder) po.potential = harder_potential(*hb, po.potential, po.body_xyz[2]);  // env_bases.py:70
   pot = po.potential;
   z0 = (float)po.initial_z;
@@ -2085,6 +2104,7 @@ __global__ __launch_bounds__(64) void pack_kernel(int n, const double* __restric
     in.feet_new = fn;
     in.potential_old = r[o_pot];
     in.initial_z = r[o_pot + 1];
+    if constexpr (R::alive == 13) in.head_z = r[o_pot + 3];  // Atlas
     if constexpr (R::kind == 3) {
 #pragma unroll
       for (int i = 0; i < 3; i++) in.avel[i] = r[o_pot + 3 + i];  // base angular velocity

@@ -73,6 +73,14 @@ class MJCFBasedRobot(XmlBasedRobot):
         self.model_xml = model_xml
 
 
+class URDFBasedRobot(XmlBasedRobot):
+    """robot_bases.py:132-175 (self_collision False, floating base)."""
+
+    def __init__(self, model_urdf, robot_name, action_dim, obs_dim, self_collision=False):
+        XmlBasedRobot.__init__(self, robot_name, action_dim, obs_dim, self_collision)
+        self.model_urdf = model_urdf
+
+
 class WalkerBase(XmlBasedRobot):
     """robot_locomotors.py:7-79 constants (target, power)."""
 
@@ -87,7 +95,8 @@ def _robot_class(key, base_cls):
     spec = _robots.spec_for(key)
 
     walker = spec.kind in (_robots.KIND_WALKER, _robots.KIND_MUJOCO_PLANAR, _robots.KIND_MUJOCO_3D)
-    bases = (WalkerBase, MJCFBasedRobot) if walker else (MJCFBasedRobot,)
+    xml = URDFBasedRobot if spec.urdf else MJCFBasedRobot
+    bases = (WalkerBase, xml) if walker else (xml,)
 
     class _R(*bases):
         foot_list = list(spec.foot_list)
@@ -95,8 +104,8 @@ def _robot_class(key, base_cls):
         def __init__(self):
             if walker:
                 WalkerBase.__init__(self, power=spec.power)
-            MJCFBasedRobot.__init__(self, spec.mjcf, spec.robot_name, action_dim=spec.action_dim,
-                                    obs_dim=spec.obs_dim)
+            xml.__init__(self, spec.urdf or spec.mjcf, spec.robot_name, action_dim=spec.action_dim,
+                         obs_dim=spec.obs_dim)
             self.spec = spec
 
     _R.__name__ = base_cls
@@ -110,6 +119,7 @@ Ant = _robot_class("ant", "Ant")                             # :130-138
 Humanoid = _robot_class("humanoid", "Humanoid")              # :141-192
 HumanoidFlagrun = _robot_class("humanoid_flagrun", "HumanoidFlagrun")  # :195-226
 HumanoidFlagrunHarder = _robot_class("humanoid_flagrun_harder", "HumanoidFlagrunHarder")  # :229-302
+Atlas = _robot_class("atlas", "Atlas")                                                     # :305-341
 HopperMuJoCo = _robot_class("hopper_mujoco", "Hopper")                # mujoco/robot_locomotors.py:82-121
 Walker2DMuJoCo = _robot_class("walker2d_mujoco", "Walker2D")          # :124-164
 HalfCheetahMuJoCo = _robot_class("halfcheetah_mujoco", "HalfCheetah")  # :167-207
@@ -310,6 +320,18 @@ class HumanoidFlagrunHarderBulletEnv(HumanoidBulletEnv):
         HumanoidBulletEnv.__init__(self, HumanoidFlagrunHarder(), render, device)
 
 
+class AtlasBulletEnv(WalkerBaseBulletEnv):
+    """gym_locomotion_envs.py:181-191: the Atlas URDF robot (30 actuated joints, power 2.9),
+    StadiumScene with 8 sub-steps of 0.0165/8 s; alive_bonus +4 minus the knees at their limit
+    while the head is above 1.3 m, else -1 (robot_locomotors.py:313-324); runs on the gang
+    kernel."""
+    env_id = "AtlasPyBulletEnv-v0"
+
+    def __init__(self, render=False, device="cuda:0"):
+        self.robot = Atlas()
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+
+
 class WalkerBaseMuJoCoEnv(WalkerBaseBulletEnv):
     """envs/mujoco/gym_locomotion_envs.py:8-118 (MuJoCo-style observations on the same
     pybullet physics)."""
@@ -436,6 +458,7 @@ ENV_CLASSES = {
     "HumanoidPyBulletEnv-v0": HumanoidBulletEnv,
     "HumanoidFlagrunPyBulletEnv-v0": HumanoidFlagrunBulletEnv,
     "HumanoidFlagrunHarderPyBulletEnv-v0": HumanoidFlagrunHarderBulletEnv,
+    "AtlasPyBulletEnv-v0": AtlasBulletEnv,
     "HopperMuJoCoEnv-v0": HopperMuJoCoEnv,
     "Walker2DMuJoCoEnv-v0": Walker2DMuJoCoEnv,
     "HalfCheetahMuJoCoEnv-v0": HalfCheetahMuJoCoEnv,

@@ -66,6 +66,8 @@ JOINT_FIXED = 4      # pybullet.JOINT_FIXED
 
 GEOM_SPHERE = 0
 GEOM_CAPSULE = 1
+GEOM_BOX = 2       # URDF robots (urdf.py): half extents + rotation in the link frame
+GEOM_CYLINDER = 3  # URDF robots: a Z cylinder, p0 / p1 its cap centres
 
 FLOOR_FRICTION = 0.8  # scene_stadium.py:33
 
@@ -130,6 +132,8 @@ class Geom:
     contype: int
     conaffinity: int
     mass: float = 0.0
+    half: Optional[np.ndarray] = None  # box / cylinder (urdf.py): half extents in the geom frame
+    rot: Optional[np.ndarray] = None   # box / cylinder: geom frame in the link frame
 
 
 @dataclass
@@ -154,6 +158,7 @@ class Link:
     geoms: List[Geom] = field(default_factory=list)
     body: str = ""
     dof: int = -1             # joint dof index (0..NJ-1) or -1 for fixed
+    max_velocity: float = 0.0  # getJointInfo maxVelocity (URDF <limit velocity>; MJCF joints: 0)
 
 
 @dataclass

@@ -29,6 +29,7 @@ KIND_MUJOCO_3D = 3      # envs/mujoco Ant / Humanoid: qpos[2:]/qvel (+ zero padd
 ALIVE_MJ_HOPPER = 10    # mujoco/gym_locomotion_envs.py:127-137 (height > -0.3, |ang| < .2)
 ALIVE_MJ_WALKER = 11    # :171-181 (1 > height > -0.2, -1 < ang < 1)
 ALIVE_MJ_CHEETAH = 12   # :214-222 (never done, no alive bonus)
+ALIVE_ATLAS = 13        # robot_locomotors.py:313-324 (+4 - knees at limit if head z > 1.3 else -1)
 
 
 @dataclass
@@ -57,6 +58,10 @@ class RobotSpec:
     reset_offset: float = 0.0                                    # swingup hinge 3.1415 + u
     flagrun: bool = False                                        # HumanoidFlagrun walk target
     harder: bool = False                                         # HumanoidFlagrunHarder attacking cube
+    urdf: Optional[str] = None                                   # URDF asset under assets/robots (Atlas)
+    base_pos: Optional[List[float]] = None                       # reset snapshot base COM (URDF robots)
+    head: Optional[str] = None                                   # Atlas alive_bonus: the head part
+    knees: Optional[List[str]] = None                            # Atlas alive_bonus: the knee joints
     power_cost: float = 0.0                                      # MuJoCo planar: coef of sum(a^2)
     qvel_clip: float = 0.0                                       # MuJoCo planar: obs qvel clip (0: none)
 
@@ -167,6 +172,16 @@ _add(RobotSpec("HumanoidFlagrunHarderPyBulletEnv-v0", "humanoid_flagrun_harder",
                power_coef=dict(SPECS["humanoid"].power_coef), initial_z=0.8,
                electricity_cost=4.25 * -2.0, stall_torque_cost=4.25 * -0.1, flagrun=True, harder=True))
 
+# Atlas: robot_locomotors.py:305-341 (URDFBasedRobot atlas_v4_with_multisense.urdf, pelvis,
+# power 2.9, robot_specific_reset -> reset_pose([0, 0, 0 + 1.0], yaw 0: random_yaw False),
+# initial_z 1.5, alive_bonus from the head height and the knees), gym_locomotion_envs.py:181-191
+# (StadiumScene timestep 0.0165/8, frame_skip 8), envs/__init__.py:99-103
+_add(RobotSpec("AtlasPyBulletEnv-v0", "atlas", "", "pelvis", action_dim=30, obs_dim=70, kind=KIND_WALKER,
+               power=2.9, foot_list=["r_foot", "l_foot"], alive=ALIVE_ATLAS, initial_z=1.5,
+               timestep=0.0165 / 8, frame_skip=8, self_collision=False,
+               urdf="atlas/atlas_description/atlas_v4_with_multisense.urdf", base_pos=[0.0, 0.0, 1.0],
+               head="head", knees=["l_leg_kny", "r_leg_kny"]))
+
 ENV_IDS = {s.env_id: s for s in SPECS.values()}
 
 
@@ -202,3 +217,15 @@ def add_to_scene_order(model: mjcf.RobotModel, robot_name: str):
 
 def reference_asset_dir() -> str:
     return os.path.join("/root/reference", "pybulletgym", "envs", "assets", "mjcf")
+
+
+def reference_robot_dir() -> str:
+    return os.path.join("/root/reference", "pybulletgym", "envs", "assets", "robots")
+
+
+def compile_model(spec: RobotSpec, asset_dir: str = None):
+    """The spec's robot compiled from its reference asset (MJCF, or URDF for Atlas)."""
+    if spec.urdf:
+        from . import urdf
+        return urdf.compile_urdf(os.path.join(reference_robot_dir(), spec.urdf), spec.key, spec.base_pos)
+    return mjcf.compile_mjcf(os.path.join(asset_dir or reference_asset_dir(), spec.mjcf), spec.key)

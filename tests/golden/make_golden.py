@@ -54,6 +54,7 @@ ROBOTS = {
     "humanoid_mujoco": ("pybulletgym.envs.mujoco.gym_locomotion_envs", "HumanoidMuJoCoEnv"),
     "double_pendulum_mujoco": ("pybulletgym.envs.mujoco.gym_pendulum_envs", "InvertedDoublePendulumMuJoCoEnv"),
     "humanoid_flagrun_harder": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "HumanoidFlagrunHarderBulletEnv"),
+    "atlas": ("pybulletgym.envs.roboschool.gym_locomotion_envs", "AtlasBulletEnv"),
 }
 CUBE_UID = 6
 
@@ -218,6 +219,8 @@ class FakeClient:
     def loadSDF(self, path): return (self.floor_uid,)
     def loadMJCF(self, path, flags=0): return (self.robot_uid,)
     def loadURDF(self, path, pos=None, *a, **k):
+        if "atlas" in str(path):  # URDFBasedRobot.reset (robot_bases.py:145-164)
+            return self.robot_uid
         if "cube" in str(path):  # HumanoidFlagrunHarder's attacking cube (gym_utils.get_cube)
             self.cube_pose = (tuple(float(v) for v in pos), (0.0, 0.0, 0.0, 1.0))
             return CUBE_UID
@@ -247,7 +250,8 @@ class FakeClient:
     def getJointInfo(self, uid, j):
         t = self.t
         lo, hi = t["_lo"][j], t["_hi"][j]
-        return (j, t["_jname"][j].encode(), t["link_jtype"][j], 7 + j, 6 + j, 1, 0.0, 0.0, lo, hi, 0.0, 0.0,
+        vmax = float(t.get("link_max_velocity", [0.0] * t["NL"])[j])  # URDF <limit velocity> (Atlas)
+        return (j, t["_jname"][j].encode(), t["link_jtype"][j], 7 + j, 6 + j, 1, 0.0, 0.0, lo, hi, 0.0, vmax,
                 t["link_name"][j].encode(), (0.0, 0.0, 1.0), (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), t["link_parent"][j])
 
     # --- state queries
@@ -297,9 +301,9 @@ def load_tables(key):
     import importlib
     sys.path.insert(0, REPO)
     pkg = importlib.import_module("pybulletgym_amd")
-    from pybulletgym_amd import mjcf, robots
+    from pybulletgym_amd import robots
     spec = robots.spec_for(key)
-    model = mjcf.compile_mjcf(os.path.join(robots.reference_asset_dir(), spec.mjcf), key)
+    model = robots.compile_model(spec)
     t["_jname"] = [l.joint_name for l in model.links]
     return t
 
@@ -320,7 +324,7 @@ def generate(key, episodes=3, steps=40, seed=1234):
     rec = {k: [] for k in ("kind", "part_xyz", "n_parts", "body_quat", "body_pos", "body_vel", "jq", "jqd",
                            "feet_prev", "feet_new", "act", "potential_old", "initial_z_in", "obs", "reward",
                            "done", "potential", "feet_out", "initial_z_out", "rewards", "flag_in", "flag_out",
-                           "body_avel", "harder_in", "harder_out")}
+                           "body_avel", "harder_in", "harder_out", "head_z")}
     part_names = []
     captured = {}
     calc_cls = type(robot)
@@ -434,6 +438,8 @@ def generate(key, episodes=3, steps=40, seed=1234):
                 rec["harder_out"].append([float(robot.frame), float(robot.on_ground_frame_counter),
                                           np.nan if cs is None else float(cs), float(robot.crawl_ignored_potential),
                                           1.0 if dr else 0.0] + (list(pos[0]) + list(vel[0]) if dr else [np.nan] * 6))
+            if t.get("head_link", -1) >= 0:  # Atlas alive_bonus: the head part's height (getLinkState[0])
+                rec["head_z"].append(float(fake.link_pos[t["head_link"]][2]))
             rec["initial_z_out"].append(float(robot.initial_z))
             part_names.append(captured["part_names"])
         elif t["kind"] == 2:
@@ -458,6 +464,8 @@ def generate(key, episodes=3, steps=40, seed=1234):
         state = {"ep": 0}
         fake.z_hook = lambda r: (r.uniform(0.05, 0.79) if state["ep"] == episodes - 1 or r.random() < 0.25
                                  else r.uniform(0.81, 1.5))
+    if key == "atlas":  # head above 1.3 m (alive +4 - knees at limit) in most calls
+        fake.z_hook = lambda r: r.uniform(0.3, 1.2) if r.random() < 0.25 else r.uniform(1.6, 2.4)
     for ep in range(episodes):
         if t.get("harder"):
             state["ep"] = ep

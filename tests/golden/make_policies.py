@@ -34,6 +34,7 @@ POLICIES = {
     "HumanoidPyBulletEnv-v0": "enjoy_TF_HumanoidPyBulletEnv_v0_2017may.py",
     "HumanoidFlagrunPyBulletEnv-v0": "enjoy_TF_HumanoidFlagrunPyBulletEnv_v0_2017may.py",
     "HumanoidFlagrunHarderPyBulletEnv-v0": "enjoy_TF_HumanoidFlagrunHarderPyBulletEnv_v0_2017may.py",
+    "AtlasPyBulletEnv-v0": "enjoy_TF_AtlasPyBulletEnv_v0_2017jul.py",
 }
 NAMES = ["weights_dense1_w", "weights_dense1_b", "weights_dense2_w", "weights_dense2_b",
          "weights_final_w", "weights_final_b"]

@@ -34,6 +34,7 @@ POLICY_FILES = {
     "HumanoidPyBulletEnv-v0": "policy_humanoid.npz",
     "HumanoidFlagrunPyBulletEnv-v0": "policy_humanoidflagrun.npz",
     "HumanoidFlagrunHarderPyBulletEnv-v0": "policy_humanoidflagrunharder.npz",
+    "AtlasPyBulletEnv-v0": "policy_atlas.npz",
 }
 MAX_STEPS = 1000  # TimeLimit (envs/__init__.py max_episode_steps)
 

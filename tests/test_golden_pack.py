@@ -9,7 +9,7 @@ import oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 WALKERS = ["hopper", "halfcheetah", "ant", "humanoid", "walker2d", "humanoid_flagrun", "ant_mujoco",
-           "humanoid_mujoco", "humanoid_flagrun_harder"]
+           "humanoid_mujoco", "humanoid_flagrun_harder", "atlas"]
 
 
 def load(key):
@@ -40,7 +40,8 @@ def test_oracle_pack_bit_exact(key):
                           g["potential_old"][i], g["initial_z_in"][i],
                           flag=g["flag_in"][i] if "flag_in" in g.files else None,
                           body_avel=g["body_avel"][i] if "body_avel" in g.files else None,
-                          harder=g["harder_in"][i] if "harder_in" in g.files else None)
+                          harder=g["harder_in"][i] if "harder_in" in g.files else None,
+                          head_z=g["head_z"][i] if "head_z" in g.files else 0.0)
         ref_obs = g["obs"][i].astype(np.float32)
         if "flag_out" in g.files:  # HumanoidFlagrun: target and flag_timeout after calc_state
             np.testing.assert_array_equal(out["flag_out"], g["flag_out"][i], err_msg=f"call {i}")

@@ -30,7 +30,7 @@ ENVS = ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPy
         "InvertedPendulumSwingupPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
         "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0",
         "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "InvertedDoublePendulumMuJoCoEnv-v0",
-        "HumanoidFlagrunHarderPyBulletEnv-v0"]
+        "HumanoidFlagrunHarderPyBulletEnv-v0", "AtlasPyBulletEnv-v0"]
 KEY = {e: oracle.ENV_KEYS[e] for e in ENVS}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -82,6 +82,8 @@ def test_device_pack_matches_reference_golden(env_id):
             rec[i, o + 3:o + 8] = g["flag_in"][i]
         if "harder_in" in g.files:  # HumanoidFlagrunHarder: bookkeeping + the recorded launch draws
             rec[i, o + 8:o + 17] = g["harder_in"][i]
+        if "head_z" in g.files:  # Atlas: the head part's height
+            rec[i, o + 3] = g["head_z"][i]
         if "body_avel" in g.files:  # MuJoCo Ant / Humanoid: torso angular velocity
             rec[i, o + 3:o + 6] = g["body_avel"][i]
     out = pack(env_id, torch.from_numpy(rec).cuda()).cpu().numpy()

@@ -69,13 +69,16 @@ def test_default_sim_params_are_the_reference_scenes():
     """pbg_default_sim_params (host only) returns the scene each env builds: StadiumScene(gravity
     9.8, timestep 0.0165/4, frame_skip 4) for the walkers (roboschool and MuJoCo
     gym_locomotion_envs.py:18-19), SingleRobotEmptyScene(9.8, 0.0165, 1) for the pendulums
-    (gym_pendulum_envs.py:14,48), numSolverIterations 5 (scene_bases.py:65)."""
+    (gym_pendulum_envs.py:14,48), StadiumScene(9.8, 0.0165/8, 8) for Atlas
+    (gym_locomotion_envs.py:187), numSolverIterations 5
+    (scene_bases.py:65)."""
     for env_id in _native.ROBOT_IDS:
         p = _native.default_sim_params(env_id)
         pend = "Pendulum" in env_id
         assert p.gravity == 9.8 and p.solver_iterations == 5, env_id
-        assert p.frame_skip == (1 if pend else 4), env_id
-        assert p.timestep == (0.0165 if pend else 0.0165 / 4), env_id
+        fs = 1 if pend else (8 if "Atlas" in env_id else 4)
+        assert p.frame_skip == fs, env_id
+        assert p.timestep == 0.0165 / fs, env_id
         assert 0.0 <= p.contact_erp <= 1.0 and 0.0 <= p.joint_limit_erp <= 1.0
     over = _native.sim_params("AntPyBulletEnv-v0", {"gravity": 1.6, "frame_skip": 2})
     assert (over.gravity, over.frame_skip, over.solver_iterations) == (1.6, 2, 5)

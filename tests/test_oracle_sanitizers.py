@@ -14,7 +14,7 @@ ORACLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"
 def test_oracle_under_asan_ubsan():
     subprocess.check_call(["make", "-s", "-C", ORACLE, "sanitize"])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
-               OMP_NUM_THREADS="2")
+               OMP_NUM_THREADS="2", OMP_STACKSIZE="64M")  # ASan redzones inflate the Atlas-sized frames
     out = subprocess.run([os.path.join(ORACLE, "_san", "pbg_oracle_san"), "12"], capture_output=True, text=True,
                          timeout=600, env=env)
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-4000:])

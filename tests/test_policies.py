@@ -19,7 +19,7 @@ import policies
 # the band pins what they do now -- a positive return where random actions score ~ -28, and
 # episodes of >= 45 steps (random: ~30) -- so a dynamics regression on the hardest robot shows.
 MIN_LEN = {"HumanoidPyBulletEnv-v0": 45, "HumanoidFlagrunPyBulletEnv-v0": 45, "HalfCheetahPyBulletEnv-v0": 900,
-           "HumanoidFlagrunHarderPyBulletEnv-v0": 220}
+           "HumanoidFlagrunHarderPyBulletEnv-v0": 220, "AtlasPyBulletEnv-v0": 15}
 BANDS = {
     "InvertedPendulumPyBulletEnv-v0": (8, 999.0, 10.0),
     "InvertedPendulumSwingupPyBulletEnv-v0": (8, 700.0, None),  # swings up and balances (random: -920)
@@ -35,6 +35,10 @@ BANDS = {
     # Band: mean return -268 over 8 oracle episodes (-211 over 64; random actions -314), length
     # ~260 steps.
     "HumanoidFlagrunHarderPyBulletEnv-v0": (8, -290.0, None),
+    # Atlas: the roboschool-trained weights (enjoy_TF_AtlasPyBulletEnv_v0_2017jul.py) command
+    # |a| up to ~40 here (apply_action clips, electricity does not) and fall in ~25 steps: mean
+    # return -795 over 8 oracle episodes (random actions +16).  A pipeline regression band only.
+    "AtlasPyBulletEnv-v0": (8, -1000.0, None),
 }
 
 

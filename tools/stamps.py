@@ -13,8 +13,9 @@ names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact row
          "store", "-", "PGS limit rows", "PGS normals", "PGS frictions"]
 gang_names = {0: "dist: forward levels", 1: "dist: inertia + motion", 2: "dist: composites", 3: "dist: M + bias",
               10: "replicated Cholesky + stage", 4: "detect",
-              11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 12: "pack: gather (FK, parts)",
-              8: "pack: walker pack (float64)", 13: "auto-reset (snapshot, noise, FK, pack)", 9: "store"}
+              11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 13: "pack: bookkeeping loads",
+              14: "pack: gather FK", 15: "pack: gather quat", 12: "pack: gather vel, parts, joints",
+              8: "pack: walker pack (float64)", 9: "store (+ auto-reset)"}
 AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
 # ENV:N[:GANG_DIST]  (GANG_DIST 0/1 forces the gang kernel's replicated / distributed dynamics)
 for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
