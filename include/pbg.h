@@ -44,7 +44,7 @@ typedef struct {
                             6 pendulum_swingup, 7 double_pendulum, 8 humanoid_flagrun,
                             9 hopper_mujoco, 10 walker2d_mujoco, 11 halfcheetah_mujoco,
                             12 ant_mujoco, 13 humanoid_mujoco, 14 double_pendulum_mujoco,
-                            15 humanoid_flagrun_harder */
+                            15 humanoid_flagrun_harder, 16 atlas */
   int n_envs;
   int action_dim;        /* action_space.shape[0]   (robot_bases.py:24-25) */
   int obs_dim;           /* observation_space.shape[0] (robot_bases.py:26-27) */
@@ -103,7 +103,8 @@ typedef struct {
 /* Scene / World parameters (scene_bases.py:8-18 Scene(gravity, timestep, frame_skip), 58-73
  * World: setGravity, numSolverIterations, numSubSteps).  pbg_default_sim_params fills the values
  * the reference's env constructs its scene with (gym_locomotion_envs.py:18-19 StadiumScene(9.8,
- * 0.0165/4, 4); gym_pendulum_envs.py:14 SingleRobotEmptyScene(9.8, 0.0165, 1); iterations 5,
+ * 0.0165/4, 4); Atlas StadiumScene(9.8, 0.0165/8, 8), gym_locomotion_envs.py:187;
+ * gym_pendulum_envs.py:14 SingleRobotEmptyScene(9.8, 0.0165, 1); iterations 5,
  * scene_bases.py:65) plus the solver ERPs the kernels use; pbg_create_ex takes a modified copy.
  * An env step is frame_skip sub-steps of `timestep` seconds; the potential divides by
  * Scene.dt = timestep * frame_skip (scene_bases.py:17); HumanoidFlagrun's flag timeout is
@@ -127,8 +128,9 @@ int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out);
  * "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "InvertedPendulumSwingupPyBulletEnv-v0",
  * "InvertedDoublePendulumPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0",
  * "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0", "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0",
- * "InvertedDoublePendulumMuJoCoEnv-v0", "HumanoidFlagrunHarderPyBulletEnv-v0" (the short robot
- * names are accepted too). */
+ * "InvertedDoublePendulumMuJoCoEnv-v0", "HumanoidFlagrunHarderPyBulletEnv-v0",
+ * "AtlasPyBulletEnv-v0" (gym_locomotion_envs.py:181-188) (the short robot names are accepted
+ * too). */
 int pbg_create(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset, pbg_handle** out);
 /* pbg_create with test / diagnostic launch options (opts NULL = pbg_create). */
 int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
