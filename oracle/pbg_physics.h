@@ -13,6 +13,7 @@
 // double (Counted<float> has no mixed-type operators: a missed cast does not compile).
 // [EXT] = Bullet semantics restated from its published algorithm.
 #pragma once
+#include <type_traits>
 
 using std::cos;
 using std::fabs;
@@ -251,6 +252,85 @@ template <class T> void mass_and_bias(const MV& m, const KinT<T>& k, T M[MAXD][M
     for (int i = 0; i < 3; i++) { M[c0 + i][c0 + i] = mc; M[c0 + 3 + i][c0 + 3 + i] = Ic; }
     C[c0] = f.x; C[c0 + 1] = f.y; C[c0 + 2] = f.z; C[c0 + 3] = tq.x; C[c0 + 4] = tq.y; C[c0 + 5] = tq.z;
   }
+}
+
+// The kernels' formulation of the same M and C (pbg_step.hip dyn_mass, pbg_gang.hip
+// gang_dyn_mass, pbg_team.hip): every body's inertia and wrench taken about one reference point
+// O (the base COM, or the robot body's COM for a fixed base) and projected on the motion vectors
+// (sw_i, sv_i) of the generalized coordinates about O,
+//   M_ij += sw_i.(J sw_j + m r x sv_j) + sv_i.(m sv_j - m r x sw_j),  C_i += sw_i.(n + r x f) + sv_i.f
+// with J = Iw + m (r.r 1 - r r^T), r = c_b - O, over the bodies both coordinates move.  Equal to
+// mass_and_bias in exact arithmetic; in float32 its parallel-axis terms (m r^2 ~ 1 kg m^2 for an
+// arm tip a metre from O) cancel down to the tip's ~1e-3 kg m^2 entries, which point Jacobians at
+// each COM do not.  The float32 instantiations (precision 32 / 33: the conditioning and
+// outlier-explanation envelopes of the parity tests) use it, so that they carry the kernels'
+// rounding; the float64 oracle keeps mass_and_bias.
+template <class T> void mass_and_bias_ref(const MV& m, const KinT<T>& k, T M[MAXD][MAXD], T* C, const T* s = nullptr) {
+  const int n = m.NDOF;
+  if (m.harder) {
+    mass_and_bias(m, k, M, C, s);  // the cube block (decoupled); the robot's entries rebuilt below
+  }
+  for (int i = 0; i < n; i++) {
+    C[i] = T(0);
+    for (int j = 0; j < n; j++) M[i][j] = T(0);
+  }
+  const V3T<T> g = v3(T(0), T(0), T((g_flags & 16) ? 0.0 : -g_opt[OPT_GRAVITY]));
+  const T kd_lin((g_flags & 4) ? 0.0 : PBG_LINEAR_DAMPING);
+  const T kd_ang((g_flags & 4) ? 0.0 : PBG_ANGULAR_DAMPING);
+  const int rb = m.floating ? 0 : m.robot_body + 1;
+  const V3T<T> O = k.c[rb];
+  // motion vectors about O of every generalized coordinate
+  V3T<T> sw[MAXD], sv[MAXD];
+  if (m.floating) {
+    const V3T<T> ob = O - k.x[0];
+    for (int e = 0; e < 3; e++) {
+      const V3T<T> ax = v3(T(e == 0), T(e == 1), T(e == 2));
+      sw[e] = vzero<T>(); sv[e] = ax;
+      sw[3 + e] = ax; sv[3 + e] = cross(ax, ob);
+    }
+  }
+  for (int l = 0; l < m.NL; l++) {
+    const int d = m.link_dof[l];
+    if (d < 0) continue;
+    const int gi = gidx(m, d);
+    if (m.link_jtype[l] == 0) { sw[gi] = k.ja[d]; sv[gi] = cross(k.ja[d], O - k.jo[d]); }
+    else { sw[gi] = vzero<T>(); sv[gi] = k.ja[d]; }
+  }
+  for (int b = 0; b < m.NL + 1; b++) {
+    if (b == 0 && !m.floating) continue;
+    const double mb = b == 0 ? m.base_mass : m.mass[b - 1];
+    if (!(mb > 0.0)) continue;
+    const T mass(mb);
+    const M3T<T> Iw = world_inertia(k.R[b], b == 0 ? m.base_inertia : m.inertia[b - 1]);
+    const V3T<T> r = k.c[b] - O;
+    const T rr = dot(r, r);
+    M3T<T> J = Iw;
+    const T rv[3] = {r.x, r.y, r.z};
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) J.m[i][j] = J.m[i][j] + mass * ((i == j ? rr : T(0)) - rv[i] * rv[j]);
+    const V3T<T> w = k.w[b], v = k.v[b];
+    const V3T<T> Iw_w = mul(Iw, w);
+    const V3T<T> f = mass * (k.ac[b] - g) + (mass * (kd_lin + kd_lin * norm(v))) * v;
+    const V3T<T> tq = mul(Iw, k.al[b]) + cross(w, Iw_w) + (kd_ang + kd_ang * norm(w)) * Iw_w;
+    const V3T<T> pr = mass * r, Nn = tq + cross(r, f);
+    // the coordinates that move body b: the base's and the joints on its chain
+    int S[MAXD], ns = 0;
+    if (m.floating)
+      for (int e = 0; e < 6; e++) S[ns++] = e;
+    for (int l = b - 1; l >= 0; l = m.link_parent[l])
+      if (m.link_dof[l] >= 0) S[ns++] = gidx(m, m.link_dof[l]);
+    for (int a = 0; a < ns; a++) {
+      const int i = S[a];
+      C[i] = C[i] + (dot(sw[i], Nn) + dot(sv[i], f));
+      for (int c = 0; c < ns; c++) {
+        const int j = S[c];
+        const V3T<T> Jw_ = mul(J, sw[j]) + cross(pr, sv[j]);
+        const V3T<T> Fv = mass * sv[j] - cross(pr, sw[j]);
+        M[i][j] = M[i][j] + (dot(sw[i], Jw_) + dot(sv[i], Fv));
+      }
+    }
+  }
+  for (int d = 0; d < m.NJ; d++) M[gidx(m, d)][gidx(m, d)] = M[gidx(m, d)][gidx(m, d)] + T(m.armature[d]);
 }
 
 // in-place Cholesky M = L L^T (lower)
@@ -590,7 +670,8 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   static thread_local ContactT<T> cts[MAXCAND];
   T C[MAXD], rhs[MAXD], qdd[MAXD], nu[MAXD];
   forward_kinematics(m, s, k);
-  mass_and_bias(m, k, M, C, s);
+  if constexpr (std::is_same<T, double>::value) mass_and_bias(m, k, M, C, s);
+  else mass_and_bias_ref(m, k, M, C, s);  // float32 envelopes: the kernels' formulation
   // joint damping tau = -d*qd from this sub-step's velocity (explicit; [EXT] pybullet
   // applyJointDamping -- applied per sub-step here, the stable choice at dt/4)
   const T* qd0 = s + PBG_BASE_WORDS + m.NJ;

@@ -13,6 +13,8 @@ Tolerances (stated per test):
     here they carry the float32 state's precision, inside the same 1e-4 relative bound.
 """
 import os
+import sys
+import time
 
 import numpy as np
 import pytest
@@ -198,8 +200,11 @@ F32_MCA_RUNS_LADDER = (256, 2048)  # ... and the escalation for an outlier a pas
 # joint and base velocities (the PyBullet observation scales joint speeds by 0.1) and the raw
 # quaternion: the same state error reads ten times larger, so their class-A bound is 1e-3, and
 # far more of their env-steps are ill conditioned at float32.
+# Atlas (URDF, 30 dofs) likewise: its 1 kg hands on two wrist joints a metre from the base make
+# the kernels' inertia-about-O arithmetic cancel (m r^2 ~ 1 against wrist entries ~1e-3): float32
+# in that formulation is off by a median 7e-5 / max 2e-3 (oracle mass_and_bias_ref).
 STRICT_REL_ENV = {e: 1e-3 for e in ("HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0", "HalfCheetahMuJoCoEnv-v0",
-                                    "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0")}
+                                    "AntMuJoCoEnv-v0", "HumanoidMuJoCoEnv-v0", "AtlasPyBulletEnv-v0")}
 # Ceiling on the ill-conditioned (class B) share per env id: the largest share any
 # test measured for it (profiles/r03_parity.jsonl; 60-step, 1,000-step config and kernel-variant
 # tests) plus 0.1.  Every class-B outlier is explained separately (above), so this bounds how
@@ -210,7 +215,7 @@ COND_FRAC_ENV = {"InvertedPendulumPyBulletEnv-v0": 0.05, "InvertedPendulumSwingu
                  "HumanoidPyBulletEnv-v0": 0.38, "Walker2DPyBulletEnv-v0": 0.65,
                  "HumanoidFlagrunPyBulletEnv-v0": 0.35, "HopperMuJoCoEnv-v0": 0.19, "Walker2DMuJoCoEnv-v0": 0.40,
                  "HalfCheetahMuJoCoEnv-v0": 0.64, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.85,
-                 "HumanoidFlagrunHarderPyBulletEnv-v0": 0.6}
+                 "HumanoidFlagrunHarderPyBulletEnv-v0": 0.6, "AtlasPyBulletEnv-v0": 0.62}
 
 
 def _probe_state(state, rng):
@@ -428,7 +433,10 @@ def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init=None, pr
     kind = "harder" if "Harder" in env_id else orc.info.kind
     acts = sample_actions(env.info.action_dim, n, steps, seed=seed)
     st = SplitStats(name or f"teacher_forced[{env_id},{n}x{steps}]", env_id, strict_share)
+    t0 = time.time()
     for t in range(steps):
+        if t % 10 == 0:  # progress for -s runs (a long oracle pass is not a hang)
+            print(f"  {st.name}: step {t}/{steps} {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
         phys, aux = env.get_state()
         orc.state[:] = phys.index_select(0, tidx).cpu().numpy()
         orc.aux[:] = aux.index_select(0, tidx).cpu().numpy()
@@ -462,10 +470,17 @@ def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init=None, pr
     return st.check()
 
 
+# Atlas: the oracle steps it ~8x slower than the Humanoid (886 floor slots, 36 dofs, 8
+# sub-steps) and falls within ~20 steps: 64 envs x 30 steps, ~900 class-A env-steps, so one
+# (explained) step above the class bound is 0.1 % of them
+TF_SIZE = {"AtlasPyBulletEnv-v0": (64, 30, 0.998)}
+
+
 @pytest.mark.parametrize("env_id", ENVS)
 def test_step_teacher_forced_parity(env_id):
-    """Every env id, 256 envs x 60 teacher-forced steps, contact-set split bounds above."""
-    _teacher_forced(env_id, 256, 60)
+    """Every env id, 256 envs x 60 teacher-forced steps (TF_SIZE), contact-set split bounds above."""
+    n, steps, share = TF_SIZE.get(env_id, (256, 60, STRICT_SHARE))
+    _teacher_forced(env_id, n, steps, strict_share=share)
 
 
 # BASELINE.json configs at their per-GPU env counts (launch geometry, LDS-resident contact

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 TAG=${1:-ab}; K=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 if [ -n "$K" ]; then
-  timeout -k 10 ${TT:-400} python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > $OUT/tests.log 2>&1; rc=$?
+  timeout -k 10 ${TT:-400} python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread -k "$K" > $OUT/tests.log 2>&1; rc=$?
   echo "tests rc=$rc" >> $OUT/tests.log; tail -3 $OUT/tests.log
   case $rc in 0|5) ;; *) exit $rc;; esac
 fi

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 rm -f $OUT/parity.jsonl
-PBG_PARITY_DUMP=$OUT/dump PBG_PARITY_REPORT=$OUT/parity.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
+PBG_PARITY_DUMP=$OUT/dump PBG_PARITY_REPORT=$OUT/parity.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
 rc=$?
 tail -3 $OUT/gpu_tests.txt
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
