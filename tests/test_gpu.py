@@ -209,6 +209,12 @@ STRICT_REL_ENV = {e: 1e-3 for e in ("HopperMuJoCoEnv-v0", "Walker2DMuJoCoEnv-v0"
 # test measured for it (profiles/r03_parity.jsonl; 60-step, 1,000-step config and kernel-variant
 # tests) plus 0.1.  Every class-B outlier is explained separately (above), so this bounds how
 # much of the comparison may fall outside the strict class.
+# Ceiling on the p99 of class B's GPU error over the oracle's own probe spread (SPREAD_RATIO by
+# default).  Atlas: the probes perturb the float64 oracle, whose point-Jacobian M has no
+# parallel-axis cancellation, so its spread misses the kernels' float32 rounding on the arm tips;
+# every class-B step above 10x the spread is still re-stepped and explained by the float32
+# envelope in the kernels' formulation (r03: 22 of 22, largest ratio 0.70), and the p99 is 17.7.
+SPREAD_P99_ENV = {"AtlasPyBulletEnv-v0": 25.0}
 COND_FRAC_ENV = {"InvertedPendulumPyBulletEnv-v0": 0.05, "InvertedPendulumSwingupPyBulletEnv-v0": 0.05,
                  "InvertedDoublePendulumPyBulletEnv-v0": 0.05, "InvertedDoublePendulumMuJoCoEnv-v0": 0.05,
                  "HopperPyBulletEnv-v0": 0.67, "HalfCheetahPyBulletEnv-v0": 0.26, "AntPyBulletEnv-v0": 0.51,
@@ -287,6 +293,7 @@ class SplitStats:
         self.strict_share = strict_share
         self.cond_frac = COND_FRAC_ENV.get(env_id, COND_FRAC)
         self.strict = STRICT_REL_ENV.get(env_id, STRICT_REL)
+        self.spread_p99 = SPREAD_P99_ENV.get(env_id, SPREAD_RATIO)
         self.name, self.n, self.nA, self.nB = name, 0, 0, 0
         self.errA, self.rewA, self.done_mis, self.cnt_mis = [], [], 0, 0
         self.maxB, self.maxC, self.ratios = 0.0, 0.0, []
@@ -379,7 +386,7 @@ class SplitStats:
         assert self.done_mis == 0 and self.cnt_mis == 0, rec
         assert self.nB / n <= self.cond_frac, rec
         if self.ratios:
-            assert rec["classB_ratio_to_oracle_spread_p50_p99_max"][1] <= SPREAD_RATIO, rec
+            assert rec["classB_ratio_to_oracle_spread_p50_p99_max"][1] <= self.spread_p99, rec
         assert fracC <= LOOSE_FRAC, rec
         return rec
 
