@@ -44,7 +44,7 @@ namespace pbg {
 // not fit, and one-wave workgroups (87 KB: one per CU) left three SIMDs of each CU idle
 // (4.72 -> 3.05 ms per step at 4,096 envs, A/B)
 template <class R>
-constexpr int gang_block() { return R::NS > 128 ? 128 : PBG_GANG_BLOCK; }
+constexpr int gang_block() { return PBG_GANG_BLOCK; }
 
 // bound_ctrl set: every permutation used here reads a valid lane, and with it the
 // compiler folds `x + mov_dpp(x)` into one v_add_f32_dpp (no mov, no DPP hazard nop).
@@ -83,9 +83,6 @@ struct GangTab {
   static constexpr int NS1 = R::NS > 0 ? R::NS : 1, NP1 = R::NPAIR > 0 ? R::NPAIR : 1;
   static constexpr int NG1 = R::NG > 0 ? R::NG : 1, NB = R::NL + 1;
   static constexpr int NL1 = Dims<R>::NLIM > 0 ? Dims<R>::NLIM : 1;
-  float slot[NS1][4];  // point (link frame) | radius
-  float slot_mu[NS1];
-  int slot_body[NS1];
   float gp0[NG1][4];   // capsule end 0 | radius
   float gp1[NG1][4];   // capsule end 1
   int geom_body[NG1];
@@ -93,7 +90,16 @@ struct GangTab {
   float pmu[NP1], pbound2[NP1];
   uint32_t chain[NB];  // joint dofs moving body b (0: the base)
   int lim_g[NL1];      // generalized index of limit row li
+  // floor slots last: robots with many (Atlas) keep them out of the workgroup's LDS copy
+  float slot[NS1][4];  // point (link frame) | radius
+  float slot_mu[NS1];
+  int slot_body[NS1];
 };
+// Atlas-sized models (more than 128 floor slots): the slot table is read from the __constant__
+// table (L1 / L2-resident, 21 KB) and the joint-limit rows live in the device workspace, so that
+// 16 envs' LDS regions fit a 4-wave workgroup
+template <class R>
+constexpr bool gang_big() { return R::NS > 128; }
 template <class R>
 constexpr GangTab<R> make_gang_tab() {
   using D = Dims<R>;
@@ -331,14 +337,16 @@ struct Gang {
   static constexpr int O_FR = O_JO + 3 * NJ1, O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
-  static constexpr int LRSZ = NLIM * LRW > NB * CW ? NLIM * LRW : NB * CW;
+  static constexpr bool LIM_WS = gang_big<R>();  // limit rows in the device workspace
+  static constexpr int LRSZ = (!LIM_WS && NLIM * LRW > NB * CW) ? NLIM * LRW : NB * CW;
   static constexpr int FIXED = O_LR + LRSZ + (Y64 ? ((O_LR + LRSZ + RW0) & 1) : 0);  // Y64: rows start even
   static constexpr int PERC = RW0 + 3 * CRW + (Y64 ? ((RW0 + 3 * CRW) & 1) : 0);
   // the kinematic parts are dead once M and the bias are built, before any contact is
   // written: they share the start of the contact area (the env region holds >= KW*NB words)
   static constexpr int O_KV = FIXED;
   static constexpr int MIN_CONTACT_WORDS = KW * NB;
-  static constexpr int GWORDS = (MAXC > 0 ? MAXC : 1) * PERC;  // device workspace per env
+  static constexpr int GW_LR = (MAXC > 0 ? MAXC : 1) * PERC;    // LIM_WS: limit rows after the contacts
+  static constexpr int GWORDS = GW_LR + (LIM_WS ? NLIM * LRW : 0);  // device workspace per env
   static constexpr int ROUNDS_S = (R::NS + T - 1) / T;
 };
 
@@ -364,7 +372,8 @@ template <class R>
 struct GangTabs {
   typedef __attribute__((address_space(3))) const GangTab<R> Tab;
   typedef __attribute__((address_space(3))) const GangDynTab<R> Dyn;
-  static constexpr int TAB_WORDS = (int)((sizeof(GangTab<R>) + 15) / 16) * 4;
+  static constexpr int TAB_COPY = (int)((gang_big<R>() ? offsetof(GangTab<R>, slot) : sizeof(GangTab<R>)) / 4);
+  static constexpr int TAB_WORDS = (TAB_COPY + 3) / 4 * 4;
   static constexpr int DYN_WORDS = (int)((sizeof(GangDynTab<R>) + 15) / 16) * 4;
   static constexpr int WORDS = TAB_WORDS + DYN_WORDS;
   static PBG_DEV Tab& tab(const lds_float* p) { return *(Tab*)p; }
@@ -386,6 +395,14 @@ PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
   using G = Gang<R, T>;
   if (c < X.cap) f(X.l + G::FIXED + c * G::PERC);
   else f(X.g + (size_t)c * G::PERC);
+}
+
+// f(p) with p the first word of joint-limit row li (LDS, or the workspace for LIM_WS models)
+template <class R, int T, class F>
+PBG_DEV void limit_at(const GangCtx& X, int li, F&& f) {
+  using G = Gang<R, T>;
+  if constexpr (G::LIM_WS) f(X.g + G::GW_LR + li * G::LRW);
+  else f(X.l + G::O_LR + li * G::LRW);
 }
 
 // A contact row in registers (loaded one step ahead of its update: PGS software
@@ -956,6 +973,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   }
   // --- distributed: floor slots (slot order) ---------------------------------------------
   uint64_t sb = 0;
+  // ST: the slot table in the workgroup's LDS copy, or (gang_big) the __constant__ table
+  auto slot_pass = [&](const auto& ST) {
   static_for<0, G::ROUNDS_S>([&](auto r_c) {
     constexpr int r = decltype(r_c)::value;
     const int sl = r * T + X.t;
@@ -964,9 +983,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     float rad = 0.f;
     if (sl < R::NS) {
       m3 Rm; f3 x;
-      frame(TB.slot_body[sl], Rm, x);
-      cc = x + mul(Rm, mk3(TB.slot[sl][0], TB.slot[sl][1], TB.slot[sl][2]));
-      rad = TB.slot[sl][3];
+      frame(ST.slot_body[sl], Rm, x);
+      cc = x + mul(Rm, mk3(ST.slot[sl][0], ST.slot[sl][1], ST.slot[sl][2]));
+      rad = ST.slot[sl][3];
       act = cc.z - rad < (float)PBG_CONTACT_THRESHOLD;
     }
     const uint64_t bal = __ballot(act);
@@ -976,10 +995,13 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       csig += pbg_contact_hash(sub, (uint32_t)sl);  // this lane's share of the signature
       const int c = nc + __popcll(bal & gang_mask & below);
       const f3 cp = mk3(cc.x, cc.y, cc.z - rad);
-      put_desc(c, cp - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[TB.slot_body[sl]], 0u, 1.f, TB.slot_mu[sl]);
+      put_desc(c, cp - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[ST.slot_body[sl]], 0u, 1.f, ST.slot_mu[sl]);
     }
     nc += __popcll(mine);
   });
+  };
+  if constexpr (gang_big<R>()) slot_pass(g_gang_tab<R>);
+  else slot_pass(TB);
   slot_bits = sb;
   // --- distributed: self-collision pairs (pair order) ------------------------------------
   if constexpr (R::NPAIR > 0) {
@@ -1116,13 +1138,14 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
     if (is_lim) {
-      lds_float* p = X.l + G::O_LR + j * G::LRW;
-#pragma unroll
-      for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
       const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
-      p[YS] = meff;
-      p[YS + 1] = pos_target(plo, P.k_limit, P.k_sep);
-      p[YS + 2] = pos_target(phi, P.k_limit, P.k_sep);
+      limit_at<R, T>(X, j, [&](auto p) {
+#pragma unroll
+        for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
+        p[YS] = meff;
+        p[YS + 1] = pos_target(plo, P.k_limit, P.k_sep);
+        p[YS + 2] = pos_target(phi, P.k_limit, P.k_sep);
+      });
     } else {
       const int w0r = G::RW0 + dir * G::CRW;
       const float tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
@@ -1148,10 +1171,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     float ly[NL1][NSL], lm[NL1], lrm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
 #pragma unroll
     for (int li = 0; li < NLIM; li++) {
-      const lds_float* p = X.l + G::O_LR + li * G::LRW;
+      limit_at<R, T>(X, li, [&](auto p) {
 #pragma unroll
-      for (int m = 0; m < NSL; m++) ly[li][m] = p[X.t + m * T];
-      lm[li] = p[YS]; ltl[li] = p[YS + 1]; lth[li] = p[YS + 2];
+        for (int m = 0; m < NSL; m++) ly[li][m] = p[X.t + m * T];
+        lm[li] = p[YS]; ltl[li] = p[YS + 1]; lth[li] = p[YS + 2];
+      });
       lrm[li] = lm[li] > 0.f ? fast_rcp(lm[li]) : 0.f;  // off the sweeps' dependency chain
       llo[li] = 0.f; lhi[li] = 0.f;
     }
@@ -1234,7 +1258,7 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
     const uint32_t* src0 = (const uint32_t*)&g_gang_tab<R>;
     const uint32_t* src1 = (const uint32_t*)&g_gang_dyn<R>;
     __attribute__((address_space(3))) uint32_t* dst = (__attribute__((address_space(3))) uint32_t*)lds;
-    for (int i = threadIdx.x; i < (int)(sizeof(GangTab<R>) / 4); i += BLK) dst[i] = src0[i];
+    for (int i = threadIdx.x; i < TT::TAB_COPY; i += BLK) dst[i] = src0[i];
     for (int i = threadIdx.x; i < (int)(sizeof(GangDynTab<R>) / 4); i += BLK) dst[TT::TAB_WORDS + i] = src1[i];
   }
   __syncthreads();
