@@ -186,7 +186,9 @@ int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, v
  * float32 for s < n_steps, e < n_envs, i < action_dim; Philox4x32-10, key = seed, counter =
  * (step0 + s, env_offset + e, i / 4, 0xAC7) -- the bench's random-action protocol
  * (BASELINE.md section 2), independent of the sharding.  out: device [n_steps, n_envs, action_dim];
- * the kernel runs on the device that owns `out` (pbg_pack likewise on its records' device). */
+ * the kernel runs on the device that owns `out` (pbg_pack likewise on its records' device).
+ * These two handle-less entry points take device (hipMalloc) or managed memory only: a host or
+ * pinned-host (hipHostMalloc) pointer has no owning device and returns PBG_E_ARG. */
 int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, uint32_t step0, int env_offset,
                        float* out, void* stream);
 

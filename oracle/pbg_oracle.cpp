@@ -61,7 +61,7 @@ int g_flags = 0;
 enum { OPT_CONTACT_ERP, OPT_DEEP_ERP, OPT_DEEP_THR, OPT_DEEP_MODE, OPT_LIMIT_MODE, OPT_DAMP_MODE, OPT_FRIC_MODE,
        OPT_WARM, OPT_WARM_FRIC, OPT_LIMIT_ERP, OPT_ITERS, OPT_SEP_MODE, OPT_SLOP, OPT_SEP_ABS, OPT_LIM_SEP_ABS,
        OPT_SPRINGS, OPT_ROLL_MU, OPT_SPIN_MU, OPT_LIM_DEEP_MODE, OPT_LIMIT_CFM, OPT_CONTACT_CFM, OPT_CONTACT_THR,
-       OPT_MARGIN, OPT_SELF_COLLISION, OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_COUNT };
+       OPT_MARGIN, OPT_SELF_COLLISION, OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_TORQUE_SUBSTEPS, OPT_COUNT };
 double g_opt[OPT_COUNT];
 const double g_opt_default[OPT_COUNT] = {
     -1.0,             // contact ERP of penetrating contact normal rows (-1: the model's, models_gen.h)
@@ -93,6 +93,9 @@ const double g_opt_default[OPT_COUNT] = {
     PBG_GRAVITY,      // scene gravity (pbg_oracle_set_sim_params, the product's pbg_sim_params_t)
     -1.0,             // sub-step timestep (-1: the model's dt_sub)
     -1.0,             // sub-steps per env step (-1: the model's frame_skip)
+    -1.0,             // sub-steps that carry apply_action's joint torques (-1: all of them; 1: the first
+                      //   only -- Bullet clears a multibody's joint torques after each internal step
+                      //   [EXT, rule study, SURVEY.md Appendix B1])
 };
 struct OptInit { OptInit() { for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = g_opt_default[i]; } } g_opt_init;
 // persistent contact impulses per env and collision candidate (warm starting):
@@ -159,7 +162,7 @@ int sim_substeps(const MV& m) { return g_opt[OPT_SUBSTEPS] > 0.0 ? (int)g_opt[OP
 double sim_env_dt(const MV& m) { return sim_dt(m) * sim_substeps(m); }
 int sim_flag_timeout(const MV& m) { return (600 + sim_substeps(m) - 1) / sim_substeps(m); }
 
-const MV* model(int robot) {
+MV* model_views() {
   static MV views[17] = {view<pbg_models::Pendulum>(), view<pbg_models::Hopper>(),
                          view<pbg_models::HalfCheetah>(), view<pbg_models::Ant>(),
                          view<pbg_models::Humanoid>(), view<pbg_models::Walker2D>(),
@@ -169,9 +172,20 @@ const MV* model(int robot) {
                          view<pbg_models::AntMuJoCo>(), view<pbg_models::HumanoidMuJoCo>(),
                          view<pbg_models::DoublePendulumMuJoCo>(), view<pbg_models::HumanoidFlagrunHarder>(),
                          view<pbg_models::Atlas>()};
-  if (robot < 0 || robot > 16) return nullptr;
-  return &views[robot];
+  return views;
 }
+const MV* model(int robot) {
+  if (robot < 0 || robot > 16) return nullptr;
+  return &model_views()[robot];
+}
+// Importer-rule study (tools/physics_rules.py): a robot's link masses, COMs and inertias replaced
+// at run time (pbg_oracle_set_link_dynamics); the compiled tables stay the product's.
+struct LinkDynOverride {
+  bool on = false;
+  double mass[MAXL], com[MAXL][3], inertia[MAXL][6], base_inertia[6], base_mass;
+  MV orig;
+};
+LinkDynOverride g_dyn_ov[17];
 
 // ------------------------------------------------------------------ physics (pbg_physics.h)
 #include "pbg_physics.h"
@@ -374,6 +388,32 @@ int pbg_oracle_set_physics(const double* v, int n) {
   for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = (v && i < n) ? v[i] : g_opt_default[i];
   if (g_cache && g_cache_n) memset(g_cache, 0, g_cache_n * 4 * MAXCAND * sizeof(double));
   return OPT_COUNT;
+}
+
+// Importer-rule study: replace robot's link dynamics (mass [NL], com [NL][3] link frame, inertia
+// [NL][6] (xx,yy,zz,xy,xz,yz), base mass and inertia [6]); mass == NULL restores the compiled
+// tables.  Returns NL (or -1).  Never used by a product-parity comparison.
+int pbg_oracle_set_link_dynamics(int robot, const double* mass, const double* com, const double* inertia,
+                                 double base_mass, const double* base_inertia) {
+  if (robot < 0 || robot > 16) return -1;
+  MV& v = model_views()[robot];
+  LinkDynOverride& o = g_dyn_ov[robot];
+  if (!o.on) o.orig = v;
+  if (!mass) {
+    v = o.orig;
+    o.on = false;
+    return v.NL;
+  }
+  for (int l = 0; l < v.NL; l++) {
+    o.mass[l] = mass[l];
+    for (int i = 0; i < 3; i++) o.com[l][i] = com[3 * l + i];
+    for (int i = 0; i < 6; i++) o.inertia[l][i] = inertia[6 * l + i];
+  }
+  for (int i = 0; i < 6; i++) o.base_inertia[i] = base_inertia[i];
+  o.base_mass = base_mass;
+  o.on = true;
+  v.mass = o.mass; v.com = o.com; v.inertia = o.inertia; v.base_inertia = o.base_inertia; v.base_mass = o.base_mass;
+  return v.NL;
 }
 
 // Link frames at a state, for tests: R [NL+1][9] row-major, COM [NL+1][3] (base first).

@@ -879,7 +879,12 @@ int physics_step(const MV& m, double* state, const float* ac, uint8_t* slot_acti
   }
   for (int d = 0; d < m.NJ; d++) qd_step[d] = s[PBG_BASE_WORDS + m.NJ + d];
   int nc = 0;
-  for (int sub = 0; sub < sim_substeps(m); sub++) nc = substep<T>(m, s, tau, slot_active, sub, sig, cache, qd_step, asig);
+  // apply_action's torques in the first OPT_TORQUE_SUBSTEPS sub-steps (default: all; rule study)
+  const int tsub = g_opt[OPT_TORQUE_SUBSTEPS] < 0 ? sim_substeps(m) : (int)g_opt[OPT_TORQUE_SUBSTEPS];
+  T zero_tau[MAXD];
+  for (int d = 0; d < m.NJ; d++) zero_tau[d] = T(0);
+  for (int sub = 0; sub < sim_substeps(m); sub++)
+    nc = substep<T>(m, s, sub < tsub ? tau : zero_tau, slot_active, sub, sig, cache, qd_step, asig);
   for (int i = 0; i < SD; i++) state[i] = (double)s[i];
   return nc;
 }

@@ -95,6 +95,16 @@ struct GangTab {
   float slot_mu[NS1];
   int slot_body[NS1];
 };
+// The gang kernel records floor contact for the first 64 slots only (the slot pass's 64-bit
+// mask, the feet test of the pack): every foot slot must be among them (codegen.py puts the
+// feet's slots first when a robot has more than 64)
+template <class R>
+constexpr bool feet_slots_below_64() {
+  for (int sl = 64; sl < R::NS; sl++)
+    for (int f = 0; f < R::NF; f++)
+      if (R::slot_link[sl] == R::foot_link[f]) return false;
+  return true;
+}
 // Atlas-sized models (more than 128 floor slots): the slot table is read from the __constant__
 // table (L1 / L2-resident, 21 KB) and the joint-limit rows live in the device workspace, so that
 // 16 envs' LDS regions fit a 4-wave workgroup
@@ -1326,6 +1336,7 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
     gather<R>(s, flags & 1u, in, [&](auto c) { STAMPX(decltype(c)::value) });
     STAMPX(12)
     uint32_t fnew = 0;
+    static_assert(feet_slots_below_64<R>(), "a foot slot past the gang kernel's 64-slot contact mask");
 #pragma unroll
     for (int f = 0; f < R::NF; f++) {
       uint64_t fm = 0;

@@ -89,7 +89,8 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     // signed: with many workgroups per CU the share can be smaller than the model tables
     long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - (long)sizeof(float) * (long)GangTabs<RR>::WORDS;
     if (budget < 0) budget = 0;
-    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED;
+    // one word reserved for the even-length pad below, so that the padded regions stay inside the budget
+    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED - 1;
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
@@ -103,6 +104,9 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     g->env_words = G::FIXED + (cap * G::PERC > G::MIN_CONTACT_WORDS ? cap * G::PERC : G::MIN_CONTACT_WORDS);
     g->env_words += g->env_words & 1;  // even: every env region 8-byte aligned (b64 row loads)
     g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
+    // the workgroup's regions must fit the CU's LDS (the contact floor MIN_CONTACT_WORDS is the only
+    // term the budget does not bound: a model whose tables + floor exceed it is not launchable)
+    if (g->lds_bytes > (size_t)163840) return (int)hipErrorInvalidConfiguration;
     g->scratch_words_per_env = G::GWORDS;
     const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;
     const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);

@@ -30,6 +30,15 @@ here as explicit choices [EXT, unpinned], in the same RobotModel the MJCF compil
   ``<limit velocity>`` -> getJointInfo's maxVelocity, which current_relative_position divides
   joint speed by (robot_bases.py:314-315); ``<dynamics damping>`` -> -d qdot per sub-step as
   mjcf.py B6; ``<limit effort>`` does not clamp TORQUE_CONTROL torques.
+* U6 one robot per env (a deliberate divergence): the reference's URDFBasedRobot.reset has no
+  ``doneLoading`` guard (``robot_bases.py:145-164``, unlike the MJCF robots' ``:107-116``), so
+  every env reset calls ``loadURDF`` again, and from the second episode on the reference scene
+  holds the earlier episodes' Atlas bodies beside the new one (``restoreState`` at
+  ``gym_locomotion_envs.py:35-36`` restores the snapshot's bodies, the new body is added at the
+  spawn pose and overlaps them; ``addToScene`` then rebinds parts / joints to the newest body).
+  That growth of the scene is a reference artefact no learner relies on; the port models exactly
+  one Atlas per env in every episode.  Atlas parity beyond the first episode is therefore
+  unpinned even where the first episode's would be.
 """
 from __future__ import annotations
 
