@@ -181,7 +181,8 @@ def occupancy(env):
 
 def kernel_name(env):
     lpe = env.info.lanes_per_env
-    k = {1: "pbg::step_kernel", 4: "pbg::team_step_kernel", 16: "pbg::gang_step_kernel"}.get(lpe, "pbg::step_kernel")
+    k = {1: "pbg::step_kernel", 4: "pbg::team_step_kernel", 16: "pbg::gang_step_kernel",
+         32: "pbg::gang_step_kernel"}.get(lpe, "pbg::step_kernel")
     return f"{k}<{env.env_id}>"
 
 
@@ -336,6 +337,8 @@ def main():
     ap.add_argument("--second-env", default=None, help="(compat) 'none' disables the extra legs")
     ap.add_argument("--leg-steps", type=int, default=200)
     ap.add_argument("--dry-run-cpu", action="store_true", help="CI: N > 1 control flow on CPU/gloo, no physics")
+    ap.add_argument("--gang-lanes", type=int, default=-1,
+                    help="A/B: gang width for the gang-kernel robots (16 or 32; -1 = the plan's choice)")
     args = ap.parse_args()
     if args.second_env == "none":
         args.legs = "none"
@@ -363,7 +366,9 @@ def main():
         from pybulletgym_amd.vec_env import VecEnv
 
         def make_env(env_id, n, dev, seed, env_offset, autoreset):
-            return VecEnv(env_id, n, device=dev, seed=seed, env_offset=env_offset, autoreset=autoreset)
+            lanes = args.gang_lanes if env_id.startswith("Humanoid") else -1
+            return VecEnv(env_id, n, device=dev, seed=seed, env_offset=env_offset, autoreset=autoreset,
+                          gang_lanes=lanes)
 
     flops = load_flops()
     n = args.envs_per_gpu

@@ -98,6 +98,7 @@ typedef struct {
   int lds_rows;   /* k >= 0: at most k contact rows (gang: contacts) per env resident in LDS,
                      the rest in the device workspace (bitwise-equality tests of that path) */
   int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics */
+  int gang_lanes; /* 16 / 32: gang width (32: the Humanoid family only; PBG_E_HIP for the others) */
 } pbg_debug_opts_t;
 
 /* Scene / World parameters (scene_bases.py:8-18 Scene(gravity, timestep, frame_skip), 58-73

@@ -40,7 +40,8 @@ class StepIO(ctypes.Structure):
 
 class DebugOpts(ctypes.Structure):
     """pbg_debug_opts_t: test / diagnostic launch options (-1 = default)."""
-    _fields_ = [("kernel", ctypes.c_int), ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int)]
+    _fields_ = [("kernel", ctypes.c_int), ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int),
+                ("gang_lanes", ctypes.c_int)]
 
 
 class SimParams(ctypes.Structure):

@@ -212,6 +212,7 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   // one-lane-per-env kernel for every robot, 2 = the gang kernel for every walker
   const int mode = (opts && (opts->kernel == 0 || opts->kernel == 2)) ? opts->kernel : 1;
   h->geo.force_dist = opts ? opts->gang_dist : -1;
+  h->geo.gang_lanes = (opts && (opts->gang_lanes == 16 || opts->gang_lanes == 32)) ? opts->gang_lanes : -1;
   int e = hip_check(o->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
   // cap on the LDS-resident contact rows (tests of the device-workspace path)
   if (opts && opts->lds_rows >= 0 && opts->lds_rows < h->geo.lds_rows) h->geo.lds_rows = opts->lds_rows;

@@ -36,6 +36,8 @@
 // Humanoid's two); contacts at c >= cap live at the same offsets in the env's device
 // workspace.  (Pairing m_eff | target and lambda | mu for b64 loads needs an even row length:
 // one word more per contact, which costs HalfCheetah at 8,192 envs one LDS-resident contact.)
+#include "pbg_fronts.h"
+
 namespace pbg {
 
 #define PBG_GANG_BLOCK 256  // lanes per gang workgroup (4 waves)
@@ -52,14 +54,31 @@ template <int CTRL>
 PBG_DEV float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
-// all-reduce over the T (4, 8 or 16) lanes of a DPP row segment; identical bits in every
-// lane (each step adds a value and its mirror image: a + b == b + a)
+// gfx950 v_permlane16_swap_b32 a, b: the odd rows of a trade places with the even rows of b.
+// With a = b = x (x uniform within each row) a ends up holding the even row's value and b the odd
+// row's, in both rows of each pair.  Inline asm because this ROCm's builtin
+// (__builtin_amdgcn_permlane16_swap) returns the first register for both of its results; the
+// s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see inside the asm.
+PBG_DEV void row_pair_swap(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+PBG_DEV void row_pair_swap_u(uint32_t& a, uint32_t& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+// all-reduce over the T (4, 8, 16 or 32) lanes of a DPP row segment (T = 32: a row pair);
+// identical bits in every lane (each step adds a value and its mirror image: a + b == b + a;
+// the row-pair step adds the even row's sum to the odd row's in that order in both rows)
 template <int T>
 PBG_DEV float gang_sum(float x) {
   x = x + dpp_f<0xB1>(x);  // quad_perm [1,0,3,2]
   x = x + dpp_f<0x4E>(x);  // quad_perm [2,3,0,1]
   if constexpr (T >= 8) x = x + dpp_f<0x141>(x);   // row_half_mirror
   if constexpr (T >= 16) x = x + dpp_f<0x140>(x);  // row_mirror
+  if constexpr (T >= 32) {
+    float a = x, b = x;
+    row_pair_swap(a, b);  // a: the even row's value, b: the odd row's, in both rows of the pair
+    x = a + b;
+  }
   return x;
 }
 PBG_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
@@ -74,8 +93,22 @@ PBG_DEV uint32_t gang_sum_u32(uint32_t x) {
   x += dpp_u<0x4E>(x);
   if constexpr (T >= 8) x += dpp_u<0x141>(x);
   if constexpr (T >= 16) x += dpp_u<0x140>(x);
+  if constexpr (T >= 32) {
+    uint32_t a = x, b = x;
+    row_pair_swap_u(a, b);
+    x = a + b;
+  }
   return x;
 }
+// 32-lane gangs (two envs per wave): for the robots whose factorisation is front-parallel and
+// whose per-lane registers then fit two waves per SIMD (Humanoid family).  The 16-lane kernel
+// stays for the others, and for these under pbg_create_debug(gang_lanes = 16).
+template <class R>
+constexpr bool gang32_ok() { return FP<R>::NF > 0 && R::NDOF >= 20 && R::NS <= 128; }
+// waves per SIMD the kernel's register budget is compiled for (__launch_bounds__): 32-lane gangs
+// exist to put two waves on a SIMD
+template <int T>
+constexpr int gang_waves_per_simd() { return T >= 32 ? 2 : 1; }
 
 // ------------------------------------------------------------------ constant tables
 template <class R>
@@ -205,16 +238,17 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
       if (R::link_parent[c - 1] + 1 == b) t.child[k++] = c;
   }
   t.child_start[NB] = k;
-  int e = 0;
+  // packed entries of M in the factor's word order (pbg_fronts.h: front-major, or the plain
+  // lower triangle for robots without a front decomposition)
   for (int a = 0; a < R::NDOF; a++)
     for (int b = 0; b <= a; b++)
       if (D::coupled(a, b)) {
+        const int e = FP<R>::idx(a, b);
         const int dk = D::dof_of(b), da = D::dof_of(a);
         t.me_i[e] = a;
         t.me_k[e] = b;
         t.me_b[e] = dk >= 0 ? R::dof_link[dk] + 1 : 0;
         t.me_arm[e] = (a == b && da >= 0) ? (float)R::dof_armature[da] : 0.f;
-        e++;
       }
   for (int i = 0; i < R::NDOF; i++) {
     const int di = D::dof_of(i);
@@ -344,7 +378,12 @@ struct Gang {
   static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
   static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
   static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
-  static constexpr int O_FR = O_JO + 3 * NJ1, O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
+  // the base's state words [p 3 | quat 4 | v 3 | w 3] (front path: the env's state lives in LDS
+  // through the sub-steps, q / qd at O_Q / O_QD)
+  static constexpr int O_BS = O_JO + 3 * NJ1;
+  static constexpr int O_FR = O_BS + 13, O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
+  // front path (pbg_fronts.h) of the distributed dynamics: state in LDS, front-parallel algebra
+  static constexpr bool LST = FP<R>::NF > 0;
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
   static constexpr bool LIM_WS = gang_big<R>();  // limit rows in the device workspace
@@ -724,18 +763,30 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   constexpr int NB = D::NB, N = R::NDOF, NLEV = gang_nlev<R>();
   const float g = X.P.gravity;
   const bool w0 = X.t == 0;
-  // base record and joint state (replicated registers -> LDS)
+  // base record and joint state (replicated registers -> LDS; the front path keeps the state in
+  // LDS: q / qd are there, the base words at O_BS)
   if (w0) {
-    const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
+    float bp[3], bq[4], bv[3], bw[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      bp[i] = G::LST ? X.l[G::O_BS + i] : s.bp[i];
+      bv[i] = G::LST ? X.l[G::O_BS + 7 + i] : s.bv[i];
+      bw[i] = G::LST ? X.l[G::O_BS + 10 + i] : s.bw[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) bq[i] = G::LST ? X.l[G::O_BS + 3 + i] : s.bq[i];
+    const m3 Rb = quat_to_m3(bq[0], bq[1], bq[2], bq[3]);
     const float rec[G::BW] = {Rb.m[0], Rb.m[1], Rb.m[2], Rb.m[3], Rb.m[4], Rb.m[5], Rb.m[6], Rb.m[7], Rb.m[8],
-                              s.bp[0], s.bp[1], s.bp[2], s.bp[0], s.bp[1], s.bp[2],
-                              R::floating ? s.bw[0] : 0.f, R::floating ? s.bw[1] : 0.f, R::floating ? s.bw[2] : 0.f,
-                              R::floating ? s.bv[0] : 0.f, R::floating ? s.bv[1] : 0.f, R::floating ? s.bv[2] : 0.f,
+                              bp[0], bp[1], bp[2], bp[0], bp[1], bp[2],
+                              R::floating ? bw[0] : 0.f, R::floating ? bw[1] : 0.f, R::floating ? bw[2] : 0.f,
+                              R::floating ? bv[0] : 0.f, R::floating ? bv[1] : 0.f, R::floating ? bv[2] : 0.f,
                               0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, 0, i) = rec[i];
+    if constexpr (!G::LST) {
 #pragma unroll
-    for (int d = 0; d < R::NJ; d++) { X.l[G::O_Q + d] = s.q[d]; X.l[G::O_QD + d] = s.qd[d]; }
+      for (int d = 0; d < R::NJ; d++) { X.l[G::O_Q + d] = s.q[d]; X.l[G::O_QD + d] = s.qd[d]; }
+    }
   }
   PBG_GANG_SYNC
   // forward pass, one level at a time (a body's parent is one level up)
@@ -882,6 +933,376 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   PBG_GANG_SYNC
 }
 
+// ------------------------------------------------------------------ front-parallel linear algebra
+// (pbg_fronts.h).  Lane t of a gang works on front q = t % FP (lanes q >= NF only add zeros to
+// the group sums); the group of FP lanes sums the fronts' Schur terms and trunk right-hand
+// sides by DPP; the trunk is factored and solved replicated.  The gang's first FP lanes store
+// the fronts' words, lane 0 the trunk's.
+template <class R>
+struct TrunkTab {
+  static constexpr int NT = FP<R>::NT;
+  static constexpr int count() {
+    int c = 0;
+    for (int t1 = 0; t1 < NT; t1++)
+      for (int t2 = 0; t2 <= t1; t2++) c += Dims<R>::coupled(FP<R>::v.tg[t1], FP<R>::v.tg[t2]);
+    return c;
+  }
+  static constexpr int NT2 = count() > 0 ? count() : 1;
+  // word of trunk pair (t1 >= t2) within the trunk block (-1: structurally zero)
+  static constexpr int pos(int t1, int t2) {
+    return Dims<R>::coupled(FP<R>::v.tg[t1], FP<R>::v.tg[t2]) ? FP<R>::v.idx[FP<R>::v.tg[t1]][FP<R>::v.tg[t2]] - FP<R>::v.toff
+                                                                : -1;
+  }
+  static constexpr int BMAX() {
+    int m = 1;
+    for (int f = 0; f < FP<R>::NF; f++) m = FP<R>::v.bsz[f] > m ? FP<R>::v.bsz[f] : m;
+    return m;
+  }
+  static constexpr int NMAX() {
+    int m = 1;
+    for (int f = 0; f < FP<R>::NF; f++) m = FP<R>::v.n[f] > m ? FP<R>::v.n[f] : m;
+    return m;
+  }
+};
+// per-lane pick of a compile-time front quantity fn(f) (f = the lane's front; -1 when q >= NF)
+template <class R>
+struct FrontSrc {
+  static constexpr int at(int k) { return k; }
+};
+template <class R, class F>
+PBG_DEV int front_pick(int q, F&& fn) {
+  return ksel<FrontSrc<R>, FP<R>::NF, int>(q, [&](auto fc) { return fn(decltype(fc)::value); });
+}
+// the trunk index t's joint velocity / base velocity from the env's LDS state (compile-time t)
+template <class R, int T, int t>
+PBG_DEV float trunk_nu(const GangCtx& X) {
+  using G = Gang<R, T>;
+  constexpr int g = FP<R>::v.tg[t], d = Dims<R>::dof_of(g);
+  if constexpr (d >= 0) return X.l[G::O_QD + d];
+  else return X.l[G::O_BS + 7 + (g - R::NJ)];  // v 3 | w 3
+}
+
+// Front-parallel replacement of dyn_solve: M (front-major words at O_L) and the right-hand side
+// (O_RHS) from LDS; factor, nu_pred = clamp(nu + dt M^-1 rhs), u = L^T nu_pred; stages L (in
+// place, the same word order), 1 / diag(L) (O_LD), u (O_U) and the limit positions (O_LP).
+template <class R, int T>
+PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
+  using D = Dims<R>;
+  using G = Gang<R, T>;
+  using TT = TrunkTab<R>;
+  constexpr int NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NT2 = TT::NT2, BM = TT::BMAX(), NM = TT::NMAX();
+  const float dt = X.P.dt;
+  const int q = opaque_lane(X.t) % GRP;
+  const int cls = q < NF ? front_pick<R>(q, [](int f) { return FP<R>::v.cls[f]; }) : -1;
+  const int boff = front_pick<R>(q, [](int f) { return FP<R>::v.off[f]; });
+  const int g0 = front_pick<R>(q, [](int f) { return FP<R>::v.g0[f]; });
+  const lds_float* blk = X.l + G::O_L + boff;
+  float Fb[BM], Fd[NM], Fy[NM];  // the lane's front block (factored in place), 1 / diag, forward solve
+  float S[NT2], z[NT];           // Schur terms W W^T (trunk pairs) and trunk right-hand-side terms
+#pragma unroll
+  for (int i = 0; i < NT2; i++) S[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT; i++) z[i] = 0.f;
+  // --- fronts: factor, forward solve ---------------------------------------------------------
+  static_for<0, FP<R>::v.ncls>([&](auto c_c) {
+    constexpr int C = decltype(c_c)::value;
+    using FC = FrontCls<R, C>;
+    constexpr int n = FC::n;
+    if (cls != C) return;
+    constexpr int bs = FP<R>::v.bsz[FC::f];
+#pragma unroll
+    for (int i = 0; i < bs; i++) Fb[i] = blk[i];
+    static_for<0, n>([&](auto a_c) {
+      constexpr int a = decltype(a_c)::value;
+      const float d = fast_sqrt(Fb[FC::a_off(a, a)]);
+      const float r = fast_rcp(d);
+      Fb[FC::a_off(a, a)] = d;
+      Fd[a] = r;
+      static_for<a + 1, n>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(b, a)) Fb[FC::a_off(b, a)] *= r;
+      });
+      static_for<0, NT>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (FC::tc(t)) Fb[FC::c_off(a, t)] *= r;
+      });
+      static_for<a + 1, n>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(b, a)) {
+          static_for<a + 1, b + 1>([&](auto b2_c) {
+            constexpr int b2 = decltype(b2_c)::value;
+            if constexpr (FC::cpl(b2, a) && FC::cpl(b, b2)) Fb[FC::a_off(b, b2)] -= Fb[FC::a_off(b, a)] * Fb[FC::a_off(b2, a)];
+          });
+          static_for<0, NT>([&](auto t_c) {
+            constexpr int t = decltype(t_c)::value;
+            if constexpr (FC::tc(t)) Fb[FC::c_off(b, t)] -= Fb[FC::c_off(a, t)] * Fb[FC::a_off(b, a)];
+          });
+        }
+      });
+      static_for<0, NT>([&](auto t1_c) {
+        constexpr int t1 = decltype(t1_c)::value;
+        if constexpr (FC::tc(t1)) {
+          static_for<0, t1 + 1>([&](auto t2_c) {
+            constexpr int t2 = decltype(t2_c)::value;
+            if constexpr (FC::tc(t2)) S[TT::pos(t1, t2)] += Fb[FC::c_off(a, t1)] * Fb[FC::c_off(a, t2)];
+          });
+        }
+      });
+    });
+    // forward solve L_f y_f = rhs_f; trunk terms z_t += L_(t,a) y_a
+    static_for<0, n>([&](auto a_c) {
+      constexpr int a = decltype(a_c)::value;
+      float v = X.l[G::O_RHS + g0 + a];
+      static_for<0, a>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(a, b)) v -= Fb[FC::a_off(a, b)] * Fy[b];
+      });
+      Fy[a] = v * Fd[a];
+      static_for<0, NT>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (FC::tc(t)) z[t] += Fb[FC::c_off(a, t)] * Fy[a];
+      });
+    });
+  });
+  // --- trunk: T - sum_f W_f W_f^T, factor, forward + backward solve ---------------------------
+  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
+  float Lt[NT2], Ldt[NT], yt[NT], xt[NT];
+#pragma unroll
+  for (int i = 0; i < NT2; i++) Lt[i] = tb[i] - gang_sum<GRP>(S[i]);
+  static_for<0, NT>([&](auto j_c) {
+    constexpr int j = decltype(j_c)::value;
+    const float d = fast_sqrt(Lt[TT::pos(j, j)]);
+    const float r = fast_rcp(d);
+    Lt[TT::pos(j, j)] = d;
+    Ldt[j] = r;
+    static_for<j + 1, NT>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      if constexpr (TT::pos(i, j) >= 0) Lt[TT::pos(i, j)] *= r;
+    });
+    static_for<j + 1, NT>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      if constexpr (TT::pos(i, j) >= 0) {
+        static_for<j + 1, i + 1>([&](auto k_c) {
+          constexpr int k = decltype(k_c)::value;
+          if constexpr (TT::pos(k, j) >= 0 && TT::pos(i, k) >= 0) Lt[TT::pos(i, k)] -= Lt[TT::pos(i, j)] * Lt[TT::pos(k, j)];
+        });
+      }
+    });
+  });
+  static_for<0, NT>([&](auto t_c) {
+    constexpr int t = decltype(t_c)::value;
+    float v = X.l[G::O_RHS + FP<R>::v.tg[t]] - gang_sum<GRP>(z[t]);
+    static_for<0, t>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      if constexpr (TT::pos(t, k) >= 0) v -= Lt[TT::pos(t, k)] * yt[k];
+    });
+    yt[t] = v * Ldt[t];
+  });
+  static_for<0, NT>([&](auto r_c) {
+    constexpr int t = NT - 1 - decltype(r_c)::value;
+    float v = yt[t];
+    static_for<t + 1, NT>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      if constexpr (TT::pos(k, t) >= 0) v -= Lt[TT::pos(k, t)] * xt[k];
+    });
+    xt[t] = v * Ldt[t];
+  });
+  // trunk nu_pred and u_t = L_t^T nu_t
+  float nut[NT];
+  static_for<0, NT>([&](auto t_c) {
+    constexpr int t = decltype(t_c)::value;
+    nut[t] = clampf(trunk_nu<R, T, t>(X) + dt * xt[t], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+  });
+  const bool wf = X.t < GRP && q < NF;  // the gang's front writers
+  // --- fronts: backward solve, nu_pred, u_f; store --------------------------------------------
+  static_for<0, FP<R>::v.ncls>([&](auto c_c) {
+    constexpr int C = decltype(c_c)::value;
+    using FC = FrontCls<R, C>;
+    constexpr int n = FC::n;
+    if (cls != C) return;
+    float xf[n], nuf[n];
+    static_for<0, n>([&](auto r_c) {
+      constexpr int a = n - 1 - decltype(r_c)::value;
+      float v = Fy[a];
+      static_for<a + 1, n>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(b, a)) v -= Fb[FC::a_off(b, a)] * xf[b];
+      });
+      static_for<0, NT>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (FC::tc(t)) v -= Fb[FC::c_off(a, t)] * xt[t];
+      });
+      xf[a] = v * Fd[a];
+    });
+    // joint dof of local a: NJ - 1 - (g0 + a); its velocity from the gang's LDS copy of qd
+    const lds_float* qd = X.l + G::O_QD + (R::NJ - 1 - g0);
+    static_for<0, n>([&](auto a_c) {
+      constexpr int a = decltype(a_c)::value;
+      nuf[a] = clampf(qd[-a] + dt * xf[a], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    });
+    if (wf) {
+      lds_float* wb = X.l + G::O_L + boff;
+      constexpr int bs = FP<R>::v.bsz[FC::f];
+#pragma unroll
+      for (int i = 0; i < bs; i++) wb[i] = Fb[i];
+      static_for<0, n>([&](auto a_c) {
+        constexpr int a = decltype(a_c)::value;
+        float u = 0.f;
+        static_for<a, n>([&](auto b_c) {
+          constexpr int b = decltype(b_c)::value;
+          if constexpr (FC::cpl(b, a)) u += Fb[FC::a_off(b, a)] * nuf[b];
+        });
+        static_for<0, NT>([&](auto t_c) {
+          constexpr int t = decltype(t_c)::value;
+          if constexpr (FC::tc(t)) u += Fb[FC::c_off(a, t)] * nut[t];
+        });
+        X.l[G::O_LD + g0 + a] = Fd[a];
+        X.l[G::O_U + g0 + a] = u;
+      });
+    }
+  });
+  if (X.t == 0) {
+    lds_float* wt = X.l + G::O_L + FP<R>::v.toff;
+#pragma unroll
+    for (int i = 0; i < NT2; i++) wt[i] = Lt[i];
+    static_for<0, NT>([&](auto t_c) {
+      constexpr int t = decltype(t_c)::value;
+      float u = 0.f;
+      static_for<t, NT>([&](auto k_c) {
+        constexpr int k = decltype(k_c)::value;
+        if constexpr (TT::pos(k, t) >= 0) u += Lt[TT::pos(k, t)] * nut[k];
+      });
+      X.l[G::O_LD + FP<R>::v.tg[t]] = Ldt[t];
+      X.l[G::O_U + FP<R>::v.tg[t]] = u;
+    });
+#pragma unroll
+    for (int i = R::NDOF; i < G::YS; i++) X.l[G::O_U + i] = 0.f;
+    static_for<0, D::NLIM>([&](auto li_c) {
+      constexpr int li = decltype(li_c)::value;
+      constexpr int d = D::LIM.v[li][0];
+      X.l[G::O_LP + 2 * li] = X.l[G::O_Q + d] - (float)R::dof_lower[d];
+      X.l[G::O_LP + 2 * li + 1] = (float)R::dof_upper[d] - X.l[G::O_Q + d];
+    });
+  }
+  (void)NM;
+  (void)s;
+}
+
+// Front-parallel replacement of integrate's back-substitution: nu = L^-T u from the staged
+// factor and the solved u (LDS), clamped; the fronts' and trunk's parts meet in LDS (O_RHS, dead
+// after the solve) and every lane then integrates the replicated state.
+template <class R, int T>
+PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
+  using G = Gang<R, T>;
+  using TT = TrunkTab<R>;
+  constexpr int NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NJ = R::NJ, N = R::NDOF;
+  const float dt = X.P.dt;
+  const float vmax = (float)PBG_MAX_COORD_VELOCITY;
+  const int q = opaque_lane(X.t) % GRP;
+  const int cls = q < NF ? front_pick<R>(q, [](int f) { return FP<R>::v.cls[f]; }) : -1;
+  const int boff = front_pick<R>(q, [](int f) { return FP<R>::v.off[f]; });
+  const int g0 = front_pick<R>(q, [](int f) { return FP<R>::v.g0[f]; });
+  // trunk: x_t = L_t^-T u_t
+  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
+  float xt[NT];
+  static_for<0, NT>([&](auto r_c) {
+    constexpr int t = NT - 1 - decltype(r_c)::value;
+    float v = X.l[G::O_U + FP<R>::v.tg[t]];
+    static_for<t + 1, NT>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      if constexpr (TT::pos(k, t) >= 0) v -= tb[TT::pos(k, t)] * xt[k];
+    });
+    xt[t] = v * X.l[G::O_LD + FP<R>::v.tg[t]];
+  });
+  const bool wf = X.t < GRP && q < NF;
+  static_for<0, FP<R>::v.ncls>([&](auto c_c) {
+    constexpr int C = decltype(c_c)::value;
+    using FC = FrontCls<R, C>;
+    constexpr int n = FC::n;
+    if (cls != C) return;
+    const lds_float* blk = X.l + G::O_L + boff;
+    float xf[n];
+    static_for<0, n>([&](auto r_c) {
+      constexpr int a = n - 1 - decltype(r_c)::value;
+      float v = X.l[G::O_U + g0 + a];
+      static_for<a + 1, n>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(b, a)) v -= blk[FC::a_off(b, a)] * xf[b];
+      });
+      static_for<0, NT>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (FC::tc(t)) v -= blk[FC::c_off(a, t)] * xt[t];
+      });
+      xf[a] = v * X.l[G::O_LD + g0 + a];
+    });
+    if (wf) {
+      static_for<0, n>([&](auto a_c) {
+        constexpr int a = decltype(a_c)::value;
+        X.l[G::O_RHS + g0 + a] = clampf(xf[a], -vmax, vmax);
+      });
+    }
+  });
+  if (X.t == 0) {
+    static_for<0, NT>([&](auto t_c) {
+      constexpr int t = decltype(t_c)::value;
+      X.l[G::O_RHS + FP<R>::v.tg[t]] = clampf(xt[t], -vmax, vmax);
+    });
+  }
+  PBG_GANG_SYNC
+  // semi-implicit Euler of the env's LDS state (one writer; the next sub-step reads it after its
+  // first gang sync)
+  if (X.t == 0) {
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+      const float qd = X.l[G::O_RHS + Dims<R>::gj(d)];
+      X.l[G::O_QD + d] = qd;
+      X.l[G::O_Q + d] += dt * qd;
+    }
+    if constexpr (R::floating) {
+      float bq[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) bq[i] = X.l[G::O_BS + 3 + i];
+      f3 w;
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const float v = X.l[G::O_RHS + NJ + i], wi = X.l[G::O_RHS + NJ + 3 + i];
+        X.l[G::O_BS + 7 + i] = v;
+        X.l[G::O_BS + 10 + i] = wi;
+        X.l[G::O_BS + i] += dt * v;
+        (i == 0 ? w.x : (i == 1 ? w.y : w.z)) = wi;
+      }
+      free_body_quat(bq, w, X.P);
+#pragma unroll
+      for (int i = 0; i < 4; i++) X.l[G::O_BS + 3 + i] = bq[i];
+    }
+  }
+  (void)N;
+  (void)s;
+}
+// the env's state record between registers and its LDS copy (front path)
+template <class R, int T>
+PBG_DEV void gang_put_state(const State<R>& s, const GangCtx& X) {
+  using G = Gang<R, T>;
+  if (X.t == 0) {
+#pragma unroll
+    for (int d = 0; d < R::NJ; d++) { X.l[G::O_Q + d] = s.q[d]; X.l[G::O_QD + d] = s.qd[d]; }
+#pragma unroll
+    for (int i = 0; i < 3; i++) { X.l[G::O_BS + i] = s.bp[i]; X.l[G::O_BS + 7 + i] = s.bv[i]; X.l[G::O_BS + 10 + i] = s.bw[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) X.l[G::O_BS + 3 + i] = s.bq[i];
+  }
+}
+template <class R, int T>
+PBG_DEV void gang_get_state(State<R>& s, const GangCtx& X) {
+  using G = Gang<R, T>;
+#pragma unroll
+  for (int d = 0; d < R::NJ; d++) { s.q[d] = X.l[G::O_Q + d]; s.qd[d] = X.l[G::O_QD + d]; }
+#pragma unroll
+  for (int i = 0; i < 3; i++) { s.bp[i] = X.l[G::O_BS + i]; s.bv[i] = X.l[G::O_BS + 7 + i]; s.bw[i] = X.l[G::O_BS + 10 + i]; }
+#pragma unroll
+  for (int i = 0; i < 4; i++) s.bq[i] = X.l[G::O_BS + 3 + i];
+}
+
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int T, bool DIST>
 PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits, uint32_t sub,
@@ -892,10 +1313,16 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   constexpr int N = R::NDOF, NB = D::NB, NLIM = D::NLIM, NSL = G::NSL, YS = G::YS;
   const SimP& P = X.P;
   const bool w0 = X.t == 0;  // the gang's writer for replicated values
+  // L (Dims<R>::lidx order) into the factor's LDS word order (pbg_fronts.h)
   auto stage_solution = [&](const float* L, const float* Ld, const float* u) {
     if (w0) {
-#pragma unroll
-      for (int i = 0; i < D::NNZ; i++) X.l[G::O_L + i] = L[i];
+      static_for<0, N>([&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        static_for<0, i + 1>([&](auto k_c) {
+          constexpr int k = decltype(k_c)::value;
+          if constexpr (D::coupled(i, k)) X.l[G::O_L + FP<R>::idx(i, k)] = L[D::lidx(i, k)];
+        });
+      });
 #pragma unroll
       for (int i = 0; i < N; i++) { X.l[G::O_LD + i] = Ld[i]; X.l[G::O_U + i] = u[i]; }
 #pragma unroll
@@ -908,16 +1335,16 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       });
     }
   };
-  // the factor L and 1 / diag(L), replicated in registers: the rows pass reads them there
-  float L[D::NNZ], Ld[N];
   if constexpr (DIST) {
     // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
+#ifndef PBG_DEV_NODYN
     gang_dyn_mass<R, T>(s, X SUB_STAMP_PASS);
+#endif
     STAMP(3)
   } else {
     // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
     {
-      float nu[N], u[N];
+      float L[D::NNZ], Ld[N], nu[N], u[N];
       dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
       STAMP(3)
       stage_solution(L, Ld, u);
@@ -1072,20 +1499,28 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   PBG_GANG_SYNC
   STAMP(4)
   if constexpr (DIST) {
-    // --- replicated: factorisation and the unconstrained velocity, staged for the PGS; after
-    // the detection, so the factor is still in registers for the rows pass --------------------
-    float rhs[N], nu[N], u[N];
+    if constexpr (FP<R>::NF > 0) {
+      // --- front-parallel factorisation and unconstrained velocity (pbg_fronts.h) -----------
+      gang_front_solve<R, T>(s, X);
+    } else {
+      // --- replicated: factorisation and the unconstrained velocity, staged for the PGS ----
+      float L[D::NNZ], Ld[N], rhs[N], nu[N], u[N];
 #pragma unroll
-    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+      for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
 #pragma unroll
-    for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
-    dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
-    stage_solution(L, Ld, u);
+      for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
+      dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
+      stage_solution(L, Ld, u);
+    }
     PBG_GANG_SYNC
     STAMP(10)
   }
   // --- distributed: constraint rows (limits first, then 3 rows per contact) --------------
+#ifdef PBG_DEV_NOROWS
+  const int njobs = 0;
+#else
   const int njobs = NLIM + 3 * nc;
+#endif
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
     if (j >= njobs) continue;
@@ -1134,7 +1569,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         J[i] = tj;
       }
     }
-    // y = L^-1 J (forward substitution over the compile-time pattern of L)
+    // y = L^-1 J (forward substitution over the compile-time pattern of L; the factor is read
+    // from its LDS staging -- the gang's lanes read the same words, a broadcast -- instead of being
+    // held in registers from the factorisation through the detection and this pass)
+    const lds_float* Lx = X.l + G::O_L;
     float y[N];
     float D2 = 0.f;
 #pragma unroll
@@ -1142,8 +1580,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       float tt = J[i];
 #pragma unroll
       for (int kk = 0; kk < i; kk++)
-        if (D::coupled(i, kk)) tt -= L[D::lidx(i, kk)] * y[kk];
-      y[i] = tt * Ld[i];
+        if (D::coupled(i, kk)) tt -= Lx[FP<R>::idx(i, kk)] * y[kk];
+      y[i] = tt * X.l[G::O_LD + i];
       D2 += y[i] * y[i];
     }
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
@@ -1177,6 +1615,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   for (int m = 0; m < NSL; m++) us[m] = X.l[G::O_U + X.t + m * T];
   {
     // joint-limit rows stay in registers for the whole solve
+#ifdef PBG_DEV_NOLIM
+    constexpr int NLIM = 0;
+#endif
     constexpr int NL1 = NLIM > 0 ? NLIM : 1;
     float ly[NL1][NSL], lm[NL1], lrm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
 #pragma unroll
@@ -1219,10 +1660,18 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #pragma unroll
   for (int m = 0; m < NSL; m++) X.l[G::O_U + X.t + m * T] = us[m];
   PBG_GANG_SYNC
-  {
+  if constexpr (DIST && G::LST) {
+    gang_front_integrate<R, T>(s, X);
+  } else {
     float L[D::NNZ], Ld[N], u[N], nu[N];
-#pragma unroll
-    for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+    // the staged factor in Dims<R>::lidx order (a compile-time permutation of its LDS words)
+    static_for<0, N>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      static_for<0, i + 1>([&](auto k_c) {
+        constexpr int k = decltype(k_c)::value;
+        if constexpr (D::coupled(i, k)) L[D::lidx(i, k)] = X.l[G::O_L + FP<R>::idx(i, k)];
+      });
+    });
 #pragma unroll
     for (int i = 0; i < N; i++) { Ld[i] = X.l[G::O_LD + i]; u[i] = X.l[G::O_U + i]; }
     integrate<R>(s, L, Ld, u, nu, P);
@@ -1256,7 +1705,7 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
 }
 
 template <class R, int T, bool DIST>
-__global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
+__global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
   extern __shared__ float lds_dyn[];
   using G = Gang<R, T>;
@@ -1290,6 +1739,8 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
+  constexpr bool LST = DIST && G::LST;  // the front path: the state in LDS through the sub-steps
+  if constexpr (LST) gang_put_state<R, T>(s, X);
   // apply_action: tau = power * power_coef * clip(a, -1, 1)   (robot_locomotors.py:26-29)
   float tau[R::NJ];
 #pragma unroll
@@ -1309,6 +1760,12 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
   STAMP(7)
   for (int sub = 0; sub < B.sp.substeps; sub++)
     nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits, (uint32_t)sub, csig SUB_STAMP_PASS);
+  if constexpr (LST) {
+    gang_get_state<R, T>(s, X);  // (the sub-step ends with a gang sync)
+    // the raw action again for the pack (electricity), instead of holding it through the physics
+#pragma unroll
+    for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
+  }
   if (io.ncontact && w0) io.ncontact[e] = nc;
   if (io.csig) {
     const uint32_t sig = gang_sum_u32<T>(csig);
@@ -1333,6 +1790,11 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
   } else {
     PackIn<R> in;
     in.env_dt = B.sp.env_dt;
+#ifdef PBG_DEV_NOPACK
+    for (int i = 0; i < R::OBS; i++) obs[i] = 0.f;
+    po = PackOut{};
+    if (0)
+#endif
     gather<R>(s, flags & 1u, in, [&](auto c) { STAMPX(decltype(c)::value) });
     STAMPX(12)
     uint32_t fnew = 0;
@@ -1349,8 +1811,13 @@ __global__ __launch_bounds__(gang_block<R>()) void gang_step_kernel(Buffers B, S
     in.feet_new = fnew;
     in.potential_old = pot_old;
     in.initial_z = z0_old;
+#ifdef PBG_DEV_NOPACK
+    if (0)
+#endif
+    {
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
     else flag_pack<R, 4>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, X.t);
+    }
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }

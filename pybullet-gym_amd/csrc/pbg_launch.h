@@ -13,12 +13,13 @@ struct ResetIO;
 
 struct Geometry {
   int team;          // lanes per env: 1 (step_kernel), 4 (team_step_kernel, pbg_team.hip) or
-                     // 16 (gang_step_kernel, pbg_gang.hip)
+                     // 16 / 32 (gang_step_kernel, pbg_gang.hip)
   int block;         // lanes per step workgroup: 16, 32 or 64
   int lds_rows;      // contact-constraint rows (gang: contacts) resident in LDS per env
   int env_words;     // gang: LDS words per env
   int gang_dist;     // gang: distributed (1) or replicated (0) unconstrained dynamics
   int force_dist;    // in: -1 = plan's choice, 0 / 1 = force gang_dist (pbg_create_debug)
+  int gang_lanes;    // in: -1 = plan's choice, 16 / 32 = gang width (pbg_create_debug)
   size_t lds_bytes;  // dynamic LDS per step workgroup
   size_t scratch_words_per_env;
   int vgprs;          // the selected step kernel's registers per lane (hipFuncGetAttributes)

@@ -76,39 +76,49 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
   }
 }
 
-// Gang geometry (pbg_gang.hip): 16 lanes per env, 4 envs per one-wave workgroup; the
-// per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
+// Gang geometry (pbg_gang.hip): T = 16 or 32 lanes per env, 256 / T envs per 4-wave workgroup;
+// the per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
 // + 3 rows), contacts past the capacity spill to the device workspace.
-template <class RR>
-static int plan_gang(int n_envs, int cus, Geometry* g) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
-    using G = Gang<RR, 16>;
-    constexpr int EPB = gang_block<RR>() / 16;  // envs per workgroup
+template <class RR, int T>
+static int plan_gang_t(int n_envs, int cus, Geometry* g) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder && (T == 16 || gang32_ok<RR>())) {
+    using G = Gang<RR, T>;
+    constexpr int EPB = gang_block<RR>() / T;  // envs per workgroup
     const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
     // signed: with many workgroups per CU the share can be smaller than the model tables
     long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - (long)sizeof(float) * (long)GangTabs<RR>::WORDS;
     if (budget < 0) budget = 0;
-    // one word reserved for the even-length pad below, so that the padded regions stay inside the budget
-    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED - 1;
+    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED;
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
+    // every env region 16-byte aligned (b64 / b128 LDS accesses): round the region up, and give
+    // back a contact when the rounding crosses the budget
+    auto region = [&](int c) {
+      const int w = G::FIXED + (c * G::PERC > G::MIN_CONTACT_WORDS ? c * G::PERC : G::MIN_CONTACT_WORDS);
+      return (w + 3) & ~3;
+    };
+    while (cap > 0 && (long)region(cap) * EPB * (long)sizeof(float) > budget) cap--;
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
-    g->gang_dist = RR::NDOF >= 8 || (size_t)n_envs * 16 > (size_t)64 * 4 * cus;
-    if (g->force_dist == 0 || g->force_dist == 1) g->gang_dist = g->force_dist;  // pbg_create_debug
-    g->team = 16;
+    g->gang_dist = RR::NDOF >= 8 || T >= 32 || (size_t)n_envs * T > (size_t)64 * 4 * cus;
+    // pbg_create_debug (32-lane gangs have no replicated-dynamics variant)
+    if ((g->force_dist == 0 || g->force_dist == 1) && T == 16) g->gang_dist = g->force_dist;
+    g->team = T;
     g->block = gang_block<RR>();
     g->lds_rows = cap;
-    g->env_words = G::FIXED + (cap * G::PERC > G::MIN_CONTACT_WORDS ? cap * G::PERC : G::MIN_CONTACT_WORDS);
-    g->env_words += g->env_words & 1;  // even: every env region 8-byte aligned (b64 row loads)
+    g->env_words = region(cap);
     g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
     // the workgroup's regions must fit the CU's LDS (the contact floor MIN_CONTACT_WORDS is the only
     // term the budget does not bound: a model whose tables + floor exceed it is not launchable)
     if (g->lds_bytes > (size_t)163840) return (int)hipErrorInvalidConfiguration;
     g->scratch_words_per_env = G::GWORDS;
-    const void* fn = g->gang_dist ? (const void*)gang_step_kernel<RR, 16, true> : (const void*)gang_step_kernel<RR, 16, false>;
+    const void* fn;
+    if constexpr (T == 16)
+      fn = g->gang_dist ? (const void*)gang_step_kernel<RR, T, true> : (const void*)gang_step_kernel<RR, T, false>;
+    else
+      fn = (const void*)gang_step_kernel<RR, T, true>;
     const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
     return e ? e : kernel_attrs(fn, g);
   } else {
@@ -116,27 +126,49 @@ static int plan_gang(int n_envs, int cus, Geometry* g) {
     return (int)hipErrorInvalidValue;
   }
 }
+// lanes: 16 or 32 (pbg_create_debug gang_lanes), -1: the plan's choice
 template <class RR>
-static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder) {
-    if (g.team != 16) return false;
-    const dim3 grid(blocks(B.n, gang_block<RR>() / 16)), blk(gang_block<RR>());
-    if (g.gang_dist)
-      hipLaunchKernelGGL((gang_step_kernel<RR, 16, true>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
-    else
-      hipLaunchKernelGGL((gang_step_kernel<RR, 16, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
+static int plan_gang(int n_envs, int cus, Geometry* g, int lanes) {
+  if (lanes < 0) lanes = 16;
+  if (lanes == 32) return plan_gang_t<RR, 32>(n_envs, cus, g);
+  return plan_gang_t<RR, 16>(n_envs, cus, g);
+}
+template <class RR, int T>
+static bool launch_gang_t(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder && (T == 16 || gang32_ok<RR>())) {
+    const dim3 grid(blocks(B.n, gang_block<RR>() / T)), blk(gang_block<RR>());
+    if constexpr (T == 16) {
+      if (!g.gang_dist) {
+        hipLaunchKernelGGL((gang_step_kernel<RR, T, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows,
+                           g.env_words);
+        return true;
+      }
+    }
+    hipLaunchKernelGGL((gang_step_kernel<RR, T, true>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows, g.env_words);
     return true;
   } else {
     (void)B; (void)io; (void)scratch; (void)g; (void)s;
     return false;
   }
 }
+template <class RR>
+static bool launch_gang(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if (g.team == 16) return launch_gang_t<RR, 16>(B, io, scratch, g, s);
+  if (g.team == 32) return launch_gang_t<RR, 32>(B, io, scratch, g, s);
+  return false;
+}
 
 // Atlas (886 floor-contact candidates) has no lane kernel: its unrolled per-slot rows would not
 // fit an instruction cache; the debug `kernel = 0` option gives it the gang kernel too.  (The
 // lane kernel is only instantiated inside these templates, behind `if constexpr`.)
 template <class RR>
-constexpr bool lane_ok() { return RR::NS <= 128; }
+constexpr bool lane_ok() {
+#ifdef PBG_DEV_GANG_ONLY  // ISA experiments on the gang kernel only (never the product library)
+  return false;
+#else
+  return RR::NS <= 128;
+#endif
+}
 template <class RR>
 static int plan_lane(int n_envs, int cus, Geometry* g) {
   if constexpr (lane_ok<RR>()) {
@@ -184,7 +216,7 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
 // (a second free body per env) runs on the lane kernel only.
 int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
-  if (R::kind != 1 && !R::harder && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g);
+  if (R::kind != 1 && !R::harder && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g, g->gang_lanes);
   return plan_lane<R>(n_envs, cus, g);
 }
 

@@ -49,14 +49,15 @@ class VecEnv:
     pbg_sim_params_t, scene_bases.py:8-18,58-73), or a ``_native.SimParams``; None = the
     reference's values (``self.sim_params`` holds the ones in force).
 
-    ``kernel`` / ``lds_rows`` / ``gang_dist`` are test and diagnostic launch options
-    (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
-    a cap on LDS-resident contact rows, forced replicated (0) / distributed (1) gang dynamics.
+    ``kernel`` / ``lds_rows`` / ``gang_dist`` / ``gang_lanes`` are test and diagnostic launch
+    options (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
+    a cap on LDS-resident contact rows, forced replicated (0) / distributed (1) gang dynamics, the
+    gang width (16 or 32 lanes per env; 32 for the Humanoid family only).
     """
 
     def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
                  autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1,
-                 sim_params=None):
+                 sim_params=None, gang_lanes: int = -1):
         if not torch.cuda.is_available():
             raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.env_id = env_id
@@ -66,7 +67,7 @@ class VecEnv:
         L = _native.lib()
         h = ctypes.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        opts = _native.DebugOpts(int(kernel), int(lds_rows), int(gang_dist))
+        opts = _native.DebugOpts(int(kernel), int(lds_rows), int(gang_dist), int(gang_lanes))
         sp = sim_params if isinstance(sim_params, _native.SimParams) else _native.sim_params(env_id, sim_params)
         _native.check(L.pbg_create_ex(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
                                       ctypes.byref(sp), ctypes.byref(opts), ctypes.byref(h)), "pbg_create")

@@ -194,6 +194,7 @@ COND_FRAC = 0.6
 LOOSE_FRAC = 0.05
 EXPLAIN_FACTOR = 3.0
 F32_MCA_RUNS = 32       # first pass per outlier ...
+F32_ESCALATE_MAX = 48   # outliers of one step beyond which the ladder is skipped (a broken kernel fails fast)
 F32_MCA_RUNS_LADDER = (256,)  # ... and the one escalation for an outlier the first pass leaves unexplained
                         # (a step on a PGS active-set boundary that ~1 % of float32 roundings cross);
                         # round 4: no 2,048-run rung -- an outlier 256 runs do not
@@ -282,8 +283,8 @@ def _explainer(env_id, s_in, x_in, act, oo, csig64, disc64, kind, seed):
         rung = np.zeros(len(idx), np.int64)
         for r, runs in enumerate(F32_MCA_RUNS_LADDER):
             again = np.flatnonzero((rel > EXPLAIN_FACTOR * env) & ~(c & flip))
-            if not len(again):
-                break
+            if not len(again) or len(again) > F32_ESCALATE_MAX:
+                break  # (a step with that many unexplained outliers fails without the escalation)
             j = idx[again]
             e2, f2, _ = _f32_envelope(env_id, s_in[j], x_in[j], act[j], oo[j], csig64[j], disc64[j], kind, seed,
                                       runs=runs, ieee=False)
@@ -513,9 +514,9 @@ def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init=None, pr
 
 
 # Atlas: the oracle steps it ~8x slower than the Humanoid (886 floor slots, 36 dofs, 8
-# sub-steps) and falls within ~20 steps: 64 envs x 30 steps, ~900 class-A env-steps, so one
-# (explained) step above the class bound is 0.1 % of them
-TF_SIZE = {"AtlasPyBulletEnv-v0": (64, 30, 0.998)}
+# sub-steps) and falls within ~20 steps: 128 envs x 30 steps, ~1,850 class-A env-steps (round 3:
+# 64 envs, where two explained float32 outliers above the 1e-3 bound already crossed the share)
+TF_SIZE = {"AtlasPyBulletEnv-v0": (128, 30, 0.998)}
 
 
 @pytest.mark.parametrize("env_id", ENVS)
@@ -820,31 +821,37 @@ def test_quad_kernel_determinism_and_offset_invariance():
                                          ("HalfCheetahPyBulletEnv-v0", {}), ("Walker2DPyBulletEnv-v0", {}),
                                          ("AntPyBulletEnv-v0", {"kernel": 2}),
                                          ("HumanoidPyBulletEnv-v0", {"gang_dist": 0}),
-                                         ("Walker2DPyBulletEnv-v0", {"gang_dist": 0})])
+                                         ("Walker2DPyBulletEnv-v0", {"gang_dist": 0}),
+                                         ("HumanoidPyBulletEnv-v0", {"gang_lanes": 16}),
+                                         ("HumanoidPyBulletEnv-v0", {"gang_lanes": 32}),
+                                         ("HumanoidFlagrunPyBulletEnv-v0", {"gang_lanes": 32})])
 def test_gang_kernel_matches_lane_kernel_teacher_forced(env_id, opts):
-    """16-lanes-per-env gang kernel (distributed or replicated dynamics) vs the lane kernel:
-    same physics and row order, different float32 summation order (DPP tree dots,
-    level-order composites) and constant-table transforms."""
-    assert _variant_vs_lane(env_id, 256, 30, **opts) == 16
+    """Gang kernel (16 or 32 lanes per env; distributed dynamics with the front-parallel
+    factorisation, or replicated dynamics) vs the lane kernel: same physics and row order,
+    different float32 summation order (DPP tree dots, level-order composites, front Schur
+    sums) and constant-table transforms."""
+    assert _variant_vs_lane(env_id, 256, 30, **opts) == opts.get("gang_lanes", 16)
 
 
-def test_gang_workspace_contacts_bitwise_equal_lds_contacts():
+@pytest.mark.parametrize("lanes", [16, 32])
+def test_gang_workspace_contacts_bitwise_equal_lds_contacts(lanes):
     """Gang contacts past the LDS capacity live in the device workspace: forcing every
     contact there (lds_rows=0) must not change a single bit (Humanoid: floor + self)."""
-    a, ca = _rollout("HumanoidPyBulletEnv-v0")
-    b, cb = _rollout("HumanoidPyBulletEnv-v0", lds_rows=0)
+    a, ca = _rollout("HumanoidPyBulletEnv-v0", gang_lanes=lanes)
+    b, cb = _rollout("HumanoidPyBulletEnv-v0", lds_rows=0, gang_lanes=lanes)
     assert ca.max() > 0
     np.testing.assert_array_equal(ca, cb)
     np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-@pytest.mark.parametrize("env_id", ["HumanoidPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0"])
-def test_gang_kernel_determinism_and_offset_invariance(env_id):
+@pytest.mark.parametrize("env_id,lanes", [("HumanoidPyBulletEnv-v0", 16), ("HalfCheetahPyBulletEnv-v0", 16),
+                                           ("HumanoidPyBulletEnv-v0", 32)])
+def test_gang_kernel_determinism_and_offset_invariance(env_id, lanes):
     """Bitwise reruns; env i of a batch starting at env_offset k == env k+i of a full batch
     (a partially filled last wave must not disturb the others)."""
     def run(n, off):
-        env = VecEnv(env_id, n, seed=21, env_offset=off, autoreset=True)
-        assert env.info.lanes_per_env == 16
+        env = VecEnv(env_id, n, seed=21, env_offset=off, autoreset=True, gang_lanes=lanes)
+        assert env.info.lanes_per_env == lanes
         env.reset()
         g = torch.Generator(device="cuda").manual_seed(0)
         acts = torch.rand((30, 97, env.info.action_dim), device="cuda", generator=g) * 2 - 1

@@ -68,13 +68,16 @@ def test_policy_weights_fixture_shapes():
 @pytest.mark.gpu
 @pytest.mark.parametrize("env_id", list(BANDS))
 def test_pretrained_policy_device(env_id):
-    """Same bands through the HIP step kernel, 64 episodes (trajectories diverge from the
-    oracle's chaotically after contact events; the score distribution must not)."""
+    """Same bands through the HIP step kernel, 256 episodes (trajectories diverge from the
+    oracle's chaotically after contact events; the score distribution must not).  256, not 64:
+    the Walker2D's returns spread from 10 to 1,100 per episode, and a 64-episode mean moved across
+    its band floor between kernel builds of identical physics (round 4: 118 against the oracle's
+    170 over 256 episodes)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import pybulletgym_amd  # noqa: F401
     _, floor, ratio = BANDS[env_id]
-    ret, length = policies.episode_returns_device(env_id, 64, seed=0)
+    ret, length = policies.episode_returns_device(env_id, 256, seed=0)
     rnd = policies.random_returns_oracle(env_id, 8, seed=0)
     assert np.isfinite(ret).all()
     assert ret.mean() >= floor, (ret.mean(), length.mean())

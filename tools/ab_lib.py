@@ -1,7 +1,7 @@
 """A/B timing of two builds of libpbg_amd.so on the same GPU (dev tool): each variant runs in
 its own subprocess (the library is loaded once per process), alternating A, B, A, B; each run
 is bench-like (Philox actions, pre-roll, one HIP graph of the timed steps).
-python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST] ...
+python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST[:GANG_LANES]] ...
 LIB_A / LIB_B: a libpbg_amd.so (run with this tree's Python package) or a directory holding a
 whole tree snapshot (its pybulletgym_amd.py, pybullet-gym_amd/ and built library), for a base
 whose C-ABI predates the current package's."""
@@ -17,7 +17,9 @@ from pybulletgym_amd import _native
 _native.LIB_PATH = "{lib}"
 from pybulletgym_amd.vec_env import VecEnv, sample_actions
 env_id, n = "{env}", {n}
-env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, gang_dist={gd})
+kw = dict(gang_dist={gd})
+if {gl} > 0: kw["gang_lanes"] = {gl}
+env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, **kw)
 env.reset()
 K, P = 300, 200
 acts = sample_actions(env.info.action_dim, n, P + K, seed=0x5EED)
@@ -30,11 +32,11 @@ print("%.5f" % (e0.elapsed_time(e1) / K))
 '''
 
 
-def run(lib, env, n, gd=-1):
+def run(lib, env, n, gd=-1, gl=-1):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if os.path.isdir(lib):
         repo, lib = lib, os.path.join(lib, "pybullet-gym_amd", "libpbg_amd.so")
-    code = CHILD.format(repo=os.path.abspath(repo), lib=os.path.abspath(lib), env=env, n=n, gd=gd)
+    code = CHILD.format(repo=os.path.abspath(repo), lib=os.path.abspath(lib), env=env, n=n, gd=gd, gl=gl)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if out.returncode:
         raise RuntimeError(out.stderr[-2000:])
@@ -44,10 +46,11 @@ def run(lib, env, n, gd=-1):
 if __name__ == "__main__":
     a, b = sys.argv[1], sys.argv[2]
     for spec in sys.argv[3:]:
-        env, n, *gd = spec.split(":")  # ENV:N[:GANG_DIST]
-        gd = int(gd[0]) if gd else -1
+        env, n, *opt = spec.split(":")  # ENV:N[:GANG_DIST[:GANG_LANES]]
+        gd = int(opt[0]) if opt else -1
+        gl = int(opt[1]) if len(opt) > 1 else -1
         ta, tb = [], []
         for _ in range(2):
-            ta.append(run(a, env, int(n), gd))
-            tb.append(run(b, env, int(n), gd))
+            ta.append(run(a, env, int(n), gd, gl))
+            tb.append(run(b, env, int(n), gd, gl))
         print(f"{env:28s} n={n:>6s}  A {min(ta):.4f} ms  B {min(tb):.4f} ms  B/A {min(tb) / min(ta):.3f}", flush=True)

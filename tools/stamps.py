@@ -12,16 +12,18 @@ L.pbg_debug_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p]
 names = ["kin+vel", "composites+M", "cholesky+solve", "limit rows", "contact rows", "PGS (rest)", "integrate", "act+load", "pack",
          "store", "-", "PGS limit rows", "PGS normals", "PGS frictions"]
 gang_names = {0: "dist: forward levels", 1: "dist: inertia + motion", 2: "dist: composites", 3: "dist: M + bias",
-              10: "replicated Cholesky + stage", 4: "detect",
+              10: "factorisation + solves (front-parallel)", 4: "detect",
               11: "rows (jobs)", 5: "PGS", 6: "integrate", 7: "act+load", 13: "pack: bookkeeping loads",
               14: "pack: gather FK", 15: "pack: gather quat", 12: "pack: gather vel, parts, joints",
               8: "pack: walker pack (float64)", 9: "store (+ auto-reset)"}
 AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
-# ENV:N[:GANG_DIST]  (GANG_DIST 0/1 forces the gang kernel's replicated / distributed dynamics)
+# ENV:N[:GANG_DIST[:GANG_LANES]]  (GANG_DIST 0/1 forces the gang kernel's replicated / distributed
+# dynamics, -1 the plan's; GANG_LANES 16 / 32 the gang width)
 for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
     env_id, n, *rest = spec.split(":")
     n = int(n)
-    env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET, gang_dist=int(rest[0]) if rest else -1)
+    env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET, gang_dist=int(rest[0]) if rest else -1,
+                 gang_lanes=int(rest[1]) if len(rest) > 1 else -1)
     env.reset()
     acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
     for i in range(200): env.step(acts[i % 30])  # pre-roll off the reset pose, as bench.py
@@ -42,6 +44,6 @@ for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
         waves = -(-n * lpe // 64)
     tot = sum(buf[i] for i in range(16))
     print(f"{env_id} n={n} lanes/env={lpe}: cycles per wave per env-step = {tot / waves / steps:.0f}")
-    labels = gang_names if lpe == 16 else dict(enumerate(names))
+    labels = gang_names if lpe >= 16 else dict(enumerate(names))
     for i in sorted(labels, key=lambda k: list(labels).index(k)):
         print(f"   {labels[i]:26s} {buf[i] / waves / steps:10.0f}  {100.0 * buf[i] / tot:5.1f}%")
