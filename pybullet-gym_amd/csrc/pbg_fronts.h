@@ -33,6 +33,7 @@
 namespace pbg {
 
 constexpr int FRONTS_MAX = 8;
+constexpr int FRONT_MIN_DOF = 14;  // generalized coordinates from which a robot takes the front path
 constexpr int FRONT_DOF_MAX = 40;
 
 template <class R>
@@ -97,7 +98,10 @@ constexpr FrontPlan<R> make_front_plan() {
   for (int b = -1; b < R::NL; b++) any_branch = any_branch || dof_children<R>(b) >= 2;
   // fronts: non-trunk dof-carrying children of the base or of trunk links
   int nf = 0;
-  bool ok = any_branch && N <= FRONT_DOF_MAX;
+  // small trees (Walker2D, HalfCheetah: 9 dofs, a 36-entry factor) keep the replicated algebra:
+  // there the group sums and the staging cost more than the factorisation they split (round-4
+  // A/B: Walker2D +2.6 %, HalfCheetah +1 % on the front path)
+  bool ok = any_branch && N <= FRONT_DOF_MAX && N >= FRONT_MIN_DOF;
   for (int c = 0; c < R::NL && ok; c++) {
     const int par = R::link_parent[c];
     if (link_in_trunk<R>(c) || !link_has_dof_subtree<R>(c)) continue;

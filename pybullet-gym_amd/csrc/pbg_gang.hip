@@ -358,9 +358,10 @@ template <class R, int T>
 struct Gang {
   using D = Dims<R>;
   static constexpr int N = R::NDOF, NNZ = D::NNZ, NB = D::NB, NLIM = D::NLIM;
-  static constexpr int NSL = (N + T - 1) / T;  // u entries per lane
+  static constexpr int NY = D::NY;             // row length: the robot's dofs (+ the cube's 6)
+  static constexpr int NSL = (NY + T - 1) / T;  // u entries per lane
   static constexpr int YS = NSL * T;           // padded row length
-  static constexpr int MAXC = R::NS + R::NPAIR;
+  static constexpr int MAXC = D::NC;  // floor slots, self pairs (+ the cube's corners and robot geoms)
   static constexpr int DW = 16;                // descriptor: rA 3 | rB 3 | n 3 | dist | fA | fB | mA | mB | floor | pad
   // rows of NSL = 2 robots (Humanoid) are laid out for one ds_read_b64 of a lane's y pair:
   // an even row length, the first row at an even LDS word (the env region, FIXED and the
@@ -376,12 +377,15 @@ struct Gang {
   static constexpr int FW = 12;                // its frame part (Rm | x) lives at O_FR, stride FW; the
   static constexpr int KW = BW - FW;           // kinematic part (c | w | v | al | ac) at O_KV, stride KW
   static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
-  static constexpr int O_L = 0, O_LD = O_L + NNZ, O_U = O_LD + N, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
+  // the factor, 1 / diag and u start on 16-byte boundaries (b128 loads; the env region is aligned)
+  static constexpr int NNZ4 = (NNZ + 3) & ~3, N4 = (N + 3) & ~3;
+  static constexpr int O_L = 0, O_LD = O_L + NNZ4, O_U = O_LD + N4, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
   static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
   // the base's state words [p 3 | quat 4 | v 3 | w 3] (front path: the env's state lives in LDS
   // through the sub-steps, q / qd at O_Q / O_QD)
   static constexpr int O_BS = O_JO + 3 * NJ1;
-  static constexpr int O_FR = O_BS + 13, O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
+  static constexpr int O_CS = O_BS + 13;  // HumanoidFlagrunHarder: the cube's state words (same layout)
+  static constexpr int O_FR = O_CS + (R::harder ? 13 : 0), O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
   // front path (pbg_fronts.h) of the distributed dynamics: state in LDS, front-parallel algebra
   static constexpr bool LST = FP<R>::NF > 0;
   // the composites (dead once M is built) share their words with the limit rows
@@ -1175,8 +1179,19 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
       X.l[G::O_LD + FP<R>::v.tg[t]] = Ldt[t];
       X.l[G::O_U + FP<R>::v.tg[t]] = u;
     });
+    if constexpr (R::harder) {
+      // the cube (block-diagonal, factor diag(sqrt m x3, sqrt I x3)): u_c = L_c^T nu_c of its
+      // free-body unconstrained velocity (cube_unconstrained on the LDS copy of its state)
+      State<R> cs;
 #pragma unroll
-    for (int i = R::NDOF; i < G::YS; i++) X.l[G::O_U + i] = 0.f;
+      for (int i = 0; i < 3; i++) { cs.cube.v[i] = X.l[G::O_CS + 7 + i]; cs.cube.w[i] = X.l[G::O_CS + 10 + i]; }
+      float uc[6];
+      cube_unconstrained<R>(cs, uc, X.P);
+#pragma unroll
+      for (int i = 0; i < 6; i++) X.l[G::O_U + R::NDOF + i] = uc[i];
+    }
+#pragma unroll
+    for (int i = D::NY; i < G::YS; i++) X.l[G::O_U + i] = 0.f;
     static_for<0, D::NLIM>([&](auto li_c) {
       constexpr int li = decltype(li_c)::value;
       constexpr int d = D::LIM.v[li][0];
@@ -1188,95 +1203,93 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
   (void)s;
 }
 
-// Front-parallel replacement of integrate's back-substitution: nu = L^-T u from the staged
-// factor and the solved u (LDS), clamped; the fronts' and trunk's parts meet in LDS (O_RHS, dead
-// after the solve) and every lane then integrates the replicated state.
+// The staged factor (word order pbg_fronts.h) and 1 / diag(L) into registers, as 16-byte LDS loads
+template <class R, int T>
+PBG_DEV void gang_load_factor(const GangCtx& X, float* L, float* Ld) {
+  using G = Gang<R, T>;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const v4f lds_v4f;
+  const lds_v4f* pl = (const lds_v4f*)(X.l + G::O_L);
+#pragma unroll
+  for (int k = 0; k < G::NNZ4 / 4; k++) {
+    const v4f a = pl[k];
+    L[4 * k] = a.x; L[4 * k + 1] = a.y; L[4 * k + 2] = a.z; L[4 * k + 3] = a.w;
+  }
+  const lds_v4f* pd = (const lds_v4f*)(X.l + G::O_LD);
+#pragma unroll
+  for (int k = 0; k < G::N4 / 4; k++) {
+    const v4f a = pd[k];
+    Ld[4 * k] = a.x; Ld[4 * k + 1] = a.y; Ld[4 * k + 2] = a.z; Ld[4 * k + 3] = a.w;
+  }
+}
+
+// The front path's integration: nu = L^-T u (replicated, the factor in registers from 16-byte
+// loads), clamped; the env's LDS state advanced by semi-implicit Euler (lane d < NJ its joint d,
+// the base and the cube by lane 0; the next sub-step reads them after its first gang sync)
 template <class R, int T>
 PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
   using G = Gang<R, T>;
-  using TT = TrunkTab<R>;
-  constexpr int NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NJ = R::NJ, N = R::NDOF;
+  using D = Dims<R>;
+  constexpr int NJ = R::NJ, N = R::NDOF;
   const float dt = X.P.dt;
   const float vmax = (float)PBG_MAX_COORD_VELOCITY;
-  const int q = opaque_lane(X.t) % GRP;
-  const int cls = q < NF ? front_pick<R>(q, [](int f) { return FP<R>::v.cls[f]; }) : -1;
-  const int boff = front_pick<R>(q, [](int f) { return FP<R>::v.off[f]; });
-  const int g0 = front_pick<R>(q, [](int f) { return FP<R>::v.g0[f]; });
-  // trunk: x_t = L_t^-T u_t
-  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
-  float xt[NT];
-  static_for<0, NT>([&](auto r_c) {
-    constexpr int t = NT - 1 - decltype(r_c)::value;
-    float v = X.l[G::O_U + FP<R>::v.tg[t]];
-    static_for<t + 1, NT>([&](auto k_c) {
-      constexpr int k = decltype(k_c)::value;
-      if constexpr (TT::pos(k, t) >= 0) v -= tb[TT::pos(k, t)] * xt[k];
-    });
-    xt[t] = v * X.l[G::O_LD + FP<R>::v.tg[t]];
-  });
-  const bool wf = X.t < GRP && q < NF;
-  static_for<0, FP<R>::v.ncls>([&](auto c_c) {
-    constexpr int C = decltype(c_c)::value;
-    using FC = FrontCls<R, C>;
-    constexpr int n = FC::n;
-    if (cls != C) return;
-    const lds_float* blk = X.l + G::O_L + boff;
-    float xf[n];
-    static_for<0, n>([&](auto r_c) {
-      constexpr int a = n - 1 - decltype(r_c)::value;
-      float v = X.l[G::O_U + g0 + a];
-      static_for<a + 1, n>([&](auto b_c) {
-        constexpr int b = decltype(b_c)::value;
-        if constexpr (FC::cpl(b, a)) v -= blk[FC::a_off(b, a)] * xf[b];
-      });
-      static_for<0, NT>([&](auto t_c) {
-        constexpr int t = decltype(t_c)::value;
-        if constexpr (FC::tc(t)) v -= blk[FC::c_off(a, t)] * xt[t];
-      });
-      xf[a] = v * X.l[G::O_LD + g0 + a];
-    });
-    if (wf) {
-      static_for<0, n>([&](auto a_c) {
-        constexpr int a = decltype(a_c)::value;
-        X.l[G::O_RHS + g0 + a] = clampf(xf[a], -vmax, vmax);
-      });
-    }
-  });
-  if (X.t == 0) {
-    static_for<0, NT>([&](auto t_c) {
-      constexpr int t = decltype(t_c)::value;
-      X.l[G::O_RHS + FP<R>::v.tg[t]] = clampf(xt[t], -vmax, vmax);
-    });
-  }
-  PBG_GANG_SYNC
-  // semi-implicit Euler of the env's LDS state (one writer; the next sub-step reads it after its
-  // first gang sync)
-  if (X.t == 0) {
+  float L[G::NNZ4], Ld[G::N4], nu[N];
+  gang_load_factor<R, T>(X, L, Ld);
 #pragma unroll
-    for (int d = 0; d < NJ; d++) {
-      const float qd = X.l[G::O_RHS + Dims<R>::gj(d)];
+  for (int i = N - 1; i >= 0; i--) {
+    float t = X.l[G::O_U + i];
+#pragma unroll
+    for (int kk = i + 1; kk < N; kk++)
+      if (D::coupled(kk, i)) t -= L[FP<R>::idx(kk, i)] * nu[kk];
+    nu[i] = t * Ld[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) nu[i] = clampf(nu[i], -vmax, vmax);
+  // lane t: joints t, t + T, ... (each velocity picked from the replicated nu by selects)
+  static_for<0, (NJ + T - 1) / T>([&](auto r_c) {
+    constexpr int r = decltype(r_c)::value;
+    float qd = nu[D::gj(r * T)];
+    static_for<r * T + 1, (r * T + T < NJ ? r * T + T : NJ)>([&](auto d_c) {
+      constexpr int d = decltype(d_c)::value;
+      qd = X.t == d - r * T ? nu[D::gj(d)] : qd;
+    });
+    const int d = r * T + X.t;
+    if (d < NJ) {
       X.l[G::O_QD + d] = qd;
       X.l[G::O_Q + d] += dt * qd;
     }
+  });
+  if (X.t == 0) {
     if constexpr (R::floating) {
       float bq[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) bq[i] = X.l[G::O_BS + 3 + i];
-      f3 w;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        const float v = X.l[G::O_RHS + NJ + i], wi = X.l[G::O_RHS + NJ + 3 + i];
-        X.l[G::O_BS + 7 + i] = v;
-        X.l[G::O_BS + 10 + i] = wi;
-        X.l[G::O_BS + i] += dt * v;
-        (i == 0 ? w.x : (i == 1 ? w.y : w.z)) = wi;
+        X.l[G::O_BS + 7 + i] = nu[NJ + i];
+        X.l[G::O_BS + 10 + i] = nu[NJ + 3 + i];
+        X.l[G::O_BS + i] += dt * nu[NJ + i];
       }
-      free_body_quat(bq, w, X.P);
+      free_body_quat(bq, mk3(nu[NJ + 3], nu[NJ + 4], nu[NJ + 5]), X.P);
 #pragma unroll
       for (int i = 0; i < 4; i++) X.l[G::O_BS + 3 + i] = bq[i];
     }
+    if constexpr (R::harder) {  // the cube: nu_c = L_c^-T u_c, clamp, semi-implicit Euler (cube_integrate)
+      State<R> cs;
+#pragma unroll
+      for (int i = 0; i < 3; i++) cs.cube.p[i] = X.l[G::O_CS + i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) cs.cube.q[i] = X.l[G::O_CS + 3 + i];
+      float uc[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) uc[i] = X.l[G::O_U + N + i];
+      cube_integrate<R>(cs, uc, X.P);
+#pragma unroll
+      for (int i = 0; i < 3; i++) { X.l[G::O_CS + i] = cs.cube.p[i]; X.l[G::O_CS + 7 + i] = cs.cube.v[i]; X.l[G::O_CS + 10 + i] = cs.cube.w[i]; }
+#pragma unroll
+      for (int i = 0; i < 4; i++) X.l[G::O_CS + 3 + i] = cs.cube.q[i];
+    }
   }
-  (void)N;
   (void)s;
 }
 // the env's state record between registers and its LDS copy (front path)
@@ -1290,6 +1303,12 @@ PBG_DEV void gang_put_state(const State<R>& s, const GangCtx& X) {
     for (int i = 0; i < 3; i++) { X.l[G::O_BS + i] = s.bp[i]; X.l[G::O_BS + 7 + i] = s.bv[i]; X.l[G::O_BS + 10 + i] = s.bw[i]; }
 #pragma unroll
     for (int i = 0; i < 4; i++) X.l[G::O_BS + 3 + i] = s.bq[i];
+    if constexpr (R::harder) {
+#pragma unroll
+      for (int i = 0; i < 3; i++) { X.l[G::O_CS + i] = s.cube.p[i]; X.l[G::O_CS + 7 + i] = s.cube.v[i]; X.l[G::O_CS + 10 + i] = s.cube.w[i]; }
+#pragma unroll
+      for (int i = 0; i < 4; i++) X.l[G::O_CS + 3 + i] = s.cube.q[i];
+    }
   }
 }
 template <class R, int T>
@@ -1301,6 +1320,12 @@ PBG_DEV void gang_get_state(State<R>& s, const GangCtx& X) {
   for (int i = 0; i < 3; i++) { s.bp[i] = X.l[G::O_BS + i]; s.bv[i] = X.l[G::O_BS + 7 + i]; s.bw[i] = X.l[G::O_BS + 10 + i]; }
 #pragma unroll
   for (int i = 0; i < 4; i++) s.bq[i] = X.l[G::O_BS + 3 + i];
+  if constexpr (R::harder) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) { s.cube.p[i] = X.l[G::O_CS + i]; s.cube.v[i] = X.l[G::O_CS + 7 + i]; s.cube.w[i] = X.l[G::O_CS + 10 + i]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) s.cube.q[i] = X.l[G::O_CS + 3 + i];
+  }
 }
 
 // ------------------------------------------------------------------ one physics sub-step
@@ -1335,6 +1360,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       });
     }
   };
+  // the replicated path keeps its factor in registers from the factorisation through the rows pass
+  // (the distributed path loads it from its LDS staging before the rows pass)
+  float Lr[G::NNZ4], Ldr[G::N4];
   if constexpr (DIST) {
     // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
 #ifndef PBG_DEV_NODYN
@@ -1344,10 +1372,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   } else {
     // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
     {
-      float L[D::NNZ], Ld[N], nu[N], u[N];
-      dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
+      float nu[N], u[N];
+      dynamics<R>(s, tau, Lr, Ldr, nu, u, P SUB_STAMP_PASS);
       STAMP(3)
-      stage_solution(L, Ld, u);
+      stage_solution(Lr, Ldr, u);
     }
     Kin<R> k;
     f3 sw[N], sv[N], O0;
@@ -1379,9 +1407,13 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     for (int i = 0; i < 9; i++) Rm.m[i] = p[i];
     x = mk3(p[9], p[10], p[11]);
   };
-  auto put_desc = [&](int c, f3 rA, f3 rB, f3 n, float dist, float fB, uint32_t mA, uint32_t mB, float floor_, float mu) {
-    const float v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, 1.f, fB,
-                            __builtin_bit_cast(float, mA), __builtin_bit_cast(float, mB), floor_, 0.f};
+  // descriptor: rA | rB | n | dist | fA (body A carries the base dofs) | fB (body B does) | chain masks of
+  // A and B | floor | cube (+1: A is HumanoidFlagrunHarder's cube, -1: B is, 0: no cube; its lever
+  // arm from the cube's centre is then rA, resp. rB)
+  auto put_desc = [&](int c, f3 rA, f3 rB, f3 n, float dist, float fB, uint32_t mA, uint32_t mB, float floor_, float mu,
+                      float fA = 1.f, float cube = 0.f) {
+    const float v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, fA, fB,
+                            __builtin_bit_cast(float, mA), __builtin_bit_cast(float, mB), floor_, cube};
     contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
       for (int w = 0; w < G::DW; w++) p[w] = v[w];
@@ -1496,6 +1528,100 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       nc += __popcll(bal & gang_mask);
     }
   }
+  // --- distributed: HumanoidFlagrunHarder's cube -- its 8 corners vs the floor, then every robot
+  // collision geom vs the box (oracle detect_cube_contacts / the lane kernel's cube_contacts), one
+  // candidate per lane, compacted in candidate order ------------------------------------------
+  if constexpr (R::harder) {
+    constexpr int NCC = 8 + R::NCG;
+    const float h = (float)PBG_CUBE_HALF, thr = (float)PBG_CONTACT_THRESHOLD;
+    const m3 Rc = quat_to_m3(X.l[G::O_CS + 3], X.l[G::O_CS + 4], X.l[G::O_CS + 5], X.l[G::O_CS + 6]);
+    const f3 xc = mk3(X.l[G::O_CS], X.l[G::O_CS + 1], X.l[G::O_CS + 2]);
+#pragma unroll
+    for (int r = 0; r < (NCC + T - 1) / T; r++) {
+      const int k = r * T + X.t;
+      bool act = false;
+      f3 rA, rB, nrm;
+      float dist = 0.f, mu = 0.f, fA = 1.f, cube = 0.f, flo = 0.f;
+      uint32_t mA = 0u;
+      if (k < 8) {  // corner k vs the floor: A = the cube, normal +z
+        const f3 lc = mk3((k & 1) ? h : -h, (k & 2) ? h : -h, (k & 4) ? h : -h);
+        const f3 pp = xc + mul(Rc, lc);
+        act = pp.z < thr;
+        rA = pp - xc; rB = mk3(0, 0, 0); nrm = mk3(0, 0, 1);
+        dist = pp.z; mu = (float)R::cube_floor_mu; fA = 0.f; cube = 1.f; flo = 1.f;
+      } else if (k < NCC) {  // robot geom g vs the box: A = the robot link, B = the cube
+        const int g = k - 8;
+        int lnk = 0;
+        float gp0[3], gp1[3], rr = 0.f, gmu = 0.f;
+        static_for<0, R::NCG>([&](auto g_c) {  // the geom's constants by selects (no table loads)
+          constexpr int gg = decltype(g_c)::value;
+          if (g == gg) {
+            lnk = R::cgeom_link[gg];
+#pragma unroll
+            for (int i = 0; i < 3; i++) { gp0[i] = (float)R::cgeom_p0[gg][i]; gp1[i] = (float)R::cgeom_p1[gg][i]; }
+            rr = (float)R::cgeom_r[gg];
+            gmu = (float)R::cgeom_mu[gg];
+          }
+        });
+        m3 Rm; f3 x;
+        frame(lnk + 1, Rm, x);
+        const f3 e0 = x + mul(Rm, mk3(gp0[0], gp0[1], gp0[2])), e1 = x + mul(Rm, mk3(gp1[0], gp1[1], gp1[2]));
+        m3 Rt;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) Rt.m[3 * i + j] = Rc.m[3 * j + i];
+        const f3 p0 = mul(Rt, e0 - xc), p1 = mul(Rt, e1 - xc), d = p1 - p0;
+        const float dd = dot3(d, d);
+        const float t0 = dd > 1e-12f ? fminf(fmaxf(-dot3(p0, d) / dd, 0.f), 1.f) : 0.f;
+        const float bound = (float)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
+        if (norm3(p0 + t0 * d) < bound + rr + thr) {
+          float t = 0.f;
+          if (dd > 1e-12f) {  // golden-section minimisation of the box's signed distance along the segment
+            const float phi = 0.6180339887498949f;
+            float a = 0.f, bb = 1.f;
+            float x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
+            float f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
+#pragma unroll 1
+            for (int it = 0; it < PBG_CUBE_GS_ITERS; it++) {
+              if (f1 <= f2) { bb = x2; x2 = x1; f2 = f1; x1 = bb - phi * (bb - a); f1 = box_sd(p0 + x1 * d, h); }
+              else { a = x1; x1 = x2; f1 = f2; x2 = a + phi * (bb - a); f2 = box_sd(p0 + x2 * d, h); }
+            }
+            t = 0.5f * (a + bb);
+          }
+          const f3 ps = p0 + t * d;
+          dist = box_sd(ps, h) - rr;
+          act = dist < thr;
+          f3 nb, qb;
+          const float qx = fabsf(ps.x) - h, qy = fabsf(ps.y) - h, qz = fabsf(ps.z) - h;
+          if (fmaxf(qx, fmaxf(qy, qz)) > 0.f) {
+            qb = mk3(fminf(fmaxf(ps.x, -h), h), fminf(fmaxf(ps.y, -h), h), fminf(fmaxf(ps.z, -h), h));
+            const f3 dv = ps - qb;
+            const float l = norm3(dv);
+            nb = l > 1e-9f ? (1.f / l) * dv : mk3(0, 0, 1);
+          } else {
+            const int ax = (qx >= qy && qx >= qz) ? 0 : (qy >= qz ? 1 : 2);
+            const float cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
+            const float sg = cc < 0.f ? -1.f : 1.f;
+            nb = mk3(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
+            qb = mk3(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
+          }
+          nrm = mul(Rc, nb);
+          const f3 PA = xc + mul(Rc, ps) - rr * nrm, PB = xc + mul(Rc, qb);
+          rA = PA - O; rB = PB - xc;
+          mu = gmu; cube = -1.f;
+          mA = lnk >= 0 ? TB.chain[lnk + 1] : 0u;
+        }
+      }
+      const uint64_t bal = __ballot(act);
+      if (act) {
+        csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + k));
+        const int c = nc + __popcll(bal & gang_mask & below);
+        put_desc(c, rA, rB, nrm, dist, 0.f, mA, 0u, flo, mu, fA, cube);
+      }
+      nc += __popcll(bal & gang_mask);
+    }
+  }
   PBG_GANG_SYNC
   STAMP(4)
   if constexpr (DIST) {
@@ -1521,6 +1647,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #else
   const int njobs = NLIM + 3 * nc;
 #endif
+  if constexpr (DIST) gang_load_factor<R, T>(X, Lr, Ldr);
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
     if (j >= njobs) continue;
@@ -1528,6 +1655,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     const bool is_lim = j < NLIM;
     int c = 0, dir = 0;
     float dist = 0.f;
+    float cubef = 0.f;            // HumanoidFlagrunHarder: the contact's cube side (descriptor word 15)
+    f3 ycl = mk3(0, 0, 0), cubes = mk3(0, 0, 0);  // and the cube part of y (linear | angular)
     if (is_lim) {
       const int g = TB.lim_g[j];
 #pragma unroll
@@ -1557,10 +1686,20 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       }
       const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
       const f3 mmA = cross3(rA, nd), mmB = cross3(rB, nd);
+      cubef = v[15];
+      cubes = mk3(0, 0, 0);
+      if constexpr (R::harder) {  // the cube's columns: +-(nd / sqrt m, (r x nd) / sqrt I), r its lever arm
+        const f3 rc = cubef > 0.f ? rA : rB;
+        const f3 mc = cross3(rc, nd);
+        const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+        ycl = cubef * rm * nd;
+        cubes = cubef * rI * mc;
+      }
+      const float fA = v[10];
 #pragma unroll
       for (int i = 0; i < N; i++) {
         const int di = D::dof_of(i);
-        const bool inA = di < 0 || ((mA >> di) & 1u), inB = di < 0 ? fB != 0.f : ((mB >> di) & 1u) != 0u;
+        const bool inA = di < 0 ? fA != 0.f : ((mA >> di) & 1u) != 0u, inB = di < 0 ? fB != 0.f : ((mB >> di) & 1u) != 0u;
         const f3 sw = mk3(X.l[G::O_SW + 3 * i], X.l[G::O_SW + 3 * i + 1], X.l[G::O_SW + 3 * i + 2]);
         const f3 sv = mk3(X.l[G::O_SV + 3 * i], X.l[G::O_SV + 3 * i + 1], X.l[G::O_SV + 3 * i + 2]);
         float tj = 0.f;
@@ -1569,10 +1708,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         J[i] = tj;
       }
     }
-    // y = L^-1 J (forward substitution over the compile-time pattern of L; the factor is read
-    // from its LDS staging -- the gang's lanes read the same words, a broadcast -- instead of being
-    // held in registers from the factorisation through the detection and this pass)
-    const lds_float* Lx = X.l + G::O_L;
+    // y = L^-1 J (forward substitution over the compile-time pattern of L, held in registers for
+    // the pass: 16-byte loads of the staged factor before the job loop)
     float y[N];
     float D2 = 0.f;
 #pragma unroll
@@ -1580,10 +1717,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       float tt = J[i];
 #pragma unroll
       for (int kk = 0; kk < i; kk++)
-        if (D::coupled(i, kk)) tt -= Lx[FP<R>::idx(i, kk)] * y[kk];
-      y[i] = tt * X.l[G::O_LD + i];
+        if (D::coupled(i, kk)) tt -= Lr[DIST ? FP<R>::idx(i, kk) : D::lidx(i, kk)] * y[kk];
+      y[i] = tt * Ldr[i];
       D2 += y[i] * y[i];
     }
+    if constexpr (R::harder) D2 += dot3(ycl, ycl) + dot3(cubes, cubes);
     const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
     if (is_lim) {
       const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
@@ -1599,8 +1737,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       const float tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
       contact_at<R, T>(X, c, [&](auto p0) {
         auto p = p0 + w0r;
+        const float yc[6] = {ycl.x, ycl.y, ycl.z, cubes.x, cubes.y, cubes.z};
 #pragma unroll
-        for (int i = 0; i < YS; i++) p[G::yw(i)] = i < N ? y[i] : 0.f;
+        for (int i = 0; i < YS; i++) p[G::yw(i)] = i < N ? y[i] : (i < G::NY ? yc[(i - N) % 6] : 0.f);
         p[YS] = meff;
         p[YS + 1] = tgt;
         p[YS + 2] = 0.f;
@@ -1688,7 +1827,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 template <class R, int T>
 PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __restrict__ st, int n,
                         float* __restrict__ obs_out, int e, int t) {
-  constexpr int SW = PBG_BASE_WORDS + 2 * R::NJ;
+  constexpr int SW = PBG_STATE_WORDS(R::NJ, R::harder);
   float w[SW];  // store_state's word order
 #pragma unroll
   for (int i = 0; i < 3; i++) { w[i] = s.bp[i]; w[7 + i] = s.bv[i]; w[10 + i] = s.bw[i]; }
@@ -1696,6 +1835,13 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
   for (int i = 0; i < 4; i++) w[3 + i] = s.bq[i];
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) { w[PBG_BASE_WORDS + d] = s.q[d]; w[PBG_BASE_WORDS + R::NJ + d] = s.qd[d]; }
+  if constexpr (R::harder) {  // the cube's words after the robot's (sim_params.h)
+    constexpr int c0 = PBG_BASE_WORDS + 2 * R::NJ;
+#pragma unroll
+    for (int i = 0; i < 3; i++) { w[c0 + i] = s.cube.p[i]; w[c0 + 7 + i] = s.cube.v[i]; w[c0 + 10 + i] = s.cube.w[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[c0 + 3 + i] = s.cube.q[i];
+  }
   static_for<0, (SW + T - 1) / T>([&](auto m_c) {
     constexpr int m = decltype(m_c)::value;
     const float v = lanes_pick<T, m, SW>(w, t);
@@ -1771,8 +1917,8 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     const uint32_t sig = gang_sum_u32<T>(csig);
     if (w0) io.csig[e] = sig;
   }
-  // the pack's bookkeeping loads after the physics (issued before it they held registers through
-  // the sub-steps: +1-1.7 % on the gang robots, A/B)
+  // the pack's bookkeeping loads after the physics (issued before it: HalfCheetah -0.5 %, Humanoid
+  // +1.9 %, Walker2D +1.1 %, Hopper +0.5 % -- round-4 A/B, r04e; round 3 likewise)
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   const double pot_old = B.pot[e];
@@ -1781,6 +1927,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   PackOut po;
   double pot_new = 0.0;
   Flag fl = load_flag<R>(B, e);
+  HarderBk hb = load_harder<R>(B, e);
   STAMPX(13)
   if constexpr (R::kind == 1) {
     pendulum_pack<R>(s, obs, po);
@@ -1816,7 +1963,14 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
 #endif
     {
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
-    else flag_pack<R, 4>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, X.t);
+    else flag_pack<R, 4>(in, act, obs, po, fl, [&](Flag& f) { flag_draw(B, e, f); }, X.t, R::harder ? &hb : nullptr);
+    }
+    if constexpr (R::harder) {  // HumanoidFlagrunHarder's _step half (robot_locomotors.py:251-302)
+      double pos[3], vel[3];
+      if (harder_step<R>(B, e, in, obs, po, hb, pos, vel, nullptr)) {  // resetBasePosition / Velocity
+#pragma unroll
+        for (int i = 0; i < 3; i++) { s.cube.p[i] = (float)pos[i]; s.cube.v[i] = (float)vel[i]; s.cube.w[i] = 0.f; }
+      }
     }
     pot_new = po.potential;
     flags = (flags & 0xFFu) | (po.feet_out << 8);
@@ -1844,7 +1998,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     if (w0) B.episode[e] = epi + 1;
     // the reset's pack deals its transcendentals over the quad as the step's does (the gang's
     // 16 lanes take the branch together): Hopper, Walker2D and HalfCheetah reset often
-    reset_env_epi<R, 4>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl, nullptr, X.t);
+    reset_env_epi<R, 4>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl, R::harder ? &hb : nullptr, X.t);
     if (w0) {
       B.pot[e] = pot;
       B.z0[e] = z0;
@@ -1856,7 +2010,10 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     B.elapsed[e] = el;
     B.flags[e] = flags;
   }
-  if (w0) store_flag<R>(B, e, fl);
+  if (w0) {
+    store_flag<R>(B, e, fl);
+    if constexpr (R::harder) store_harder<R>(B, e, hb);
+  }
   gang_store<R, T>(s, obs, B.st, B.n, io.obs, e, X.t);
   STAMP(9)
   STAMP_FLUSH

@@ -81,7 +81,7 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
 // + 3 rows), contacts past the capacity spill to the device workspace.
 template <class RR, int T>
 static int plan_gang_t(int n_envs, int cus, Geometry* g) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder && (T == 16 || gang32_ok<RR>())) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>())) {
     using G = Gang<RR, T>;
     constexpr int EPB = gang_block<RR>() / T;  // envs per workgroup
     const int wgs = (n_envs + EPB - 1) / EPB;
@@ -103,8 +103,8 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
     g->gang_dist = RR::NDOF >= 8 || T >= 32 || (size_t)n_envs * T > (size_t)64 * 4 * cus;
-    // pbg_create_debug (32-lane gangs have no replicated-dynamics variant)
-    if ((g->force_dist == 0 || g->force_dist == 1) && T == 16) g->gang_dist = g->force_dist;
+    // pbg_create_debug (32-lane gangs and the cube robot have no replicated-dynamics variant)
+    if ((g->force_dist == 0 || g->force_dist == 1) && T == 16 && !RR::harder) g->gang_dist = g->force_dist;
     g->team = T;
     g->block = gang_block<RR>();
     g->lds_rows = cap;
@@ -115,7 +115,7 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     if (g->lds_bytes > (size_t)163840) return (int)hipErrorInvalidConfiguration;
     g->scratch_words_per_env = G::GWORDS;
     const void* fn;
-    if constexpr (T == 16)
+    if constexpr (T == 16 && !RR::harder)
       fn = g->gang_dist ? (const void*)gang_step_kernel<RR, T, true> : (const void*)gang_step_kernel<RR, T, false>;
     else
       fn = (const void*)gang_step_kernel<RR, T, true>;
@@ -135,9 +135,9 @@ static int plan_gang(int n_envs, int cus, Geometry* g, int lanes) {
 }
 template <class RR, int T>
 static bool launch_gang_t(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && !RR::harder && (T == 16 || gang32_ok<RR>())) {
+  if constexpr ((RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>())) {
     const dim3 grid(blocks(B.n, gang_block<RR>() / T)), blk(gang_block<RR>());
-    if constexpr (T == 16) {
+    if constexpr (T == 16 && !RR::harder) {
       if (!g.gang_dist) {
         hipLaunchKernelGGL((gang_step_kernel<RR, T, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows,
                            g.env_words);
@@ -216,7 +216,7 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
 // (a second free body per env) runs on the lane kernel only.
 int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
-  if (R::kind != 1 && !R::harder && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g, g->gang_lanes);
+  if (R::kind != 1 && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g, g->gang_lanes);
   return plan_lane<R>(n_envs, cus, g);
 }
 

@@ -357,8 +357,11 @@ struct TRows {
   int cap;          // rows resident in LDS
   int lane;         // lane in the wave (4 e + k)
   PBG_DEV lds_float& stage(int w) const { return lds[(size_t)w * ES]; }
-  PBG_DEV lds_float* P(int r) const { return rows + (size_t)r * ES * W + PW * lane; }
-  PBG_DEV lds_float* S(int r) const { return rows + (size_t)r * ES * W + SOFF + 4 * (lane >> 2); }
+  // row offsets by a 24-bit multiply (rows < 2^24): the 32-bit v_mul_lo_u32 the compiler chose for
+  // an unbounded row index is a quarter-rate instruction, two of them per normal row of the sweep
+  PBG_DEV int roff(int r) const { return (int)__umul24((unsigned)r, (unsigned)(ES * W)); }
+  PBG_DEV lds_float* P(int r) const { return rows + roff(r) + PW * lane; }
+  PBG_DEV lds_float* S(int r) const { return rows + roff(r) + SOFF + 4 * (lane >> 2); }
   // row words of lane k in the workspace ([word][env], stride n)
   PBG_DEV float* gP(int r, int k) const { return gbl + ((size_t)r * W + (size_t)k * PW) * n; }
   PBG_DEV float* gS(int r) const { return gbl + ((size_t)r * W + 4 * PW) * n; }
@@ -372,7 +375,7 @@ struct TRows {
       return k < 2 ? yB[k + 4] : 0.f;
     };
     if (r < cap) {
-      lds_float* p0 = rows + (size_t)r * ES * W + PW * (lane & ~3);
+      lds_float* p0 = rows + roff(r) + PW * (lane & ~3);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (slot < 0 && k != k0) continue;
