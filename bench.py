@@ -306,7 +306,10 @@ def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
                       "traffic_source": (f"pybullet-gym_amd/perf/{os.path.basename(pmc['_path'])} (round "
                                          f"{pmc.get('round')}: FETCH_SIZE/WRITE_SIZE PMC passes, corrected)")
                       if pmc else None,
-                      "kernel": kernel_name(env), "kernel_ms": kernel_ms, "alg_bytes_per_env_step": alg}}
+                      "kernel": kernel_name(env), "kernel_ms": kernel_ms, "alg_bytes_per_env_step": alg,
+                      # the step is FP32-VALU (issue / latency) bound, not HBM bound (SURVEY.md 8d,
+                      # BASELINE.md 4): the binding roofline is the `flop_roofline` block beside this one
+                      "binding": "valu-fp32", "binding_line": "flop_roofline"}}
     f = flops.get(SHORT.get(env.env_id, env.env_id))
     if f:
         tf = f["flops_per_env_step"] * n / (kernel_ms * 1e-3) / 1e12

@@ -325,15 +325,16 @@ int pbg_pack_record_sizes(const char* env_id, int* in_words, int* out_words) {
 #ifdef PBG_STAMPS
 // diagnostic build only: read and clear the per-phase wave-cycle sums of one robot's kernel
 int pbg_debug_stamps(int rid, unsigned long long* host_out) {
-  switch (rid) {
-    case 0: return pbg::debug_stamps_Pendulum(host_out);
-    case 1: return pbg::debug_stamps_Hopper(host_out);
-    case 2: return pbg::debug_stamps_HalfCheetah(host_out);
-    case 3: return pbg::debug_stamps_Ant(host_out);
-    case 4: return pbg::debug_stamps_Humanoid(host_out);
-    case 5: return pbg::debug_stamps_Walker2D(host_out);
-  }
-  return PBG_E_ENV;
+  using F = int (*)(unsigned long long*);
+  static const F table[17] = {pbg::debug_stamps_Pendulum, pbg::debug_stamps_Hopper, pbg::debug_stamps_HalfCheetah,
+                              pbg::debug_stamps_Ant, pbg::debug_stamps_Humanoid, pbg::debug_stamps_Walker2D,
+                              pbg::debug_stamps_PendulumSwingup, pbg::debug_stamps_DoublePendulum,
+                              pbg::debug_stamps_HumanoidFlagrun, pbg::debug_stamps_HopperMuJoCo,
+                              pbg::debug_stamps_Walker2DMuJoCo, pbg::debug_stamps_HalfCheetahMuJoCo,
+                              pbg::debug_stamps_AntMuJoCo, pbg::debug_stamps_HumanoidMuJoCo,
+                              pbg::debug_stamps_DoublePendulumMuJoCo, pbg::debug_stamps_HumanoidFlagrunHarder,
+                              pbg::debug_stamps_Atlas};
+  return (rid >= 0 && rid < 17) ? table[rid](host_out) : PBG_E_ENV;
 }
 #endif
 

@@ -377,17 +377,22 @@ struct Gang {
   static constexpr int FW = 12;                // its frame part (Rm | x) lives at O_FR, stride FW; the
   static constexpr int KW = BW - FW;           // kinematic part (c | w | v | al | ac) at O_KV, stride KW
   static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
-  // the factor, 1 / diag and u start on 16-byte boundaries (b128 loads; the env region is aligned)
-  static constexpr int NNZ4 = (NNZ + 3) & ~3, N4 = (N + 3) & ~3;
+  // front path (pbg_fronts.h) of the distributed dynamics: state in LDS, front-parallel algebra
+  static constexpr bool LST = FP<R>::NF > 0;
+  // front path: the factor, 1 / diag and u start on 16-byte boundaries (b128 loads; the env
+  // region is 16-byte aligned).  The small trees keep the round-3 layout (8-byte regions, no
+  // base-state words): the extra words shifted their regions' LDS banks and cost Walker2D 2 %
+  // with identical code (round-4 A/B)
+  static constexpr int REGION_ALIGN = LST ? 4 : 2;
+  static constexpr int NNZ4 = LST ? (NNZ + 3) & ~3 : NNZ, N4 = LST ? (N + 3) & ~3 : N;
   static constexpr int O_L = 0, O_LD = O_L + NNZ4, O_U = O_LD + N4, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
   static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
   // the base's state words [p 3 | quat 4 | v 3 | w 3] (front path: the env's state lives in LDS
   // through the sub-steps, q / qd at O_Q / O_QD)
   static constexpr int O_BS = O_JO + 3 * NJ1;
-  static constexpr int O_CS = O_BS + 13;  // HumanoidFlagrunHarder: the cube's state words (same layout)
+  static constexpr int O_CS = O_BS + (LST ? 13 : 0);  // HumanoidFlagrunHarder: the cube's state words (same layout)
   static constexpr int O_FR = O_CS + (R::harder ? 13 : 0), O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
-  // front path (pbg_fronts.h) of the distributed dynamics: state in LDS, front-parallel algebra
-  static constexpr bool LST = FP<R>::NF > 0;
+  static_assert(!R::harder || LST, "the cube robot runs the front path");
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
   static constexpr bool LIM_WS = gang_big<R>();  // limit rows in the device workspace
@@ -1223,42 +1228,91 @@ PBG_DEV void gang_load_factor(const GangCtx& X, float* L, float* Ld) {
   }
 }
 
-// The front path's integration: nu = L^-T u (replicated, the factor in registers from 16-byte
-// loads), clamped; the env's LDS state advanced by semi-implicit Euler (lane d < NJ its joint d,
-// the base and the cube by lane 0; the next sub-step reads them after its first gang sync)
+// The front path's integration: nu = L^-T u, front-parallel like gang_front_solve (the trunk's
+// back-substitution replicated, then lane q < NF of each group its front's, with the trunk terms
+// last: the same summation order as a dense back-substitution over the leaf-first order),
+// clamped; the env's LDS state advanced by semi-implicit Euler (the first group's front lanes
+// their fronts' joints, lane 0 the trunk joints, the base and the cube; the next sub-step reads
+// them after its first gang sync)
 template <class R, int T>
 PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
   using G = Gang<R, T>;
   using D = Dims<R>;
-  constexpr int NJ = R::NJ, N = R::NDOF;
+  using TT = TrunkTab<R>;
+  constexpr int NJ = R::NJ, N = R::NDOF, NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NT2 = TT::NT2;
   const float dt = X.P.dt;
   const float vmax = (float)PBG_MAX_COORD_VELOCITY;
-  float L[G::NNZ4], Ld[G::N4], nu[N];
-  gang_load_factor<R, T>(X, L, Ld);
+  // --- trunk ---------------------------------------------------------------------------------
+  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
+  float Lt[NT2], xt[NT];
 #pragma unroll
-  for (int i = N - 1; i >= 0; i--) {
-    float t = X.l[G::O_U + i];
-#pragma unroll
-    for (int kk = i + 1; kk < N; kk++)
-      if (D::coupled(kk, i)) t -= L[FP<R>::idx(kk, i)] * nu[kk];
-    nu[i] = t * Ld[i];
-  }
-#pragma unroll
-  for (int i = 0; i < N; i++) nu[i] = clampf(nu[i], -vmax, vmax);
-  // lane t: joints t, t + T, ... (each velocity picked from the replicated nu by selects)
-  static_for<0, (NJ + T - 1) / T>([&](auto r_c) {
-    constexpr int r = decltype(r_c)::value;
-    float qd = nu[D::gj(r * T)];
-    static_for<r * T + 1, (r * T + T < NJ ? r * T + T : NJ)>([&](auto d_c) {
-      constexpr int d = decltype(d_c)::value;
-      qd = X.t == d - r * T ? nu[D::gj(d)] : qd;
+  for (int i = 0; i < NT2; i++) Lt[i] = tb[i];
+  static_for<0, NT>([&](auto r_c) {
+    constexpr int t = NT - 1 - decltype(r_c)::value;
+    constexpr int g = FP<R>::v.tg[t];
+    float v = X.l[G::O_U + g];
+    static_for<t + 1, NT>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      if constexpr (TT::pos(k, t) >= 0) v -= Lt[TT::pos(k, t)] * xt[k];
     });
-    const int d = r * T + X.t;
-    if (d < NJ) {
-      X.l[G::O_QD + d] = qd;
-      X.l[G::O_Q + d] += dt * qd;
+    xt[t] = v * X.l[G::O_LD + g];
+  });
+  float nut[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) nut[t] = clampf(xt[t], -vmax, vmax);
+  // --- fronts --------------------------------------------------------------------------------
+  const int q = opaque_lane(X.t) % GRP;
+  const int cls = q < NF ? front_pick<R>(q, [](int f) { return FP<R>::v.cls[f]; }) : -1;
+  const int boff = front_pick<R>(q, [](int f) { return FP<R>::v.off[f]; });
+  const int g0 = front_pick<R>(q, [](int f) { return FP<R>::v.g0[f]; });
+  const bool wf = X.t < GRP && q < NF;  // the gang's front writers
+  static_for<0, FP<R>::v.ncls>([&](auto c_c) {
+    constexpr int C = decltype(c_c)::value;
+    using FC = FrontCls<R, C>;
+    constexpr int n = FC::n;
+    if (cls != C) return;
+    const lds_float* blk = X.l + G::O_L + boff;
+    float xf[n];
+    static_for<0, n>([&](auto r_c) {
+      constexpr int a = n - 1 - decltype(r_c)::value;
+      float v = X.l[G::O_U + g0 + a];
+      static_for<a + 1, n>([&](auto b_c) {
+        constexpr int b = decltype(b_c)::value;
+        if constexpr (FC::cpl(b, a)) v -= blk[FC::a_off(b, a)] * xf[b];
+      });
+      static_for<0, NT>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (FC::tc(t)) v -= blk[FC::c_off(a, t)] * xt[t];
+      });
+      xf[a] = v * X.l[G::O_LD + g0 + a];
+    });
+    if (wf) {
+      // joint dof of local a: NJ - 1 - (g0 + a) (leaf-first order)
+      lds_float* qd = X.l + G::O_QD + (NJ - 1 - g0);
+      lds_float* qq = X.l + G::O_Q + (NJ - 1 - g0);
+      static_for<0, n>([&](auto a_c) {
+        constexpr int a = decltype(a_c)::value;
+        const float v = clampf(xf[a], -vmax, vmax);
+        qd[-a] = v;
+        qq[-a] += dt * v;
+      });
     }
   });
+  float nu[N];  // the trunk part (compile-time indices; the fronts' entries are not used below)
+  static_for<0, NT>([&](auto t_c) {
+    constexpr int t = decltype(t_c)::value;
+    nu[FP<R>::v.tg[t]] = nut[t];
+  });
+  if (X.t == 0) {
+    static_for<0, NT>([&](auto t_c) {
+      constexpr int t = decltype(t_c)::value;
+      constexpr int d = D::dof_of(FP<R>::v.tg[t]);
+      if constexpr (d >= 0) {
+        X.l[G::O_QD + d] = nut[t];
+        X.l[G::O_Q + d] += dt * nut[t];
+      }
+    });
+  }
   if (X.t == 0) {
     if constexpr (R::floating) {
       float bq[4];
@@ -1630,13 +1684,14 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       gang_front_solve<R, T>(s, X);
     } else {
       // --- replicated: factorisation and the unconstrained velocity, staged for the PGS ----
-      float L[D::NNZ], Ld[N], rhs[N], nu[N], u[N];
+      // (the factor stays in Lr / Ldr for the rows pass: no reload from LDS)
+      float rhs[N], nu[N], u[N];
 #pragma unroll
-      for (int i = 0; i < D::NNZ; i++) L[i] = X.l[G::O_L + i];
+      for (int i = 0; i < D::NNZ; i++) Lr[i] = X.l[G::O_L + i];
 #pragma unroll
       for (int i = 0; i < N; i++) rhs[i] = X.l[G::O_RHS + i];
-      dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
-      stage_solution(L, Ld, u);
+      dyn_solve<R>(s, Lr, rhs, Ldr, nu, u, P);
+      stage_solution(Lr, Ldr, u);
     }
     PBG_GANG_SYNC
     STAMP(10)
@@ -1647,7 +1702,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #else
   const int njobs = NLIM + 3 * nc;
 #endif
-  if constexpr (DIST) gang_load_factor<R, T>(X, Lr, Ldr);
+  if constexpr (DIST && FP<R>::NF > 0) gang_load_factor<R, T>(X, Lr, Ldr);
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
     if (j >= njobs) continue;

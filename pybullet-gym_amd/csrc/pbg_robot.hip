@@ -93,11 +93,11 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
-    // every env region 16-byte aligned (b64 / b128 LDS accesses): round the region up, and give
-    // back a contact when the rounding crosses the budget
+    // every env region 16-byte (front path: b128 LDS loads) or 8-byte (b64 row loads) aligned:
+    // round the region up, and give back a contact when the rounding crosses the budget
     auto region = [&](int c) {
       const int w = G::FIXED + (c * G::PERC > G::MIN_CONTACT_WORDS ? c * G::PERC : G::MIN_CONTACT_WORDS);
-      return (w + 3) & ~3;
+      return (w + G::REGION_ALIGN - 1) & ~(G::REGION_ALIGN - 1);
     };
     while (cap > 0 && (long)region(cap) * EPB * (long)sizeof(float) > budget) cap--;
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its

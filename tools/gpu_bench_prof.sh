@@ -1,7 +1,7 @@
 #!/bin/bash
 # bench + rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE; WRITE_SIZE; SQ
-# instruction/cycle counters; VALU op mix) for the two metric workloads (Ant 16,384 envs and
-# Humanoid 4,096 envs).  usage: tools/gpu_bench_prof.sh TAG [bench args...]
+# instruction/cycle counters; VALU op mix) for the bench workloads (Ant 16,384 envs, Humanoid
+# 4,096, Hopper 4,096, HalfCheetah 8,192; PROF_ROBOTS="ant humanoid" narrows the list).  usage: tools/gpu_bench_prof.sh TAG [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
@@ -13,8 +13,13 @@ export TMPDIR=/tmp
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 # the bench command itself (same steps / warmup), without the CPU leg
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
-for W in ant humanoid; do
-  if [ $W = ant ]; then A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384"; else A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096"; fi
+for W in ${PROF_ROBOTS:-ant humanoid hopper halfcheetah}; do
+  case $W in
+    ant) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384";;
+    humanoid) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096";;
+    hopper) A="--env HopperPyBulletEnv-v0 --envs-per-gpu 4096";;
+    halfcheetah) A="--env HalfCheetahPyBulletEnv-v0 --envs-per-gpu 8192";;
+  esac
   B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline --second-env none $A"
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$W/pmc_fetch -o run -- $B > $OUT/$W.pmc_fetch.log 2>&1
   timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$W/pmc_write -o run -- $B > $OUT/$W.pmc_write.log 2>&1

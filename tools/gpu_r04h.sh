@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-4 dev pass: walker tests, A/B of the round-3 tree on the small robots, Humanoid-family stamps
+set -o pipefail
+TAG=${1:-r04h}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "gang or teacher_forced_parity or free_running" > $OUT/tests.txt 2>&1; rc=$?
+tail -3 $OUT/tests.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python tools/ab_lib.py ab/r03 pybullet-gym_amd/libpbg_amd.so Walker2DPyBulletEnv-v0:4096 HalfCheetahPyBulletEnv-v0:8192 HopperPyBulletEnv-v0:4096 HumanoidPyBulletEnv-v0:4096 > $OUT/ab_r03.txt 2>&1 || exit 1
+cat $OUT/ab_r03.txt
+timeout -k 10 400 python tools/stamps.py HumanoidFlagrunHarderPyBulletEnv-v0:4096 AtlasPyBulletEnv-v0:4096 AntPyBulletEnv-v0:16384 Walker2DPyBulletEnv-v0:4096 > $OUT/stamps.txt 2>&1; rc=$?
+cat $OUT/stamps.txt
+exit $rc

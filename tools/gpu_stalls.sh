@@ -6,8 +6,13 @@ TAG=${1:-stalls}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-for W in ant humanoid; do
-  if [ $W = ant ]; then A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384"; else A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096"; fi
+for W in ${PROF_ROBOTS:-ant humanoid}; do
+  case $W in
+    ant) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384";;
+    humanoid) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096";;
+    hopper) A="--env HopperPyBulletEnv-v0 --envs-per-gpu 4096";;
+    halfcheetah) A="--env HalfCheetahPyBulletEnv-v0 --envs-per-gpu 8192";;
+  esac
   B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline --second-env none $A"
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_WAIT_ANY --output-format csv -d $OUT/$W/pmc_wait -o run -- $B > $OUT/$W.pmc_wait.log 2>&1 || exit 1
   timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC --output-format csv -d $OUT/$W/pmc_lds -o run -- $B > $OUT/$W.pmc_lds.log 2>&1 || exit 1

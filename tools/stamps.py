@@ -30,11 +30,11 @@ for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
     rid = _native.ROBOT_IDS[env_id]
-    L.pbg_debug_stamps(rid, buf)
+    assert L.pbg_debug_stamps(rid, buf) == 0, env_id
     steps = 20
     for i in range(steps): env.step(acts[10 + i])
     torch.cuda.synchronize()
-    L.pbg_debug_stamps(rid, buf)
+    assert L.pbg_debug_stamps(rid, buf) == 0, env_id
     lpe = max(1, env.info.lanes_per_env)
     if lpe == 1:  # lane kernel: workgroups of 16/32/64 lanes, one wave each (plan_* in pbg_robot.hip)
         per_cu, b = -(-n // 256), 16
