@@ -395,7 +395,10 @@ struct Gang {
   static_assert(!R::harder || LST, "the cube robot runs the front path");
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
-  static constexpr bool LIM_WS = gang_big<R>();  // limit rows in the device workspace
+  // limit rows in the device workspace (Atlas; HumanoidFlagrunHarder: its cube brings ~10 contacts
+  // per env, and the 629 words of LDS limit rows -- dead once the PGS holds them in registers --
+  // are 3 more LDS-resident contacts)
+  static constexpr bool LIM_WS = gang_big<R>() || R::harder;
   static constexpr int LRSZ = (!LIM_WS && NLIM * LRW > NB * CW) ? NLIM * LRW : NB * CW;
   static constexpr int FIXED = O_LR + LRSZ + (Y64 ? ((O_LR + LRSZ + RW0) & 1) : 0);  // Y64: rows start even
   static constexpr int PERC = RW0 + 3 * CRW + (Y64 ? ((RW0 + 3 * CRW) & 1) : 0);
@@ -444,6 +447,12 @@ struct GangTabs {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
   }
 
+// word offset of contact c's record (24-bit multiply: the 64-bit v_mad_u64_u32 the compiler chose
+// for the row addresses is a multi-pass instruction, two per normal row of the sweep)
+template <class R, int T>
+PBG_DEV int coff(int c) {
+  return (int)__umul24((unsigned)c, (unsigned)Gang<R, T>::PERC);
+}
 // f(p) with p the first word of contact c: its LDS record if resident, else its device
 // workspace record -- one branch for a whole record's loads or stores (a per-word
 // accessor left one divergent branch per word in the code: 442 branches in the detection
@@ -451,8 +460,8 @@ struct GangTabs {
 template <class R, int T, class F>
 PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
   using G = Gang<R, T>;
-  if (c < X.cap) f(X.l + G::FIXED + c * G::PERC);
-  else f(X.g + (size_t)c * G::PERC);
+  if (c < X.cap) f(X.l + G::FIXED + coff<R, T>(c));
+  else f(X.g + coff<R, T>(c));
 }
 
 // f(p) with p the first word of joint-limit row li (LDS, or the workspace for LIM_WS models)
@@ -478,7 +487,7 @@ PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
   typedef __attribute__((address_space(3))) const v2f lds_v2f;
   const int w0 = G::RW0 + dir * G::CRW;
   if (LDS || c < X.cap) {
-    const lds_float* p = X.l + G::FIXED + c * G::PERC + w0;
+    const lds_float* p = X.l + G::FIXED + coff<R, T>(c) + w0;
     if constexpr (G::Y64) {
       static_assert((G::FIXED + G::RW0) % 2 == 0 && G::PERC % 2 == 0 && G::CRW % 2 == 0, "b64 rows");
       const v2f a = *(lds_v2f*)(p + 2 * X.t);
@@ -489,7 +498,7 @@ PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
     }
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   } else {
-    const float* p = X.g + (size_t)c * G::PERC + w0;
+    const float* p = X.g + coff<R, T>(c) + w0;
 #pragma unroll
     for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t * G::NSL + m];
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
@@ -503,10 +512,10 @@ PBG_DEV float gang_fric_limit(const GangCtx& X, int c) {
   typedef __attribute__((address_space(3))) const v2f lds_v2f;
   constexpr int w = G::RW0 + G::YS + 2;
   if (LDS || c < X.cap) {
-    const lds_float* p = X.l + G::FIXED + c * G::PERC;
+    const lds_float* p = X.l + G::FIXED + coff<R, T>(c);
     return p[G::DW] * p[w];
   }
-  const float* p = X.g + (size_t)c * G::PERC;
+  const float* p = X.g + coff<R, T>(c);
   return p[G::DW] * p[w];
 }
 template <class R, int T, bool LDS>
@@ -514,8 +523,8 @@ PBG_DEV void gang_set_lam(const GangCtx& X, int c, int dir, float v) {
   using G = Gang<R, T>;
   const int w = G::RW0 + dir * G::CRW + G::YS + 2;
   if (X.t == 0) {
-    if (LDS || c < X.cap) X.l[G::FIXED + c * G::PERC + w] = v;
-    else X.g[(size_t)c * G::PERC + w] = v;
+    if (LDS || c < X.cap) X.l[G::FIXED + coff<R, T>(c) + w] = v;
+    else X.g[coff<R, T>(c) + w] = v;
   }
 }
 // PGS update of a loaded row with u sliced over the gang; the new impulse has the same bits
@@ -542,15 +551,17 @@ PBG_DEV float gang_update(const GRow<R, T>& r, float* us, float lo, float hi) {
 // masked update, a finished gang's look-ahead registers stayed pending on the skipped path
 // and the compiler's wait at the loop head drained every LDS load (lgkmcnt(0)), so no row's
 // loads overlapped the previous update.
-template <class R, int T, bool LDS>
+// NW: 32-bit words of the positive-impulse mask (the caller takes NW = 1 when no env of the wave
+// has more than 32 contacts, the model's full width otherwise)
+template <class R, int T, bool LDS, int NW>
 PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
   using G = Gang<R, T>;
   using Row = GRow<R, T>;
   if (nc <= 0) return;
-  // positive normal impulses, one bit per contact in NW 32-bit words (Hopper, Walker2D,
-  // HalfCheetah: one word; Humanoid: three), set and walked branch-free (selects over the
-  // words) -- the 64-bit mask with a branch per word cost 6-8 % of the step.
-  constexpr int NW = (G::MAXC + 31) / 32;
+  // positive normal impulses, one bit per contact in NW 32-bit words, set and walked
+  // branch-free (selects over the words) -- the 64-bit mask with a branch per word cost 6-8 %
+  // of the step; the three-word selects of the Humanoid's 95 candidates were 12 of a normal
+  // row's ~50 instructions, hence the one-word instantiation for the common case
   if constexpr (NW > 4) {
     // more than 128 contact candidates (Atlas): the plain order -- every normal, then the two
     // friction rows of each contact whose normal impulse came out positive, a load-then-test
@@ -1825,6 +1836,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       llo[li] = 0.f; lhi[li] = 0.f;
     }
     const bool all_lds = !wave_any(nc > X.cap);  // every contact row of the wave in LDS
+    constexpr int NWF = (G::MAXC + 31) / 32;
+    const bool few = NWF == 1 || !wave_any(nc > 32);  // a one-word positive-impulse mask suffices
     for (int it = 0; it < P.iterations; it++) {
 #pragma unroll
       for (int li = 0; li < NLIM; li++) {
@@ -1845,8 +1858,13 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #pragma unroll
         for (int m = 0; m < NSL; m++) us[m] += ly[li][m] * dl;
       }
-      if (all_lds) gang_contact_sweep<R, T, true>(X, nc, us);
-      else gang_contact_sweep<R, T, false>(X, nc, us);
+      if (few) {
+        if (all_lds) gang_contact_sweep<R, T, true, 1>(X, nc, us);
+        else gang_contact_sweep<R, T, false, 1>(X, nc, us);
+      } else {
+        if (all_lds) gang_contact_sweep<R, T, true, NWF>(X, nc, us);
+        else gang_contact_sweep<R, T, false, NWF>(X, nc, us);
+      }
     }
   }
   // --- replicated: gather u, back-substitute, integrate ----------------------------------
