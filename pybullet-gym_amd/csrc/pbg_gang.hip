@@ -391,7 +391,11 @@ struct Gang {
   // through the sub-steps, q / qd at O_Q / O_QD)
   static constexpr int O_BS = O_JO + 3 * NJ1;
   static constexpr int O_CS = O_BS + (LST ? 13 : 0);  // HumanoidFlagrunHarder: the cube's state words (same layout)
-  static constexpr int O_FR = O_CS + (R::harder ? 13 : 0), O_LP = O_FR + FW * NB, O_LR = O_LP + 2 * NLIM;
+  // front path: the body frames (FW = 12) and the composites / limit rows (CW = 16) on 16-byte
+  // boundaries, so their records load as b128 with immediate offsets (ds_read2_b32 pairs past
+  // the first KiB of the region needed a v_add_u32 per address)
+  static constexpr int al4(int x) { return LST ? (x + 3) & ~3 : x; }
+  static constexpr int O_FR = al4(O_CS + (R::harder ? 13 : 0)), O_LP = O_FR + FW * NB, O_LR = al4(O_LP + 2 * NLIM);
   static_assert(!R::harder || LST, "the cube robot runs the front path");
   // the composites (dead once M is built) share their words with the limit rows
   static constexpr int O_CP = O_LR;
@@ -421,6 +425,25 @@ struct GangCtx {
   int le;        // gang in the wave
   SimP P;        // scene parameters (kernel arguments)
 };
+// n words (n % 4 == 0) from / to a 16-byte aligned LDS address as b128 accesses (front path:
+// the composite records; the compiler split them into ds_read2_b32 pairs with an address add each)
+template <int n>
+PBG_DEV void lds_ld4(const lds_float* p, float* v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const v4f lds_v4f;
+#pragma unroll
+  for (int k = 0; k < n / 4; k++) {
+    const v4f a = ((lds_v4f*)p)[k];
+    v[4 * k] = a.x; v[4 * k + 1] = a.y; v[4 * k + 2] = a.z; v[4 * k + 3] = a.w;
+  }
+}
+template <int n>
+PBG_DEV void lds_st4(lds_float* p, const float* v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4f lds_v4f;
+#pragma unroll
+  for (int k = 0; k < n / 4; k++) ((lds_v4f*)p)[k] = v4f{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+}
 // word w (0..26) of body b's record: frame part (w < 12) or kinematic part
 template <class R, int T>
 PBG_DEV lds_float* body_word(const lds_float* l, int b, int w) {
@@ -849,8 +872,14 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
                               pr.x, pr.y, pr.z, f.x, f.y, f.z, Nn.x, Nn.y, Nn.z, m};
     lds_float* C = X.l + G::O_CP + G::CW * b;
     const bool massive = m > 0.f;
+    float cv[G::CW];
 #pragma unroll
-    for (int i = 0; i < G::CW; i++) C[i] = massive ? cmp[i] : 0.f;
+    for (int i = 0; i < G::CW; i++) cv[i] = massive ? cmp[i] : 0.f;
+    if constexpr (G::LST) lds_st4<G::CW>(C, cv);
+    else {
+#pragma unroll
+      for (int i = 0; i < G::CW; i++) C[i] = cv[i];
+    }
   }
 #pragma unroll
   for (int r_ = 0; r_ < (N + T - 1) / T; r_++) {
@@ -889,19 +918,31 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
         const int b = ksel<S, KN, int>(t, [&](auto bc) { return decltype(bc)::value; });
         lds_float* C = X.l + G::O_CP + G::CW * b;
         float acc[G::CW];
+        if constexpr (G::LST) lds_ld4<G::CW>(C, acc);
+        else {
 #pragma unroll
-        for (int i = 0; i < G::CW; i++) acc[i] = C[i];
+          for (int i = 0; i < G::CW; i++) acc[i] = C[i];
+        }
         static_for<0, MC>([&](auto j_c) {
           constexpr int j = decltype(j_c)::value;
           const int c = ksel<S, KN, int>(t, [&](auto bc) { return j < GC::v.nch[decltype(bc)::value] ? GC::v.ch[decltype(bc)::value][j] : -1; });
           if (c >= 0) {
             const lds_float* K = X.l + G::O_CP + G::CW * c;
+            float kv[G::CW];
+            if constexpr (G::LST) lds_ld4<G::CW>(K, kv);
+            else {
 #pragma unroll
-            for (int i = 0; i < G::CW; i++) acc[i] += K[i];
+              for (int i = 0; i < G::CW; i++) kv[i] = K[i];
+            }
+#pragma unroll
+            for (int i = 0; i < G::CW; i++) acc[i] += kv[i];
           }
         });
+        if constexpr (G::LST) lds_st4<G::CW>(C, acc);
+        else {
 #pragma unroll
-        for (int i = 0; i < G::CW; i++) C[i] = acc[i];
+          for (int i = 0; i < G::CW; i++) C[i] = acc[i];
+        }
       }
     });
     PBG_GANG_SYNC
@@ -917,7 +958,13 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int k = r_ * T + X.t;
     if (k >= N) continue;
     const int bk = TD.g_body[k], d = TD.g_dof[k];
-    const lds_float* C = X.l + G::O_CP + G::CW * bk;
+    const lds_float* Cp = X.l + G::O_CP + G::CW * bk;
+    float C[G::CW];
+    if constexpr (G::LST) lds_ld4<G::CW>(Cp, C);
+    else {
+#pragma unroll
+      for (int i = 0; i < G::CW; i++) C[i] = Cp[i];
+    }
     s6 J;
 #pragma unroll
     for (int i = 0; i < 6; i++) J.a[i] = C[i];
@@ -1713,7 +1760,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #else
   const int njobs = NLIM + 3 * nc;
 #endif
-  if constexpr (DIST && FP<R>::NF > 0) gang_load_factor<R, T>(X, Lr, Ldr);
+  // the front path holds its staged factor in registers for the rows pass unless it is too big to
+  // (Atlas: the register copy spilled 1.2 KB per lane; its rows read the LDS words instead)
+  constexpr bool LREG = !DIST || FP<R>::NF == 0 || G::NNZ4 + G::N4 <= 240;
+  if constexpr (DIST && FP<R>::NF > 0 && LREG) gang_load_factor<R, T>(X, Lr, Ldr);
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
     if (j >= njobs) continue;
@@ -1783,8 +1833,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       float tt = J[i];
 #pragma unroll
       for (int kk = 0; kk < i; kk++)
-        if (D::coupled(i, kk)) tt -= Lr[DIST ? FP<R>::idx(i, kk) : D::lidx(i, kk)] * y[kk];
-      y[i] = tt * Ldr[i];
+        if (D::coupled(i, kk)) tt -= (LREG ? Lr[DIST ? FP<R>::idx(i, kk) : D::lidx(i, kk)] : X.l[G::O_L + FP<R>::idx(i, kk)]) * y[kk];
+      y[i] = tt * (LREG ? Ldr[i] : X.l[G::O_LD + i]);
       D2 += y[i] * y[i];
     }
     if constexpr (R::harder) D2 += dot3(ycl, ycl) + dot3(cubes, cubes);
@@ -1926,7 +1976,7 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
 template <class R, int T, bool DIST>
 __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
-  extern __shared__ float lds_dyn[];
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   using G = Gang<R, T>;
   using TT = GangTabs<R>;
   constexpr int BLK = gang_block<R>();
@@ -1947,7 +1997,10 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   const int e = blockIdx.x * EPB + X.le;
   if (e >= B.n) return;  // whole gangs only (no workgroup barrier below)
   X.le &= 64 / T - 1;     // gang within the wave (ballot masks)
-  X.l = lds + TT::WORDS + (threadIdx.x / T) * env_words;
+  // (env_words is a multiple of REGION_ALIGN: saying so lets the compiler prove the 8 / 16-byte
+  // alignment of the region's fixed words and use b64 / b128 LDS accesses with offsets instead
+  // of ds_read2_b32 pairs, whose 8-bit offsets needed a v_add_u32 for every address)
+  X.l = lds + TT::WORDS + (threadIdx.x / T) * (env_words & ~(G::REGION_ALIGN - 1));
   X.g = scratch + (size_t)e * G::GWORDS;
   X.cap = cap;
   X.P = B.sp;
