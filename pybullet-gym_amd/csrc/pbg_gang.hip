@@ -375,26 +375,40 @@ struct Gang {
   static constexpr int NJ1 = R::NJ > 0 ? R::NJ : 1;
   static constexpr int BW = 27;                // body record: Rm 9 | x 3 | c 3 | w 3 | v 3 | al 3 | ac 3
   static constexpr int FW = 12;                // its frame part (Rm | x) lives at O_FR, stride FW; the
-  static constexpr int KW = BW - FW;           // kinematic part (c | w | v | al | ac) at O_KV, stride KW
   static constexpr int CW = 16;                // composite: J 6 | m r 3 | F 3 | N 3 | m
   // front path (pbg_fronts.h) of the distributed dynamics: state in LDS, front-parallel algebra
   static constexpr bool LST = FP<R>::NF > 0;
-  // front path: the factor, 1 / diag and u start on 16-byte boundaries (b128 loads; the env
-  // region is 16-byte aligned).  The small trees keep the round-3 layout (8-byte regions, no
-  // base-state words): the extra words shifted their regions' LDS banks and cost Walker2D 2 %
-  // with identical code (round-4 A/B)
-  static constexpr int REGION_ALIGN = LST ? 4 : 2;
+  // AL: the aligned layout -- 16-byte env regions whose records (frames, kinematic parts,
+  // composites) start on 16-byte boundaries and whose 3-vectors pair up on 8-byte ones, so the
+  // compiler, which can prove it from the kernel's address arithmetic, emits b64 / b128 accesses
+  // with immediate offsets (round-4 A/B against 8-byte regions: Walker2D -7.6 %, HalfCheetah
+  // -6.6 %, Hopper -2.5 %; Humanoid -8 % over the three steps).  The factor, 1 / diag and u start
+  // on 16-byte boundaries on the front path (b128 factor loads).
+  static constexpr bool AL = true;
+  static constexpr int REGION_ALIGN = AL ? 4 : 2;
+  // kinematic part (c | w | v | al | ac) at O_KV, stride KW (aligned layout: a 16-word record on a
+  // 16-byte boundary, read and written as four b128; not for Atlas, whose 30 bodies' kinematic
+  // area is the env region's floor and must stay within the LDS budget)
+  static constexpr bool KAL = AL && !gang_big<R>();
+  static constexpr int KW = KAL ? 16 : BW - FW;
   static constexpr int NNZ4 = LST ? (NNZ + 3) & ~3 : NNZ, N4 = LST ? (N + 3) & ~3 : N;
-  static constexpr int O_L = 0, O_LD = O_L + NNZ4, O_U = O_LD + N4, O_RHS = O_U + YS, O_SW = O_RHS + N, O_SV = O_SW + 3 * N;
-  static constexpr int O_Q = O_SV + 3 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1, O_JA = O_TAU + NJ1, O_JO = O_JA + 3 * NJ1;
+  // motion vectors s_w | s_v of generalized index i: the front path interleaves them per index
+  // at an even word, stride SS = 6 (three b64 loads per index); the small trees keep two
+  // stride-3 arrays (their round-3 layout)
+  static constexpr int SS = AL ? 6 : 3;
+  static constexpr int O_L = 0, O_LD = O_L + NNZ4, O_U = O_LD + N4, O_RHS = O_U + YS;
+  static constexpr int O_SW = AL ? (O_RHS + N + 1) & ~1 : O_RHS + N, O_SV = AL ? O_SW + 3 : O_SW + 3 * N;
+  static constexpr int O_Q = O_SW + 6 * N, O_QD = O_Q + NJ1, O_TAU = O_QD + NJ1;
+  // joint axis | origin of dof d, interleaved like s_w | s_v on the front path
+  static constexpr int O_JA = AL ? (O_TAU + NJ1 + 1) & ~1 : O_TAU + NJ1, O_JO = AL ? O_JA + 3 : O_JA + 3 * NJ1;
   // the base's state words [p 3 | quat 4 | v 3 | w 3] (front path: the env's state lives in LDS
   // through the sub-steps, q / qd at O_Q / O_QD)
-  static constexpr int O_BS = O_JO + 3 * NJ1;
+  static constexpr int O_BS = O_JA + 6 * NJ1;
   static constexpr int O_CS = O_BS + (LST ? 13 : 0);  // HumanoidFlagrunHarder: the cube's state words (same layout)
   // front path: the body frames (FW = 12) and the composites / limit rows (CW = 16) on 16-byte
   // boundaries, so their records load as b128 with immediate offsets (ds_read2_b32 pairs past
   // the first KiB of the region needed a v_add_u32 per address)
-  static constexpr int al4(int x) { return LST ? (x + 3) & ~3 : x; }
+  static constexpr int al4(int x) { return AL ? (x + 3) & ~3 : x; }
   static constexpr int O_FR = al4(O_CS + (R::harder ? 13 : 0)), O_LP = O_FR + FW * NB, O_LR = al4(O_LP + 2 * NLIM);
   static_assert(!R::harder || LST, "the cube robot runs the front path");
   // the composites (dead once M is built) share their words with the limit rows
@@ -408,8 +422,8 @@ struct Gang {
   static constexpr int PERC = RW0 + 3 * CRW + (Y64 ? ((RW0 + 3 * CRW) & 1) : 0);
   // the kinematic parts are dead once M and the bias are built, before any contact is
   // written: they share the start of the contact area (the env region holds >= KW*NB words)
-  static constexpr int O_KV = FIXED;
-  static constexpr int MIN_CONTACT_WORDS = KW * NB;
+  static constexpr int O_KV = KAL ? al4(FIXED) : FIXED;
+  static constexpr int MIN_CONTACT_WORDS = (O_KV - FIXED) + KW * NB;
   static constexpr int GW_LR = (MAXC > 0 ? MAXC : 1) * PERC;    // LIM_WS: limit rows after the contacts
   static constexpr int GWORDS = GW_LR + (LIM_WS ? NLIM * LRW : 0);  // device workspace per env
   static constexpr int ROUNDS_S = (R::NS + T - 1) / T;
@@ -719,14 +733,24 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
   const lds_float* P = body_word<R, T>(X.l, p, 0);
   const lds_float* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
   m3 Rp, Ro;
+  float pr[G::FW + G::KW];  // the parent's record: frame | kinematic part
+  if constexpr (G::KAL) {
+    lds_ld4<G::FW>(P, pr);
+    lds_ld4<G::KW>(PK + G::FW, pr + G::FW);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 9; i++) Rp.m[i] = P[i];
+    for (int i = 0; i < G::FW; i++) pr[i] = P[i];
+#pragma unroll
+    for (int i = G::FW; i < G::BW; i++) pr[i] = PK[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) Rp.m[i] = pr[i];
   static_for<0, 9>([&](auto i_c) {
     constexpr int i = decltype(i_c)::value;
     Ro.m[i] = PBG_LV(DTh::v.ro[b][i]);
   });
-  const f3 xp = mk3(P[9], P[10], P[11]), cp = mk3(PK[12], PK[13], PK[14]), wp = mk3(PK[15], PK[16], PK[17]);
-  const f3 vp = mk3(PK[18], PK[19], PK[20]), alp = mk3(PK[21], PK[22], PK[23]), acp = mk3(PK[24], PK[25], PK[26]);
+  const f3 xp = mk3(pr[9], pr[10], pr[11]), cp = mk3(pr[12], pr[13], pr[14]), wp = mk3(pr[15], pr[16], pr[17]);
+  const f3 vp = mk3(pr[18], pr[19], pr[20]), alp = mk3(pr[21], pr[22], pr[23]), acp = mk3(pr[24], pr[25], pr[26]);
   const m3 R0 = mul_kb(Rp, Ro);
   const f3 x0 = xp + mulc(Rp, PBG_LV(DTh::v.opos[b][0]), PBG_LV(DTh::v.opos[b][1]), PBG_LV(DTh::v.opos[b][2]));
   const f3 axl = mk3(PBG_LV(DTh::v.axis[b][0]), PBG_LV(DTh::v.axis[b][1]), PBG_LV(DTh::v.axis[b][2]));
@@ -762,8 +786,8 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
       const f3 rc = c - o;
       v = vo + cross3(w, rc);
       ac = ao + cross3(al, rc) + cross3(w, cross3(w, rc));
-      X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
-      X.l[G::O_JO + 3 * d] = o.x; X.l[G::O_JO + 3 * d + 1] = o.y; X.l[G::O_JO + 3 * d + 2] = o.z;
+      X.l[G::O_JA + G::SS * d] = a.x; X.l[G::O_JA + G::SS * d + 1] = a.y; X.l[G::O_JA + G::SS * d + 2] = a.z;
+      X.l[G::O_JO + G::SS * d] = o.x; X.l[G::O_JO + G::SS * d + 1] = o.y; X.l[G::O_JO + G::SS * d + 2] = o.z;
     } else if constexpr (jt == 1) {
       const f3 a = mulc(R0, axl);
       x = x0 + q * a;
@@ -773,8 +797,8 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
       al = alp;
       v = vp + cross3(wp, r) + qd * a;
       ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * qd) * cross3(wp, a);
-      X.l[G::O_JA + 3 * d] = a.x; X.l[G::O_JA + 3 * d + 1] = a.y; X.l[G::O_JA + 3 * d + 2] = a.z;
-      X.l[G::O_JO + 3 * d] = x0.x; X.l[G::O_JO + 3 * d + 1] = x0.y; X.l[G::O_JO + 3 * d + 2] = x0.z;
+      X.l[G::O_JA + G::SS * d] = a.x; X.l[G::O_JA + G::SS * d + 1] = a.y; X.l[G::O_JA + G::SS * d + 2] = a.z;
+      X.l[G::O_JO + G::SS * d] = x0.x; X.l[G::O_JO + G::SS * d + 1] = x0.y; X.l[G::O_JO + G::SS * d + 2] = x0.z;
     } else {
       c = x + mulc(Rm, com);
       const f3 r = c - cp;
@@ -783,10 +807,15 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
       v = vp + cross3(wp, r);
       ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
     }
-    const float rec[G::BW] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
-                              x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z};
+    const float rec[G::BW + 1] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
+                                  x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z, 0.f};
+    if constexpr (G::KAL) {
+      lds_st4<G::FW>(body_word<R, T>(X.l, body, 0), rec);
+      lds_st4<G::KW>(body_word<R, T>(X.l, body, G::FW), rec + G::FW);
+    } else {
 #pragma unroll
-    for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, body, i) = rec[i];
+      for (int i = 0; i < G::BW; i++) *body_word<R, T>(X.l, body, i) = rec[i];
+    }
   };
   if constexpr (JT >= 0) {
     kin(std::integral_constant<int, JT>{});
@@ -875,7 +904,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     float cv[G::CW];
 #pragma unroll
     for (int i = 0; i < G::CW; i++) cv[i] = massive ? cmp[i] : 0.f;
-    if constexpr (G::LST) lds_st4<G::CW>(C, cv);
+    if constexpr (G::AL) lds_st4<G::CW>(C, cv);
     else {
 #pragma unroll
       for (int i = 0; i < G::CW; i++) C[i] = cv[i];
@@ -888,8 +917,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int d = TD.g_dof[i];
     f3 sw, sv;
     if (d >= 0) {
-      const f3 a = mk3(X.l[G::O_JA + 3 * d], X.l[G::O_JA + 3 * d + 1], X.l[G::O_JA + 3 * d + 2]);
-      const f3 o = mk3(X.l[G::O_JO + 3 * d], X.l[G::O_JO + 3 * d + 1], X.l[G::O_JO + 3 * d + 2]);
+      const f3 a = mk3(X.l[G::O_JA + G::SS * d], X.l[G::O_JA + G::SS * d + 1], X.l[G::O_JA + G::SS * d + 2]);
+      const f3 o = mk3(X.l[G::O_JO + G::SS * d], X.l[G::O_JO + G::SS * d + 1], X.l[G::O_JO + G::SS * d + 2]);
       const bool rev = TD.jt[TD.g_body[i]] == 0;
       sw = rev ? a : mk3(0, 0, 0);
       sv = rev ? cross3(o - O, a) : a;
@@ -899,8 +928,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
       sw = kk < 3 ? mk3(0, 0, 0) : e;
       sv = kk < 3 ? e : mk3(0, 0, 0);
     }
-    X.l[G::O_SW + 3 * i] = sw.x; X.l[G::O_SW + 3 * i + 1] = sw.y; X.l[G::O_SW + 3 * i + 2] = sw.z;
-    X.l[G::O_SV + 3 * i] = sv.x; X.l[G::O_SV + 3 * i + 1] = sv.y; X.l[G::O_SV + 3 * i + 2] = sv.z;
+    X.l[G::O_SW + G::SS * i] = sw.x; X.l[G::O_SW + G::SS * i + 1] = sw.y; X.l[G::O_SW + G::SS * i + 2] = sw.z;
+    X.l[G::O_SV + G::SS * i] = sv.x; X.l[G::O_SV + G::SS * i + 1] = sv.y; X.l[G::O_SV + G::SS * i + 2] = sv.z;
   }
   PBG_GANG_SYNC
   STAMP(1)
@@ -918,7 +947,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
         const int b = ksel<S, KN, int>(t, [&](auto bc) { return decltype(bc)::value; });
         lds_float* C = X.l + G::O_CP + G::CW * b;
         float acc[G::CW];
-        if constexpr (G::LST) lds_ld4<G::CW>(C, acc);
+        if constexpr (G::AL) lds_ld4<G::CW>(C, acc);
         else {
 #pragma unroll
           for (int i = 0; i < G::CW; i++) acc[i] = C[i];
@@ -929,7 +958,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
           if (c >= 0) {
             const lds_float* K = X.l + G::O_CP + G::CW * c;
             float kv[G::CW];
-            if constexpr (G::LST) lds_ld4<G::CW>(K, kv);
+            if constexpr (G::AL) lds_ld4<G::CW>(K, kv);
             else {
 #pragma unroll
               for (int i = 0; i < G::CW; i++) kv[i] = K[i];
@@ -938,7 +967,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
             for (int i = 0; i < G::CW; i++) acc[i] += kv[i];
           }
         });
-        if constexpr (G::LST) lds_st4<G::CW>(C, acc);
+        if constexpr (G::AL) lds_st4<G::CW>(C, acc);
         else {
 #pragma unroll
           for (int i = 0; i < G::CW; i++) C[i] = acc[i];
@@ -952,7 +981,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
   // linear part) into the dead kinematic area past the reference body's record (gang_O
   // still reads that), and the bias C_k = s_k . (N, F) of the same composite
   constexpr int O_FK = G::O_KV + G::KW * (Dims<R>::REF_BODY + 1);
-  static_assert(G::KW * (Dims<R>::REF_BODY + 1) + 6 * N <= G::MIN_CONTACT_WORDS, "f_k past the kinematic area");
+  static_assert((G::O_KV - G::FIXED) + G::KW * (Dims<R>::REF_BODY + 1) + 6 * N <= G::MIN_CONTACT_WORDS, "f_k past the kinematic area");
 #pragma unroll
   for (int r_ = 0; r_ < (N + T - 1) / T; r_++) {
     const int k = r_ * T + X.t;
@@ -960,7 +989,7 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int bk = TD.g_body[k], d = TD.g_dof[k];
     const lds_float* Cp = X.l + G::O_CP + G::CW * bk;
     float C[G::CW];
-    if constexpr (G::LST) lds_ld4<G::CW>(Cp, C);
+    if constexpr (G::AL) lds_ld4<G::CW>(Cp, C);
     else {
 #pragma unroll
       for (int i = 0; i < G::CW; i++) C[i] = Cp[i];
@@ -970,8 +999,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     for (int i = 0; i < 6; i++) J.a[i] = C[i];
     const f3 p1 = mk3(C[6], C[7], C[8]);
     const float cm = C[15];
-    const f3 swk = mk3(X.l[G::O_SW + 3 * k], X.l[G::O_SW + 3 * k + 1], X.l[G::O_SW + 3 * k + 2]);
-    const f3 svk = mk3(X.l[G::O_SV + 3 * k], X.l[G::O_SV + 3 * k + 1], X.l[G::O_SV + 3 * k + 2]);
+    const f3 swk = mk3(X.l[G::O_SW + G::SS * k], X.l[G::O_SW + G::SS * k + 1], X.l[G::O_SW + G::SS * k + 2]);
+    const f3 svk = mk3(X.l[G::O_SV + G::SS * k], X.l[G::O_SV + G::SS * k + 1], X.l[G::O_SV + G::SS * k + 2]);
     const f3 Jw_ = mul(J, swk) + cross3(p1, svk);
     const f3 Fv = cm * svk - cross3(p1, swk);
     lds_float* f = X.l + O_FK + 6 * k;
@@ -993,8 +1022,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int gi = TD.me_i[j], gk = TD.me_k[j];
     const lds_float* f = X.l + O_FK + 6 * gk;
     const f3 Jw_ = mk3(f[0], f[1], f[2]), Fv = mk3(f[3], f[4], f[5]);
-    const f3 swi = mk3(X.l[G::O_SW + 3 * gi], X.l[G::O_SW + 3 * gi + 1], X.l[G::O_SW + 3 * gi + 2]);
-    const f3 svi = mk3(X.l[G::O_SV + 3 * gi], X.l[G::O_SV + 3 * gi + 1], X.l[G::O_SV + 3 * gi + 2]);
+    const f3 swi = mk3(X.l[G::O_SW + G::SS * gi], X.l[G::O_SW + G::SS * gi + 1], X.l[G::O_SW + G::SS * gi + 2]);
+    const f3 svi = mk3(X.l[G::O_SV + G::SS * gi], X.l[G::O_SV + G::SS * gi + 1], X.l[G::O_SV + G::SS * gi + 2]);
     X.l[G::O_L + j] = (dot3(swi, Jw_) + dot3(svi, Fv)) + TD.me_arm[j];
   }
   PBG_GANG_SYNC
@@ -1495,8 +1524,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     if (w0) {
 #pragma unroll
       for (int i = 0; i < N; i++) {
-        X.l[G::O_SW + 3 * i] = sw[i].x; X.l[G::O_SW + 3 * i + 1] = sw[i].y; X.l[G::O_SW + 3 * i + 2] = sw[i].z;
-        X.l[G::O_SV + 3 * i] = sv[i].x; X.l[G::O_SV + 3 * i + 1] = sv[i].y; X.l[G::O_SV + 3 * i + 2] = sv[i].z;
+        X.l[G::O_SW + G::SS * i] = sw[i].x; X.l[G::O_SW + G::SS * i + 1] = sw[i].y; X.l[G::O_SW + G::SS * i + 2] = sw[i].z;
+        X.l[G::O_SV + G::SS * i] = sv[i].x; X.l[G::O_SV + G::SS * i + 1] = sv[i].y; X.l[G::O_SV + G::SS * i + 2] = sv[i].z;
       }
 #pragma unroll
       for (int b = 0; b < D::NB; b++) {
@@ -1816,8 +1845,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       for (int i = 0; i < N; i++) {
         const int di = D::dof_of(i);
         const bool inA = di < 0 ? fA != 0.f : ((mA >> di) & 1u) != 0u, inB = di < 0 ? fB != 0.f : ((mB >> di) & 1u) != 0u;
-        const f3 sw = mk3(X.l[G::O_SW + 3 * i], X.l[G::O_SW + 3 * i + 1], X.l[G::O_SW + 3 * i + 2]);
-        const f3 sv = mk3(X.l[G::O_SV + 3 * i], X.l[G::O_SV + 3 * i + 1], X.l[G::O_SV + 3 * i + 2]);
+        const f3 sw = mk3(X.l[G::O_SW + G::SS * i], X.l[G::O_SW + G::SS * i + 1], X.l[G::O_SW + G::SS * i + 2]);
+        const f3 sv = mk3(X.l[G::O_SV + G::SS * i], X.l[G::O_SV + G::SS * i + 1], X.l[G::O_SV + G::SS * i + 2]);
         float tj = 0.f;
         if (inA) tj += dot3(nd, sv) + dot3(mmA, sw);
         if (inB) tj -= dot3(nd, sv) + dot3(mmB, sw);

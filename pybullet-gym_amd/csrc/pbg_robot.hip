@@ -84,6 +84,9 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
   if constexpr ((RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>())) {
     using G = Gang<RR, T>;
     constexpr int EPB = gang_block<RR>() / T;  // envs per workgroup
+    // the layout's floor (fixed words + the kinematic area, no LDS contact) must fit one CU's LDS
+    static_assert(4L * (GangTabs<RR>::WORDS + EPB * ((G::FIXED + G::MIN_CONTACT_WORDS + 3L) & ~3L)) <= 163840L,
+                  "gang env regions exceed the CU's LDS");
     const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
     // signed: with many workgroups per CU the share can be smaller than the model tables

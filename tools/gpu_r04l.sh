@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-4 dev pass: gang + teacher-forced tests; A/B base (committed) vs new; new vs align-all variant
+set -o pipefail
+TAG=${1:-r04l}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "gang or teacher_forced_parity or harder or workspace" > $OUT/tests.txt 2>&1; rc=$?
+tail -3 $OUT/tests.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python tools/ab_lib.py ab/base.so ab/new.so HumanoidPyBulletEnv-v0:4096 HumanoidFlagrunHarderPyBulletEnv-v0:4096 AtlasPyBulletEnv-v0:4096 > $OUT/ab_new.txt 2>&1 || exit 1
+cat $OUT/ab_new.txt
+timeout -k 10 600 python tools/ab_lib.py ab/new.so ab/alall.so Walker2DPyBulletEnv-v0:4096 HalfCheetahPyBulletEnv-v0:8192 HopperPyBulletEnv-v0:4096 > $OUT/ab_alall.txt 2>&1; rc=$?
+cat $OUT/ab_alall.txt
+exit $rc
