@@ -339,7 +339,7 @@ PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k
 template <class R, int ES>
 struct TRows {
   using T = Team<R>;
-  static constexpr int NDB = T::NDB, NC = T::NC, MR = 3 * T::NC;
+  static constexpr int NDB = T::NDB, NC = T::NC, MR = 3 * T::NC, ES_ = ES;
   static constexpr int PW = NDB + 2;    // per-lane words of a row
   static constexpr int W = 4 * PW + 4;  // words per env per row (P of its 4 lanes + S)
   static constexpr int SOFF = 4 * ES * PW;  // S block within a row region
@@ -434,6 +434,17 @@ struct TRows {
       row.meff = q[0]; row.tgt = q[n]; row.lam = q[2 * (size_t)n];
     }
   }
+  // LDS-resident row at word offset o of the wave's row regions (P(r) = rows + o, o = roff(r) +
+  // PW * lane; its S record at o + sdelta()): the normal sweep steps o by a compile-time stride
+  // instead of recomputing the row address from the row index
+  PBG_DEV int poff(int r) const { return roff(r) + PW * lane; }
+  PBG_DEV int sdelta() const { return SOFF + 4 * (lane >> 2) - PW * lane; }
+  static PBG_DEV void load_at(const lds_float* p, const lds_float* q, Row& row) {
+    const v4f a = *(const lds_float4*)p;
+    row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
+    const v2f b = *(const lds_float2*)q;
+    row.meff = b.x; row.tgt = b.y; row.lam = q[2];
+  }
   template <bool LDS>
   PBG_DEV void set_lam(int r, float v) const {
     if (LDS || r < cap) S(r)[2] = v;
@@ -489,7 +500,34 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
   // branch makes the compiler's LDS wait at the join conservative (lgkmcnt(0)), which
   // serialises every row behind the next row's loads.
   uint32_t pos = 0;
-  {
+  if constexpr (LDS && RW::PW == 4) {
+    // normal rows 0, 3, 6, ...: word offsets stepped by the compile-time row stride, the look-ahead
+    // clamped at the last normal row (an add and a min per row instead of the index arithmetic)
+    constexpr int NS = 3 * RW::ES_ * RW::W;
+    const int sd = rw.sdelta();
+    const lds_float* plast = rw.rows + rw.poff(3 * (nc - 1));
+    const lds_float *pA = rw.rows + rw.poff(0), *pB;
+    lds_float *qA = (lds_float*)pA + sd, *qB;
+    Row A, B;
+    RW::load_at(pA, qA, A);
+    int c = 0;
+    while (true) {
+      pB = pA + NS < plast ? pA + NS : plast;
+      qB = (lds_float*)pB + sd;
+      RW::load_at(pB, qB, B);
+      float nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
+      qA[2] = nl;
+      pos |= (nl > 0.f ? 1u : 0u) << c;
+      if (++c >= nc) break;
+      pA = pB + NS < plast ? pB + NS : plast;
+      qA = (lds_float*)pA + sd;
+      RW::load_at(pA, qA, A);
+      nl = RW::update(B, ub, uB, 0.f, 3.0e38f);
+      qB[2] = nl;
+      pos |= (nl > 0.f ? 1u : 0u) << c;
+      if (++c >= nc) break;
+    }
+  } else {
     Row A, B;
     rw.template load<LDS>(0, kb, A);
     int c = 0;
