@@ -29,13 +29,19 @@
 // kernel runs n/4 full waves (1,024 at 4,096 envs: one per SIMD).
 //
 // Per-env LDS region (words), [gang-shared]:
-//   L (NNZ) | Ld (N) | u (YS) | sw (3N) | sv (3N) | body frames (12 NB) | limit pos (2 NLIM)
-//   | limit rows NLIM x (YS + 5) | contacts 0..cap-1 x PERC
+//   L (NNZ) | Ld (N) | u (YS) | rhs (N) | s_w | s_v (6N, interleaved per index) | q | qd | tau (NJ
+//   each) | joint axis | origin (6 NJ, interleaved) | base state (13, front path) | cube state (13,
+//   FlagrunHarder) | body frames (12 NB) | limit pos (2 NLIM) | limit rows NLIM x (YS + 5) or the
+//   composites (16 NB) | contacts 0..cap-1 x PERC (kinematic parts, 16 NB, at the contacts' start
+//   until M is built).  Records start on 16-byte boundaries (Gang<R, T>::AL).
 // contact c: descriptor (DW) | mu | 3 rows x (y (YS) | m_eff | target | lambda); a row's y is
 // lane-major (lane t's NSL words y[t], y[t + T], ... contiguous: one ds_read_b64 for
 // Humanoid's two); contacts at c >= cap live at the same offsets in the env's device
 // workspace.  (Pairing m_eff | target and lambda | mu for b64 loads needs an even row length:
 // one word more per contact, which costs HalfCheetah at 8,192 envs one LDS-resident contact.)
+#ifdef PBG_DEV_CHECKS
+#include <cassert>
+#endif
 #include "pbg_fronts.h"
 
 namespace pbg {
@@ -435,6 +441,9 @@ struct GangCtx {
   lds_float* l;  // env LDS region
   float* g;      // env device workspace
   int cap;       // contacts resident in LDS
+#ifdef PBG_DEV_CHECKS
+  int env_words;  // the env region's words (contact_at's bound check)
+#endif
   int t;         // lane in the gang
   int le;        // gang in the wave
   SimP P;        // scene parameters (kernel arguments)
@@ -497,6 +506,9 @@ PBG_DEV int coff(int c) {
 template <class R, int T, class F>
 PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
   using G = Gang<R, T>;
+#ifdef PBG_DEV_CHECKS  // diagnostic build: a contact record inside its LDS region / workspace slice
+  assert(c >= 0 && c < G::MAXC && (c >= X.cap || G::FIXED + (c + 1) * G::PERC <= X.env_words));
+#endif
   if (c < X.cap) f(X.l + G::FIXED + coff<R, T>(c));
   else f(X.g + coff<R, T>(c));
 }
@@ -2032,6 +2044,9 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   X.l = lds + TT::WORDS + (threadIdx.x / T) * (env_words & ~(G::REGION_ALIGN - 1));
   X.g = scratch + (size_t)e * G::GWORDS;
   X.cap = cap;
+#ifdef PBG_DEV_CHECKS
+  X.env_words = env_words;
+#endif
   X.P = B.sp;
   const bool w0 = X.t == 0;
   STAMP_DECL
