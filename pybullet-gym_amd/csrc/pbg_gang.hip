@@ -650,20 +650,47 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
     }
   };
   {
-    Row A, B;
-    gang_load_row<R, T, LDS>(X, 0, 0, A);
-    int c = 0;
-    while (true) {
-      gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, B);
-      float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
-      gang_set_lam<R, T, LDS>(X, c, 0, nl);
-      mark(c, nl);
-      if (++c >= nc) break;
-      gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, A);
-      nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
-      gang_set_lam<R, T, LDS>(X, c, 0, nl);
-      mark(c, nl);
-      if (++c >= nc) break;
+    if constexpr (LDS || G::NSL > 2) {  // (Atlas, NSL = 3: a third register set spilled)
+      Row A, B;
+      gang_load_row<R, T, LDS>(X, 0, 0, A);
+      int c = 0;
+      while (true) {
+        gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, B);
+        float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        mark(c, nl);
+        if (++c >= nc) break;
+        gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, A);
+        nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        mark(c, nl);
+        if (++c >= nc) break;
+      }
+    } else {
+      // rows past the LDS capacity come from the device workspace (L2): loaded two rows ahead,
+      // three register sets in rotation (a row's impulse is written only by its own update, and a
+      // clamped look-ahead that re-reads the last row is never used)
+      Row A, B, C;
+      gang_load_row<R, T, LDS>(X, 0, 0, A);
+      gang_load_row<R, T, LDS>(X, min(1, nc - 1), 0, B);
+      int c = 0;
+      while (true) {
+        gang_load_row<R, T, LDS>(X, min(c + 2, nc - 1), 0, C);
+        float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        mark(c, nl);
+        if (++c >= nc) break;
+        gang_load_row<R, T, LDS>(X, min(c + 2, nc - 1), 0, A);
+        nl = gang_update<R, T>(B, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        mark(c, nl);
+        if (++c >= nc) break;
+        gang_load_row<R, T, LDS>(X, min(c + 2, nc - 1), 0, B);
+        nl = gang_update<R, T>(C, us, 0.f, 3.0e38f);
+        gang_set_lam<R, T, LDS>(X, c, 0, nl);
+        mark(c, nl);
+        if (++c >= nc) break;
+      }
     }
   }
   // next contact with a positive normal impulse (-1: none left)
@@ -1940,7 +1967,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
         const float nlo = clampf(llo[li] + meff * (ltl[li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dlo = nlo - llo[li];
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const float yu2 = meff > 0.f ? yu + dlo * lrm[li] : yu;
+        // lrm = 0 when meff = 0: no select on the chain (Atlas keeps it: without it the allocator
+        // spilled 48 bytes of its 512 registers)
+        const float yu2 = G::NSL > 2 && !(meff > 0.f) ? yu : yu + dlo * lrm[li];
         const float nhi = clampf(lhi[li] + meff * (lth[li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
         const float dhi = nhi - lhi[li];
         llo[li] = nlo;
