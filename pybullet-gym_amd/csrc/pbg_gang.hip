@@ -2064,7 +2064,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   X.tabs = lds;
   X.t = threadIdx.x % T;
   X.le = threadIdx.x / T;
-  const int e = blockIdx.x * EPB + X.le;
+  const int e = xcd_block() * EPB + X.le;
   if (e >= B.n) return;  // whole gangs only (no workgroup barrier below)
   X.le &= 64 / T - 1;     // gang within the wave (ballot masks)
   // (env_words is a multiple of REGION_ALIGN: saying so lets the compiler prove the 8 / 16-byte

@@ -248,6 +248,17 @@ struct State {
   std::conditional_t<(R::harder != 0), CubeState, NoCube> cube;
 };
 
+// XCD-aware block order for the step kernels: the dispatcher deals workgroups round-robin over the
+// 8 XCDs (workgroup b -> XCD b % 8), each with its own L2, so consecutive env blocks -- which share
+// the 128-byte lines of every SoA word (16 envs = 64 bytes) -- landed on different XCDs and each
+// fetched the whole line.  Block b processes env block (b % 8) * (G / 8) + b / 8: every XCD walks
+// one contiguous range of env blocks (a permutation when G % 8 == 0; identity otherwise).
+PBG_DEV int xcd_block() {
+  const int G = (int)gridDim.x, b = (int)blockIdx.x;
+  if (G & 7) return b;
+  return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 template <class R>
 PBG_DEV void load_state(State<R>& s, const float* __restrict__ st, int n, int e) {
 #pragma unroll

@@ -1271,7 +1271,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   using T = Team<R>;
   constexpr int NDB = T::NDB, SB = PBG_BASE_WORDS;
   extern __shared__ float lds_dyn[];
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tid = xcd_block() * blockDim.x + threadIdx.x;
   const int e = tid >> 2;
   if (e >= B.n) return;
   const Lane L = make_lane(tid & 3);
