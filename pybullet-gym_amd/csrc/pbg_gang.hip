@@ -1829,8 +1829,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   const int njobs = NLIM + 3 * nc;
 #endif
   // the front path holds its staged factor in registers for the rows pass unless it is too big to
-  // (Atlas: the register copy spilled 1.2 KB per lane; its rows read the LDS words instead)
-  constexpr bool LREG = !DIST || FP<R>::NF == 0 || G::NNZ4 + G::N4 <= 240;
+  // (Atlas: the register copy spilled 1.2 KB per lane; its rows read the LDS words instead) or the
+  // gang is 32 lanes wide (two waves per SIMD, 256 registers: 148 -> 12 bytes of spills, Humanoid
+  // -1.2 %, FlagrunHarder -13 % on 32-lane gangs; r04_ab_gang32_lds_factor.txt)
+  constexpr bool LREG = !DIST || FP<R>::NF == 0 || (T == 16 && G::NNZ4 + G::N4 <= 240);
   if constexpr (DIST && FP<R>::NF > 0 && LREG) gang_load_factor<R, T>(X, Lr, Ldr);
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
