@@ -4,7 +4,8 @@ is bench-like (Philox actions, pre-roll, one HIP graph of the timed steps).
 python tools/ab_lib.py LIB_A LIB_B ENV:N[:GANG_DIST[:GANG_LANES]] ...
 LIB_A / LIB_B: a libpbg_amd.so (run with this tree's Python package) or a directory holding a
 whole tree snapshot (its pybulletgym_amd.py, pybullet-gym_amd/ and built library), for a base
-whose C-ABI predates the current package's."""
+whose C-ABI predates the current package's.  (The snapshots live under ab/, which .gpurunignore
+keeps off the GPU box between A/B campaigns: drop that line to upload them.)"""
 import os
 import subprocess
 import sys
