@@ -1,6 +1,13 @@
-// Small fixed-size vector / matrix helpers and Philox4x32-10 for the step kernel.
+// Small fixed-size vector / matrix helpers and Philox4x32-10 for the step kernels.
+//
+// The physics types are templates over the scalar S: float for the float32 kernels, double for
+// the reference-precision path (pybullet's btScalar is double, scene_bases.py:75-76 ->
+// stepSimulation).  The float names (f3, m3, s6) are the S = float instances; every helper
+// deduces S from its vector / matrix operands, and compile-time model constants enter through
+// a non-deduced scalar (nd<S>), so a float kernel's code is what it was before the templates.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #define PBG_DEV __device__ __forceinline__
@@ -19,26 +26,53 @@ PBG_DEV void static_for(F&& f) {
   if constexpr (E > B) static_for_impl<B>(f, std::make_integer_sequence<int, E - B>{});
 }
 
-struct f3 {
-  float x, y, z;
+// a scalar parameter that takes part in no deduction (converted to S)
+template <class S>
+struct nd_ {
+  using type = S;
 };
-PBG_DEV f3 mk3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
-PBG_DEV f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
-PBG_DEV f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
-PBG_DEV f3 operator-(f3 a) { return mk3(-a.x, -a.y, -a.z); }
-PBG_DEV f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
-PBG_DEV f3& operator+=(f3& a, f3 b) { a.x += b.x; a.y += b.y; a.z += b.z; return a; }
-PBG_DEV float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-PBG_DEV f3 cross3(f3 a, f3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+template <class S>
+using nd = typename nd_<S>::type;
+
+template <class S>
+struct V3 {
+  S x, y, z;
+};
+using f3 = V3<float>;
+// mk3(x, y, z): a float vector; mk3<double>(x, y, z): a double one
+template <class S = float>
+PBG_DEV V3<S> mk3(nd<S> x, nd<S> y, nd<S> z) { V3<S> r; r.x = x; r.y = y; r.z = z; return r; }
+template <class S>
+PBG_DEV V3<S> operator+(V3<S> a, V3<S> b) { return mk3<S>(a.x + b.x, a.y + b.y, a.z + b.z); }
+template <class S>
+PBG_DEV V3<S> operator-(V3<S> a, V3<S> b) { return mk3<S>(a.x - b.x, a.y - b.y, a.z - b.z); }
+template <class S>
+PBG_DEV V3<S> operator-(V3<S> a) { return mk3<S>(-a.x, -a.y, -a.z); }
+template <class S>
+PBG_DEV V3<S> operator*(nd<S> s, V3<S> a) { return mk3<S>(s * a.x, s * a.y, s * a.z); }
+template <class S>
+PBG_DEV V3<S>& operator+=(V3<S>& a, V3<S> b) { a.x += b.x; a.y += b.y; a.z += b.z; return a; }
+template <class S>
+PBG_DEV S dot3(V3<S> a, V3<S> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <class S>
+PBG_DEV V3<S> cross3(V3<S> a, V3<S> b) {
+  return mk3<S>(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
 // Physics-side fast reciprocal / sqrt (v_rcp_f32 / v_sqrt_f32 / v_rsq_f32, ~1 ulp); the
-// numpy-exact pack keeps IEEE division and sqrt.
+// numpy-exact pack keeps IEEE division and sqrt.  The double overloads are the IEEE operations
+// (correctly rounded division and sqrt): the reference-precision path's accuracy is float64's.
 PBG_DEV float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 PBG_DEV float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
-PBG_DEV float norm3(f3 a) { return fast_sqrt(dot3(a, a)); }
+PBG_DEV double fast_rcp(double x) { return 1.0 / x; }
+PBG_DEV double fast_sqrt(double x) { return __builtin_sqrt(x); }
+PBG_DEV double fast_rsq(double x) { return 1.0 / __builtin_sqrt(x); }
+template <class S>
+PBG_DEV S norm3(V3<S> a) { return fast_sqrt(dot3(a, a)); }
 // clamp(x, lo, hi) for lo <= hi in one v_med3_f32 (fminf(fmaxf()) costs two instructions
 // plus the IEEE canonicalisations of its operands); same result for non-NaN x
 PBG_DEV float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+PBG_DEV double clampf(double x, double lo, double hi) { return __builtin_fmin(__builtin_fmax(x, lo), hi); }
 
 
 // sin/cos for the moderate arguments of the physics (joint angles, exp-map half angles):
@@ -59,17 +93,23 @@ PBG_DEV void sincos_fast(float x, float* sp, float* cp) {
   *sp = (q & 2) ? -s0 : s0;
   *cp = ((q + 1) & 2) ? -c0 : c0;
 }
+// float64: the device library's sincos (ocml, within 1 ulp), as the oracle's libm sin / cos
+PBG_DEV void sincos_fast(double x, double* sp, double* cp) { sincos(x, sp, cp); }
 
 // row-major 3x3
-struct m3 {
-  float m[9];
+template <class S>
+struct M3 {
+  S m[9];
 };
-PBG_DEV f3 mul(const m3& A, f3 v) {
-  return mk3(A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
-             A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z);
+using m3 = M3<float>;
+template <class S>
+PBG_DEV V3<S> mul(const M3<S>& A, V3<S> v) {
+  return mk3<S>(A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
+                A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z);
 }
-PBG_DEV m3 mul(const m3& A, const m3& B) {
-  m3 C;
+template <class S>
+PBG_DEV M3<S> mul(const M3<S>& A, const M3<S>& B) {
+  M3<S> C;
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
@@ -77,19 +117,21 @@ PBG_DEV m3 mul(const m3& A, const m3& B) {
       C.m[3 * i + j] = A.m[3 * i] * B.m[j] + A.m[3 * i + 1] * B.m[3 + j] + A.m[3 * i + 2] * B.m[6 + j];
   return C;
 }
-PBG_DEV m3 quat_to_m3(float x, float y, float z, float w) {
-  m3 R;
+template <class S>
+PBG_DEV M3<S> quat_to_m3(S x, S y, S z, S w) {
+  M3<S> R;
   R.m[0] = 1 - 2 * (y * y + z * z); R.m[1] = 2 * (x * y - w * z); R.m[2] = 2 * (x * z + w * y);
   R.m[3] = 2 * (x * y + w * z); R.m[4] = 1 - 2 * (x * x + z * z); R.m[5] = 2 * (y * z - w * x);
   R.m[6] = 2 * (x * z - w * y); R.m[7] = 2 * (y * z + w * x); R.m[8] = 1 - 2 * (x * x + y * y);
   return R;
 }
 // rotation by angle about a unit axis given by compile-time constants
-PBG_DEV m3 axis_angle_m3(float ax, float ay, float az, float ang) {
-  float s, c;
+template <class S>
+PBG_DEV M3<S> axis_angle_m3(nd<S> ax, nd<S> ay, nd<S> az, S ang) {
+  S s, c;
   sincos_fast(ang, &s, &c);
-  float t = 1 - c;
-  m3 R;
+  S t = 1 - c;
+  M3<S> R;
   R.m[0] = t * ax * ax + c;      R.m[1] = t * ax * ay - s * az; R.m[2] = t * ax * az + s * ay;
   R.m[3] = t * ax * ay + s * az; R.m[4] = t * ay * ay + c;      R.m[5] = t * ay * az - s * ax;
   R.m[6] = t * ax * az - s * ay; R.m[7] = t * ay * az + s * ax; R.m[8] = t * az * az + c;
@@ -101,64 +143,76 @@ PBG_DEV m3 axis_angle_m3(float ax, float ay, float az, float ang) {
 // x + (-0) == x exactly, so whole terms fold away (no fast-math needed).
 // Only a compile-time c is inspected (__builtin_constant_p resolves after inlining); a
 // run-time c is a plain product (no selects).
-PBG_DEV float kmul(float c, float x) {
-  if (__builtin_constant_p(c)) return c == 0.f ? -0.f : (c == 1.f ? x : (c == -1.f ? -x : c * x));
+template <class S>
+PBG_DEV S kmul(nd<S> c, S x) {
+  if (__builtin_constant_p(c)) return c == S(0) ? -S(0) : (c == S(1) ? x : (c == S(-1) ? -x : c * x));
   return c * x;
 }
 // A * c for a constant vector c
-PBG_DEV f3 mulc(const m3& A, float cx, float cy, float cz) {
-  return mk3(kmul(cx, A.m[0]) + kmul(cy, A.m[1]) + kmul(cz, A.m[2]), kmul(cx, A.m[3]) + kmul(cy, A.m[4]) + kmul(cz, A.m[5]),
-             kmul(cx, A.m[6]) + kmul(cy, A.m[7]) + kmul(cz, A.m[8]));
+template <class S>
+PBG_DEV V3<S> mulc(const M3<S>& A, nd<S> cx, nd<S> cy, nd<S> cz) {
+  return mk3<S>(kmul<S>(cx, A.m[0]) + kmul<S>(cy, A.m[1]) + kmul<S>(cz, A.m[2]),
+                kmul<S>(cx, A.m[3]) + kmul<S>(cy, A.m[4]) + kmul<S>(cz, A.m[5]),
+                kmul<S>(cx, A.m[6]) + kmul<S>(cy, A.m[7]) + kmul<S>(cz, A.m[8]));
 }
-PBG_DEV f3 mulc(const m3& A, f3 c) { return mulc(A, c.x, c.y, c.z); }
+template <class S>
+PBG_DEV V3<S> mulc(const M3<S>& A, V3<S> c) { return mulc<S>(A, c.x, c.y, c.z); }
 // A * C for a constant matrix C (row-major)
-PBG_DEV m3 mulc(const m3& A, const m3& C) {
-  m3 O;
+template <class S>
+PBG_DEV M3<S> mulc(const M3<S>& A, const M3<S>& C) {
+  M3<S> O;
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++)
-      O.m[3 * i + j] = kmul(C.m[j], A.m[3 * i]) + kmul(C.m[3 + j], A.m[3 * i + 1]) + kmul(C.m[6 + j], A.m[3 * i + 2]);
+      O.m[3 * i + j] = kmul<S>(C.m[j], A.m[3 * i]) + kmul<S>(C.m[3 + j], A.m[3 * i + 1]) + kmul<S>(C.m[6 + j], A.m[3 * i + 2]);
   return O;
 }
 // constant quaternion (x,y,z,w) -> matrix, folded at compile time
-PBG_DEV m3 quat_to_m3c(double x, double y, double z, double w) {
-  m3 R;
-  R.m[0] = (float)(1 - 2 * (y * y + z * z)); R.m[1] = (float)(2 * (x * y - w * z)); R.m[2] = (float)(2 * (x * z + w * y));
-  R.m[3] = (float)(2 * (x * y + w * z)); R.m[4] = (float)(1 - 2 * (x * x + z * z)); R.m[5] = (float)(2 * (y * z - w * x));
-  R.m[6] = (float)(2 * (x * z - w * y)); R.m[7] = (float)(2 * (y * z + w * x)); R.m[8] = (float)(1 - 2 * (x * x + y * y));
+template <class S = float>
+PBG_DEV M3<S> quat_to_m3c(double x, double y, double z, double w) {
+  M3<S> R;
+  R.m[0] = (S)(1 - 2 * (y * y + z * z)); R.m[1] = (S)(2 * (x * y - w * z)); R.m[2] = (S)(2 * (x * z + w * y));
+  R.m[3] = (S)(2 * (x * y + w * z)); R.m[4] = (S)(1 - 2 * (x * x + z * z)); R.m[5] = (S)(2 * (y * z - w * x));
+  R.m[6] = (S)(2 * (x * z - w * y)); R.m[7] = (S)(2 * (y * z + w * x)); R.m[8] = (S)(1 - 2 * (x * x + y * y));
   return R;
 }
 // rotation about a constant unit axis
-PBG_DEV m3 axis_angle_m3c(float ax, float ay, float az, float ang) {
-  float s, c;
+template <class S>
+PBG_DEV M3<S> axis_angle_m3c(nd<S> ax, nd<S> ay, nd<S> az, S ang) {
+  S s, c;
   sincos_fast(ang, &s, &c);
-  const float t = 1 - c;
-  m3 R;
-  R.m[0] = kmul(ax * ax, t) + c;       R.m[1] = kmul(ax * ay, t) - kmul(az, s); R.m[2] = kmul(ax * az, t) + kmul(ay, s);
-  R.m[3] = kmul(ax * ay, t) + kmul(az, s); R.m[4] = kmul(ay * ay, t) + c;       R.m[5] = kmul(ay * az, t) - kmul(ax, s);
-  R.m[6] = kmul(ax * az, t) - kmul(ay, s); R.m[7] = kmul(ay * az, t) + kmul(ax, s); R.m[8] = kmul(az * az, t) + c;
+  const S t = 1 - c;
+  M3<S> R;
+  R.m[0] = kmul<S>(ax * ax, t) + c;       R.m[1] = kmul<S>(ax * ay, t) - kmul<S>(az, s); R.m[2] = kmul<S>(ax * az, t) + kmul<S>(ay, s);
+  R.m[3] = kmul<S>(ax * ay, t) + kmul<S>(az, s); R.m[4] = kmul<S>(ay * ay, t) + c;       R.m[5] = kmul<S>(ay * az, t) - kmul<S>(ax, s);
+  R.m[6] = kmul<S>(ax * az, t) - kmul<S>(ay, s); R.m[7] = kmul<S>(ay * az, t) + kmul<S>(ax, s); R.m[8] = kmul<S>(az * az, t) + c;
   return R;
 }
 
 // symmetric 3x3 stored (xx, yy, zz, xy, xz, yz)
-struct s6 {
-  float a[6];
+template <class S>
+struct S6 {
+  S a[6];
 };
-PBG_DEV f3 mul(const s6& S, f3 v) {
-  return mk3(S.a[0] * v.x + S.a[3] * v.y + S.a[4] * v.z, S.a[3] * v.x + S.a[1] * v.y + S.a[5] * v.z,
-             S.a[4] * v.x + S.a[5] * v.y + S.a[2] * v.z);
+using s6 = S6<float>;
+template <class S>
+PBG_DEV V3<S> mul(const S6<S>& W, V3<S> v) {
+  return mk3<S>(W.a[0] * v.x + W.a[3] * v.y + W.a[4] * v.z, W.a[3] * v.x + W.a[1] * v.y + W.a[5] * v.z,
+                W.a[4] * v.x + W.a[5] * v.y + W.a[2] * v.z);
 }
-// R I R^T for body-frame inertia I6 = (xx, yy, zz, xy, xz, yz)
-PBG_DEV s6 rotate_inertia(const m3& R, const float* I6) {
-  const float I[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
-  float RI[9];
+// R I R^T for body-frame inertia I6 = (xx, yy, zz, xy, xz, yz) (model constants: converted to S
+// first)
+template <class S, class IT>
+PBG_DEV S6<S> rotate_inertia(const M3<S>& R, const IT* I6) {
+  const S I[9] = {(S)I6[0], (S)I6[3], (S)I6[4], (S)I6[3], (S)I6[1], (S)I6[5], (S)I6[4], (S)I6[5], (S)I6[2]};
+  S RI[9];
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++)
-      RI[3 * i + j] = kmul(I[j], R.m[3 * i]) + kmul(I[3 + j], R.m[3 * i + 1]) + kmul(I[6 + j], R.m[3 * i + 2]);
-  s6 W;
+      RI[3 * i + j] = kmul<S>(I[j], R.m[3 * i]) + kmul<S>(I[3 + j], R.m[3 * i + 1]) + kmul<S>(I[6 + j], R.m[3 * i + 2]);
+  S6<S> W;
   W.a[0] = RI[0] * R.m[0] + RI[1] * R.m[1] + RI[2] * R.m[2];
   W.a[1] = RI[3] * R.m[3] + RI[4] * R.m[4] + RI[5] * R.m[5];
   W.a[2] = RI[6] * R.m[6] + RI[7] * R.m[7] + RI[8] * R.m[8];
@@ -166,11 +220,6 @@ PBG_DEV s6 rotate_inertia(const m3& R, const float* I6) {
   W.a[4] = RI[0] * R.m[6] + RI[1] * R.m[7] + RI[2] * R.m[8];
   W.a[5] = RI[3] * R.m[6] + RI[4] * R.m[7] + RI[5] * R.m[8];
   return W;
-}
-
-PBG_DEV s6 rotate_inertia(const m3& R, const double* I6) {
-  const float I[6] = {(float)I6[0], (float)I6[1], (float)I6[2], (float)I6[3], (float)I6[4], (float)I6[5]};
-  return rotate_inertia(R, I);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

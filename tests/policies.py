@@ -66,12 +66,14 @@ def reset_draws(n: int, nr: int, seed: int) -> np.ndarray:
     return np.random.default_rng(seed).uniform(-0.1, 0.1, (n, nr))
 
 
-def episode_returns_oracle(env_id: str, n: int, seed: int = 0, steps: int = MAX_STEPS, nthreads: int = 8):
-    """One episode per env (until done or `steps`) through the CPU oracle.
+def episode_returns_oracle(env_id: str, n: int, seed: int = 0, steps: int = MAX_STEPS, nthreads: int = 8,
+                           precision: int = 64):
+    """One episode per env (until done or `steps`) through the CPU oracle (precision 64: float64
+    physics; 32: the same algorithm in IEEE float32, the kernels' formulation).
     Returns (returns[n] float64, lengths[n] int)."""
     import oracle
     pi = Policy(env_id)
-    e = oracle.OracleEnvs(env_id, n, nthreads=nthreads)
+    e = oracle.OracleEnvs(env_id, n, nthreads=nthreads, precision=precision)
     obs = e.reset(reset_draws(n, e.info.NR, seed))
     ret = np.zeros(n)
     length = np.zeros(n, dtype=np.int64)
