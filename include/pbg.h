@@ -91,7 +91,10 @@ typedef struct {
                          sub-step (sim_params.h pbg_contact_hash; for parity tests) */
 } pbg_step_io_t;
 
-/* Test / diagnostic launch options (pbg_create_debug).  -1 = the default everywhere. */
+/* Test / diagnostic launch options (pbg_create_debug / pbg_create_ex).  -1 = the default everywhere.
+ * ABI note: round 4 appended gang_lanes (3 -> 4 ints) without a size field; the struct is frozen at
+ * these four ints.  Callers that need another option use pbg_create_v2 (pbg_create_opts_t is
+ * versioned by its struct_size). */
 typedef struct {
   int kernel;     /* 0: one-lane-per-env kernel for every robot; 2: the 16-lane gang kernel for
                      every walker (Ant included); -1 / 1: default (quad for Ant, gang otherwise) */
@@ -119,6 +122,22 @@ typedef struct {
   double joint_limit_erp; /* [0, 1]: share of a joint-limit violation corrected per sub-step */
 } pbg_sim_params_t;
 
+/* Options of pbg_create_v2, versioned: set struct_size = sizeof(pbg_create_opts_t) of the header the
+ * caller was built with; the library reads only the fields that size covers (fields past it take
+ * their defaults), so options appended later never read past an older caller's struct. */
+typedef struct {
+  uint32_t struct_size;  /* sizeof(pbg_create_opts_t) at the caller's build */
+  int precision;         /* physics state and arithmetic: 32 = float32 (the default; the fast
+                            kernels) or 64 = float64, the reference's precision (pybullet's
+                            btScalar is double: stepSimulation, scene_bases.py:75-76).  The
+                            observation / reward pack is float64 in both, as in the reference.
+                            64: every env id but AtlasPyBulletEnv-v0 (PBG_E_HIP) */
+  int kernel;            /* as in pbg_debug_opts_t; precision 32 only */
+  int lds_rows;
+  int gang_dist;
+  int gang_lanes;
+} pbg_create_opts_t;
+
 /* The reference's parameters for env_id (see pbg_sim_params_t). */
 int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out);
 
@@ -140,6 +159,13 @@ int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, 
  * diagnostic launch options (NULL = defaults).  PBG_E_ARG for parameters out of range. */
 int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                   const pbg_sim_params_t* params, const pbg_debug_opts_t* opts, pbg_handle** out);
+/* pbg_create_ex with versioned options (opts NULL = defaults: float32, the default kernels).
+ * PBG_E_ARG for a bad struct_size or precision; PBG_E_HIP when the env id has no kernel of the
+ * requested precision. */
+int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                  const pbg_sim_params_t* params, const pbg_create_opts_t* opts, pbg_handle** out);
+/* The handle's physics precision: 32 or 64 (PBG_E_ARG for NULL). */
+int pbg_precision(const pbg_handle* h);
 /* The parameters a handle was created with. */
 int pbg_get_sim_params(const pbg_handle* h, pbg_sim_params_t* out);
 /* BaseBulletEnv._close (env_bases.py:103-107) */

@@ -44,6 +44,15 @@ class DebugOpts(ctypes.Structure):
                 ("gang_lanes", ctypes.c_int)]
 
 
+class CreateOpts(ctypes.Structure):
+    """pbg_create_opts_t (pbg_create_v2): versioned by struct_size; precision 32 or 64."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("precision", ctypes.c_int), ("kernel", ctypes.c_int),
+                ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int), ("gang_lanes", ctypes.c_int)]
+
+    def __init__(self, precision=32, kernel=-1, lds_rows=-1, gang_dist=-1, gang_lanes=-1):
+        super().__init__(ctypes.sizeof(CreateOpts), precision, kernel, lds_rows, gang_dist, gang_lanes)
+
+
 class SimParams(ctypes.Structure):
     """pbg_sim_params_t: the scene of a handle (scene_bases.py:8-18,58-73)."""
     _fields_ = [("gravity", ctypes.c_double), ("timestep", ctypes.c_double), ("frame_skip", ctypes.c_int),
@@ -73,6 +82,9 @@ def lib():
                                    ctypes.POINTER(H)]
     L.pbg_create_ex.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(SimParams),
                                 ctypes.POINTER(DebugOpts), ctypes.POINTER(H)]
+    L.pbg_create_v2.argtypes = [ctypes.c_char_p, I, I, ctypes.c_uint64, I, ctypes.POINTER(SimParams),
+                                ctypes.POINTER(CreateOpts), ctypes.POINTER(H)]
+    L.pbg_precision.argtypes = [H]
     L.pbg_default_sim_params.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimParams)]
     L.pbg_get_sim_params.argtypes = [H, ctypes.POINTER(SimParams)]
     L.pbg_sample_actions.argtypes = [I, I, I, ctypes.c_uint64, ctypes.c_uint32, I, P, P]
@@ -89,13 +101,14 @@ def lib():
     L.pbg_last_error.restype = ctypes.c_char_p
     for f in ("pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state", "pbg_set_state",
               "pbg_pack_record_sizes", "pbg_pack", "pbg_create_debug", "pbg_sample_actions", "pbg_create_ex",
-              "pbg_default_sim_params", "pbg_get_sim_params"):
+              "pbg_default_sim_params", "pbg_get_sim_params", "pbg_create_v2", "pbg_precision"):
         getattr(L, f).restype = I
     _lib = L
     return L
 
 
-EXPORTED = ("pbg_create", "pbg_create_debug", "pbg_create_ex", "pbg_default_sim_params", "pbg_get_sim_params",
+EXPORTED = ("pbg_create", "pbg_create_debug", "pbg_create_ex", "pbg_create_v2", "pbg_precision",
+            "pbg_default_sim_params", "pbg_get_sim_params",
             "pbg_destroy", "pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex",
             "pbg_get_state", "pbg_set_state", "pbg_pack_record_sizes", "pbg_pack", "pbg_sample_actions",
             "pbg_last_error")

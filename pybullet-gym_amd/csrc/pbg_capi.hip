@@ -49,12 +49,16 @@ int env_robot_id(const char* env_id) {
   return -1;
 }
 
-struct Ops {
+// The per-robot kernels of one precision (pbg_robot.hip)
+struct Kern {
   int (*plan)(int, int, int, pbg::Geometry*);
   int (*step)(const pbg::Buffers&, const pbg::StepIO&, float*, const pbg::Geometry&, hipStream_t);
   int (*reset)(const pbg::Buffers&, const pbg::ResetIO&, hipStream_t);
   int (*get_state)(const pbg::Buffers&, double*, double*, hipStream_t);
   int (*set_state)(const pbg::Buffers&, const double*, const double*, hipStream_t);
+};
+struct Ops {
+  Kern k32, k64;  // float32 kernels; the float64 (reference-precision) kernels
   int (*pack)(int, const double*, double*, hipStream_t);
   pbg_info_t info;
   int pack_in, pack_out;
@@ -99,10 +103,13 @@ int check_sim_params(const pbg_sim_params_t& p) {
   return PBG_OK;
 }
 
-#define PBG_OPS(NAME, RID)                                                                               \
-  Ops{pbg::plan_##NAME, pbg::launch_step_##NAME, pbg::launch_reset_##NAME, pbg::launch_get_state_##NAME, \
-      pbg::launch_set_state_##NAME, pbg::launch_pack_##NAME, info_of<pbg_models::NAME>(RID),             \
-      pbg::PackRec<pbg_models::NAME>::IN, pbg::PackRec<pbg_models::NAME>::OUT, defaults_of<pbg_models::NAME>()}
+#define PBG_OPS(NAME, RID)                                                                                   \
+  Ops{Kern{pbg::plan_##NAME, pbg::launch_step_##NAME, pbg::launch_reset_##NAME, pbg::launch_get_state_##NAME,  \
+           pbg::launch_set_state_##NAME},                                                                    \
+      Kern{pbg::plan64_##NAME, pbg::launch_step64_##NAME, pbg::launch_reset64_##NAME,                        \
+           pbg::launch_get_state64_##NAME, pbg::launch_set_state64_##NAME},                                  \
+      pbg::launch_pack_##NAME, info_of<pbg_models::NAME>(RID), pbg::PackRec<pbg_models::NAME>::IN,          \
+      pbg::PackRec<pbg_models::NAME>::OUT, defaults_of<pbg_models::NAME>()}
 
 const Ops* ops(int rid) {
   static const Ops table[17] = {PBG_OPS(Pendulum, 0), PBG_OPS(Hopper, 1), PBG_OPS(HalfCheetah, 2), PBG_OPS(Ant, 3),
@@ -146,7 +153,9 @@ int device_of(const void* p) {
 
 struct pbg_handle {
   int rid, device, n;
+  int precision;  // 32 or 64 (pbg_create_v2)
   const Ops* ops;
+  const Kern* k;  // the kernels of that precision
   pbg::Buffers B;
   float* scratch;
   pbg::Geometry geo;
@@ -177,7 +186,34 @@ int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, 
 
 int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                   const pbg_sim_params_t* params, const pbg_debug_opts_t* opts, pbg_handle** out) {
+  pbg_create_opts_t o;
+  memset(&o, 0, sizeof(o));
+  o.struct_size = (uint32_t)sizeof(o);
+  o.precision = 32;
+  o.kernel = opts ? opts->kernel : -1;
+  o.lds_rows = opts ? opts->lds_rows : -1;
+  o.gang_dist = opts ? opts->gang_dist : -1;
+  o.gang_lanes = opts ? opts->gang_lanes : -1;
+  return pbg_create_v2(env_id, n_envs, device, seed, env_offset, params, &o, out);
+}
+
+int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
+                  const pbg_sim_params_t* params, const pbg_create_opts_t* copts, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
+  // versioned options: read only the fields the caller's struct holds (struct_size); absent = defaults
+  pbg_create_opts_t co;
+  memset(&co, 0, sizeof(co));
+  co.precision = 32; co.kernel = -1; co.lds_rows = -1; co.gang_dist = -1; co.gang_lanes = -1;
+  if (copts) {
+    if (copts->struct_size < (uint32_t)(2 * sizeof(uint32_t)) || copts->struct_size > (uint32_t)sizeof(co))
+      return fail(PBG_E_ARG, "pbg_create_v2: opts->struct_size %s%ld is not a pbg_create_opts_t size", "",
+                  (long)copts->struct_size);
+    memcpy(&co, copts, copts->struct_size);
+  }
+  if (co.precision != 32 && co.precision != 64)
+    return fail(PBG_E_ARG, "pbg_create_v2: precision must be 32 or 64%s (got %ld)", "", co.precision);
+  const pbg_debug_opts_t dbg = {co.kernel, co.lds_rows, co.gang_dist, co.gang_lanes};
+  const pbg_debug_opts_t* opts = &dbg;
   *out = nullptr;
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_create: unknown env id '%s'%ld", env_id ? env_id : "(null)");
@@ -194,7 +230,9 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   h->rid = rid;
   h->device = device;
   h->n = n_envs;
+  h->precision = co.precision;
   h->ops = o;
+  h->k = co.precision == 64 ? &o->k64 : &o->k32;
   h->info = o->info;
   h->info.n_envs = n_envs;
   h->info.substeps = sp.frame_skip;
@@ -203,8 +241,10 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   B.n = n_envs;
   B.seed = seed;
   B.env_offset = env_offset;
-  B.sp = pbg::resolve_sim_params(sp.timestep, sp.frame_skip, sp.solver_iterations, sp.gravity, sp.contact_erp,
-                                 sp.joint_limit_erp, PBG_ANGULAR_MOTION_THRESHOLD);
+  B.sp = pbg::resolve_sim_params<float>(sp.timestep, sp.frame_skip, sp.solver_iterations, sp.gravity, sp.contact_erp,
+                                        sp.joint_limit_erp, PBG_ANGULAR_MOTION_THRESHOLD);
+  B.sp64 = pbg::resolve_sim_params<double>(sp.timestep, sp.frame_skip, sp.solver_iterations, sp.gravity,
+                                           sp.contact_erp, sp.joint_limit_erp, PBG_ANGULAR_MOTION_THRESHOLD);
   const size_t n = (size_t)n_envs;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -213,12 +253,19 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   const int mode = (opts && (opts->kernel == 0 || opts->kernel == 2)) ? opts->kernel : 1;
   h->geo.force_dist = opts ? opts->gang_dist : -1;
   h->geo.gang_lanes = (opts && (opts->gang_lanes == 16 || opts->gang_lanes == 32)) ? opts->gang_lanes : -1;
-  int e = hip_check(o->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
+  int e = hip_check(h->k->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
+  if (e && co.precision == 64) {
+    snprintf(g_err, sizeof(g_err), "pbg_create: no float64 kernel for %s (Atlas' 886 contact slots have no lane kernel)",
+             env_id);
+    delete h;
+    return PBG_E_HIP;
+  }
   // cap on the LDS-resident contact rows (tests of the device-workspace path)
   if (opts && opts->lds_rows >= 0 && opts->lds_rows < h->geo.lds_rows) h->geo.lds_rows = opts->lds_rows;
-  e |= hip_check(hipMalloc(&B.st, sizeof(float) * n * h->info.state_words), "hipMalloc state");
+  const size_t wb = co.precision == 64 ? sizeof(double) : sizeof(float);  // state / z0 / workspace word
+  e |= hip_check(hipMalloc(&B.st, wb * n * h->info.state_words), "hipMalloc state");
   e |= hip_check(hipMalloc(&B.pot, sizeof(double) * n), "hipMalloc potential");
-  e |= hip_check(hipMalloc(&B.z0, sizeof(float) * n), "hipMalloc z0");
+  e |= hip_check(hipMalloc(&B.z0, wb * n), "hipMalloc z0");
   e |= hip_check(hipMalloc(&B.elapsed, sizeof(int) * n), "hipMalloc elapsed");
   e |= hip_check(hipMalloc(&B.flags, sizeof(uint32_t) * n), "hipMalloc flags");
   e |= hip_check(hipMalloc(&B.episode, sizeof(uint32_t) * n), "hipMalloc episode");
@@ -226,11 +273,11 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   e |= hip_check(hipMalloc(&B.ftm, sizeof(int32_t) * 2 * n), "hipMalloc flag counters");
   e |= hip_check(hipMalloc(&B.hkd, sizeof(double) * 2 * n), "hipMalloc crawl potentials");
   e |= hip_check(hipMalloc(&B.hki, sizeof(int32_t) * 3 * n), "hipMalloc cube counters");
-  e |= hip_check(hipMalloc(&h->scratch, sizeof(float) * n * h->geo.scratch_words_per_env), "hipMalloc scratch");
+  e |= hip_check(hipMalloc(&h->scratch, (size_t)h->geo.word_bytes * n * h->geo.scratch_words_per_env), "hipMalloc scratch");
   if (!e) {
-    e |= hip_check(hipMemset(B.st, 0, sizeof(float) * n * h->info.state_words), "hipMemset");
+    e |= hip_check(hipMemset(B.st, 0, wb * n * h->info.state_words), "hipMemset");
     e |= hip_check(hipMemset(B.pot, 0, sizeof(double) * n), "hipMemset");
-    e |= hip_check(hipMemset(B.z0, 0, sizeof(float) * n), "hipMemset");
+    e |= hip_check(hipMemset(B.z0, 0, wb * n), "hipMemset");
     e |= hip_check(hipMemset(B.elapsed, 0, sizeof(int) * n), "hipMemset");
     e |= hip_check(hipMemset(B.flags, 0, sizeof(uint32_t) * n), "hipMemset");
     e |= hip_check(hipMemset(B.episode, 0, sizeof(uint32_t) * n), "hipMemset");
@@ -264,6 +311,8 @@ int pbg_get_sim_params(const pbg_handle* h, pbg_sim_params_t* out) {
   return PBG_OK;
 }
 
+int pbg_precision(const pbg_handle* h) { return h ? h->precision : PBG_E_ARG; }
+
 int pbg_info(const pbg_handle* h, pbg_info_t* out) {
   if (!h || !out) return fail(PBG_E_ARG, "pbg_info: NULL argument%s%ld");
   *out = h->info;
@@ -280,7 +329,7 @@ int pbg_reset(pbg_handle* h, const uint8_t* mask, const float* init_q, float* ob
   if (!h || !obs) return fail(PBG_E_ARG, "pbg_reset: NULL handle or obs%s%ld");
   DeviceGuard dg(h->device);
   pbg::ResetIO io{mask, init_q, obs};
-  return hip_check(h->ops->reset(h->B, io, (hipStream_t)stream), "reset_kernel launch");
+  return hip_check(h->k->reset(h->B, io, (hipStream_t)stream), "reset_kernel launch");
 }
 
 int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
@@ -289,7 +338,7 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream) {
   DeviceGuard dg(h->device);
   pbg::StepIO s{io->act, io->obs, io->rew, io->rew64, io->done, io->trunc, io->term_obs, io->ncontact, io->autoreset,
                 io->rew_terms, io->csig};
-  return hip_check(h->ops->step(h->B, s, h->scratch, h->geo, (hipStream_t)stream), "step_kernel launch");
+  return hip_check(h->k->step(h->B, s, h->scratch, h->geo, (hipStream_t)stream), "step_kernel launch");
 }
 
 int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* done, void* stream) {
@@ -305,13 +354,13 @@ int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* d
 int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream) {
   if (!h || !phys || !aux) return fail(PBG_E_ARG, "pbg_get_state: NULL argument%s%ld");
   DeviceGuard dg(h->device);
-  return hip_check(h->ops->get_state(h->B, phys, aux, (hipStream_t)stream), "get_state launch");
+  return hip_check(h->k->get_state(h->B, phys, aux, (hipStream_t)stream), "get_state launch");
 }
 
 int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream) {
   if (!h || !phys) return fail(PBG_E_ARG, "pbg_set_state: NULL argument%s%ld");
   DeviceGuard dg(h->device);
-  return hip_check(h->ops->set_state(h->B, phys, aux, (hipStream_t)stream), "set_state launch");
+  return hip_check(h->k->set_state(h->B, phys, aux, (hipStream_t)stream), "set_state launch");
 }
 
 int pbg_pack_record_sizes(const char* env_id, int* in_words, int* out_words) {

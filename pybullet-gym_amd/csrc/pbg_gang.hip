@@ -1877,7 +1877,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       if constexpr (R::harder) {  // the cube's columns: +-(nd / sqrt m, (r x nd) / sqrt I), r its lever arm
         const f3 rc = cubef > 0.f ? rA : rB;
         const f3 mc = cross3(rc, nd);
-        const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+        const float rm = 1.f / CubeK<float>::sm(), rI = 1.f / CubeK<float>::sI();
         ycl = cubef * rm * nd;
         cubes = cubef * rI * mc;
       }
@@ -2082,7 +2082,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   const bool w0 = X.t == 0;
   STAMP_DECL
   State<R> s;
-  load_state<R>(s, B.st, B.n, e);
+  load_state<R>(s, st_of<R>(B), B.n, e);
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
@@ -2123,7 +2123,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   const double pot_old = B.pot[e];
-  const float z0_old = B.z0[e];
+  const float z0_old = z0_of<R>(B)[e];
   float obs[R::OBS];
   PackOut po;
   double pot_new = 0.0;
@@ -2202,7 +2202,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     reset_env_epi<R, 4>(B, e, s, nullptr, obs, has_floor, pot, z0, epi, fl, R::harder ? &hb : nullptr, X.t);
     if (w0) {
       B.pot[e] = pot;
-      B.z0[e] = z0;
+      z0_of<R>(B)[e] = z0;
       B.elapsed[e] = 0;
       B.flags[e] = has_floor ? 1u : 0u;
     }
@@ -2215,7 +2215,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     store_flag<R>(B, e, fl);
     if constexpr (R::harder) store_harder<R>(B, e, hb);
   }
-  gang_store<R, T>(s, obs, B.st, B.n, io.obs, e, X.t);
+  gang_store<R, T>(s, obs, st_of<R>(B), B.n, io.obs, e, X.t);
   STAMP(9)
   STAMP_FLUSH
 }

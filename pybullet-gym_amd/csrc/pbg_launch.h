@@ -24,6 +24,7 @@ struct Geometry {
   size_t scratch_words_per_env;
   int vgprs;          // the selected step kernel's registers per lane (hipFuncGetAttributes)
   int scratch_bytes;  // and its private segment per lane
+  int word_bytes = 4; // bytes per constraint-row / workspace word: 4 (float32 kernels) or 8 (float64)
 };
 
 #define PBG_DECLARE_ROBOT(NAME)                                                                            \
@@ -33,7 +34,12 @@ struct Geometry {
   int launch_get_state_##NAME(const Buffers& B, double* phys, double* aux, hipStream_t s);                 \
   int launch_set_state_##NAME(const Buffers& B, const double* phys, const double* aux, hipStream_t s);     \
   int launch_pack_##NAME(int n, const double* in, double* out, hipStream_t s);                              \
-  int debug_stamps_##NAME(unsigned long long* host_out);
+  int debug_stamps_##NAME(unsigned long long* host_out);                                                   \
+  int plan64_##NAME(int n_envs, int cus, int mode, Geometry* g);                                             \
+  int launch_step64_##NAME(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s); \
+  int launch_reset64_##NAME(const Buffers& B, const ResetIO& io, hipStream_t s);                           \
+  int launch_get_state64_##NAME(const Buffers& B, double* phys, double* aux, hipStream_t s);               \
+  int launch_set_state64_##NAME(const Buffers& B, const double* phys, const double* aux, hipStream_t s);
 
 PBG_DECLARE_ROBOT(Pendulum)
 PBG_DECLARE_ROBOT(Hopper)

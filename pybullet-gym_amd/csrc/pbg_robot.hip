@@ -184,14 +184,16 @@ static int plan_lane(int n_envs, int cus, Geometry* g) {
     const int wpc = (wgs + cus - 1) / cus;
     const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
     using RW = Rows<RR, 64>;
-    long words = (long)(budget / ((size_t)b * sizeof(float))) - RW::NC - RW::LIMW;
+    constexpr size_t WB = sizeof(real_t<RR>);  // LDS word: float, or double on the float64 path
+    long words = (long)(budget / ((size_t)b * WB)) - RW::NC - RW::LIMW;
     int cap = (int)(words / RW::W);
     if (cap > RW::MR) cap = RW::MR;
     if (cap < 0) cap = 0;
     g->block = b;
     g->lds_rows = cap;
-    g->lds_bytes = (size_t)b * sizeof(float) * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
+    g->lds_bytes = (size_t)b * WB * ((size_t)RW::LIMW + (size_t)cap * RW::W + RW::NC);
     g->scratch_words_per_env = RW::WORDS;
+    g->word_bytes = (int)WB;
     const void* fn = b == 64 ? (const void*)step_kernel<RR, 64> : (b == 32 ? (const void*)step_kernel<RR, 32> : (const void*)step_kernel<RR, 16>);
     const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
     return e ? e : kernel_attrs(fn, g);
@@ -246,6 +248,30 @@ int PBG_FN(launch_set_state_)(const Buffers& B, const double* phys, const double
 
 int PBG_FN(launch_pack_)(int n, const double* in, double* out, hipStream_t s) {
   hipLaunchKernelGGL(pack_kernel<R>, dim3(blocks(n, 64)), dim3(64), 0, s, n, in, out);
+  return (int)hipGetLastError();
+}
+
+// ---- the reference-precision path (pbg_create_v2 precision 64): float64 physics state and
+// arithmetic (pybullet's btScalar, scene_bases.py:75-76), the lane-per-env kernel of every robot
+// with at most 128 floor-contact slots (Atlas: PBG_E_HIP at create)
+using R64 = F64<R>;
+int PBG_FN(plan64_)(int n_envs, int cus, int mode, Geometry* g) {
+  (void)mode;
+  return plan_lane<R64>(n_envs, cus, g);
+}
+int PBG_FN(launch_step64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  return launch_lane<R64>(B, io, scratch, g, s);
+}
+int PBG_FN(launch_reset64_)(const Buffers& B, const ResetIO& io, hipStream_t s) {
+  hipLaunchKernelGGL(reset_kernel<R64>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, io);
+  return (int)hipGetLastError();
+}
+int PBG_FN(launch_get_state64_)(const Buffers& B, double* phys, double* aux, hipStream_t s) {
+  hipLaunchKernelGGL(get_state_kernel<R64>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, phys, aux);
+  return (int)hipGetLastError();
+}
+int PBG_FN(launch_set_state64_)(const Buffers& B, const double* phys, const double* aux, hipStream_t s) {
+  hipLaunchKernelGGL(set_state_kernel<R64>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, phys, aux);
   return (int)hipGetLastError();
 }
 

@@ -237,16 +237,38 @@ struct Dims {
 
 // ------------------------------------------------------------------ state record in registers
 // HumanoidFlagrunHarder's cube: a second free body (words after the robot's, sim_params.h)
+template <class T>
 struct CubeState {
-  float p[3], q[4], v[3], w[3];
+  T p[3], q[4], v[3], w[3];
 };
 struct NoCube {};
 template <class R>
 struct State {
-  float bp[3], bq[4], bv[3], bw[3];
-  float q[R::NJ > 0 ? R::NJ : 1], qd[R::NJ > 0 ? R::NJ : 1];
-  std::conditional_t<(R::harder != 0), CubeState, NoCube> cube;
+  using T = real_t<R>;
+  T bp[3], bq[4], bv[3], bw[3];
+  T q[R::NJ > 0 ? R::NJ : 1], qd[R::NJ > 0 ? R::NJ : 1];
+  std::conditional_t<(R::harder != 0), CubeState<T>, NoCube> cube;
 };
+
+// The handle's state / initial_z buffers and scene in R's precision (pbg_types.h real_t)
+template <class R>
+PBG_DEV real_t<R>* st_of(const Buffers& B) { return static_cast<real_t<R>*>(B.st); }
+template <class R>
+PBG_DEV real_t<R>* z0_of(const Buffers& B) { return static_cast<real_t<R>*>(B.z0); }
+template <class R>
+PBG_DEV const SimPT<real_t<R>>& sp_of(const Buffers& B) {
+  if constexpr (std::is_same<real_t<R>, double>::value) return B.sp64;
+  else return B.sp;
+}
+// precision-generic libm pieces (float: the f-suffixed calls the float32 kernels always made)
+PBG_DEV float tabs(float x) { return fabsf(x); }
+PBG_DEV double tabs(double x) { return fabs(x); }
+PBG_DEV float tmin(float a, float b) { return fminf(a, b); }
+PBG_DEV double tmin(double a, double b) { return fmin(a, b); }
+PBG_DEV float tmax(float a, float b) { return fmaxf(a, b); }
+PBG_DEV double tmax(double a, double b) { return fmax(a, b); }
+PBG_DEV float tsqrt(float x) { return sqrtf(x); }
+PBG_DEV double tsqrt(double x) { return sqrt(x); }
 
 // XCD-aware block order for the step kernels: the dispatcher deals workgroups round-robin over the
 // 8 XCDs (workgroup b -> XCD b % 8), each with its own L2, so consecutive env blocks -- which share
@@ -260,7 +282,7 @@ PBG_DEV int xcd_block() {
 }
 
 template <class R>
-PBG_DEV void load_state(State<R>& s, const float* __restrict__ st, int n, int e) {
+PBG_DEV void load_state(State<R>& s, const real_t<R>* __restrict__ st, int n, int e) {
 #pragma unroll
   for (int i = 0; i < 3; i++) s.bp[i] = st[(size_t)i * n + e];
 #pragma unroll
@@ -286,7 +308,7 @@ PBG_DEV void load_state(State<R>& s, const float* __restrict__ st, int n, int e)
   }
 }
 template <class R>
-PBG_DEV void store_state(const State<R>& s, float* __restrict__ st, int n, int e) {
+PBG_DEV void store_state(const State<R>& s, real_t<R>* __restrict__ st, int n, int e) {
 #pragma unroll
   for (int i = 0; i < 3; i++) st[(size_t)i * n + e] = s.bp[i];
 #pragma unroll
@@ -335,16 +357,17 @@ PBG_DEV void lanes_store_row(const float (&obs)[R::OBS], float* __restrict__ out
 // load snapshot (gym_locomotion_envs.py:23-25 restoreState) + reset noise on reset dofs
 template <class R>
 PBG_DEV void snapshot_state(State<R>& s) {
+  using T = real_t<R>;
 #pragma unroll
-  for (int i = 0; i < 3; i++) s.bp[i] = (float)R::base_pos[i];
+  for (int i = 0; i < 3; i++) s.bp[i] = (T)R::base_pos[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) s.bq[i] = (float)R::base_quat[i];
+  for (int i = 0; i < 4; i++) s.bq[i] = (T)R::base_quat[i];
 #pragma unroll
   for (int i = 0; i < 3; i++) { s.bv[i] = 0.f; s.bw[i] = 0.f; }
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) { s.q[d] = 0.f; s.qd[d] = 0.f; }
   if constexpr (R::harder) {  // restoreState + resetBasePositionAndOrientation(cube, (-1.5, 0, 0.05)) (:241)
-    s.cube.p[0] = (float)PBG_CUBE_X0; s.cube.p[1] = (float)PBG_CUBE_Y0; s.cube.p[2] = (float)PBG_CUBE_Z0;
+    s.cube.p[0] = (T)PBG_CUBE_X0; s.cube.p[1] = (T)PBG_CUBE_Y0; s.cube.p[2] = (T)PBG_CUBE_Z0;
     s.cube.q[0] = 0.f; s.cube.q[1] = 0.f; s.cube.q[2] = 0.f; s.cube.q[3] = 1.f;
 #pragma unroll
     for (int i = 0; i < 3; i++) { s.cube.v[i] = 0.f; s.cube.w[i] = 0.f; }
@@ -355,29 +378,32 @@ PBG_DEV void snapshot_state(State<R>& s) {
 template <class R>
 struct Kin {
   static constexpr int NB = R::NL + 1;
-  m3 Rm[NB];
-  f3 x[NB], c[NB];
+  M3<real_t<R>> Rm[NB];
+  V3<real_t<R>> x[NB], c[NB];
 };
 template <class R>
 struct KinVel {
   static constexpr int NB = R::NL + 1;
-  f3 w[NB], v[NB], al[NB], ac[NB];
+  V3<real_t<R>> w[NB], v[NB], al[NB], ac[NB];
 };
 
 // Forward kinematics (positions; optionally the world axis / anchor of every joint dof).
 template <class R, bool AXES = false>
-PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, f3* ja = nullptr, f3* jo = nullptr) {
+PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, V3<real_t<R>>* ja = nullptr, V3<real_t<R>>* jo = nullptr) {
+  using T = real_t<R>;
+  using f3 = V3<T>;
+  using m3 = M3<T>;
   k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
-  k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  k.x[0] = mk3<T>(s.bp[0], s.bp[1], s.bp[2]);
   k.c[0] = k.x[0];
   static_for<0, R::NL>([&](auto l_c) {
     constexpr int l = decltype(l_c)::value;
     constexpr int p = R::link_parent[l] + 1;
-    const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+    const m3 Ro = quat_to_m3c<T>(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
     const m3 R0 = mulc(k.Rm[p], Ro);
-    const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
-    const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
-    const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
+    const f3 x0 = k.x[p] + mulc(k.Rm[p], (T)R::link_offset_pos[l][0], (T)R::link_offset_pos[l][1], (T)R::link_offset_pos[l][2]);
+    const f3 axl = mk3<T>((T)R::link_axis[l][0], (T)R::link_axis[l][1], (T)R::link_axis[l][2]);
+    const f3 anl = mk3<T>((T)R::link_anchor[l][0], (T)R::link_anchor[l][1], (T)R::link_anchor[l][2]);
     constexpr int jt = R::link_jtype[l], d = R::link_dof[l];
     if constexpr (jt == 0) {
       const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
@@ -392,7 +418,7 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, f3* ja = nullptr, f3* jo = nul
       k.Rm[l + 1] = R0;
       k.x[l + 1] = x0;
     }
-    k.c[l + 1] = k.x[l + 1] + mulc(k.Rm[l + 1], (float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]);
+    k.c[l + 1] = k.x[l + 1] + mulc(k.Rm[l + 1], (T)R::link_com[l][0], (T)R::link_com[l][1], (T)R::link_com[l][2]);
   });
 }
 
@@ -420,24 +446,28 @@ PBG_DEV State<R> opaque_positions(const State<R>& s) {
 // the LDS capacity (rare: many simultaneous contacts) go to a device workspace laid out
 // [word][env] (coalesced).
 typedef __attribute__((address_space(3))) float lds_float;  // explicit LDS pointers
+typedef __attribute__((address_space(3))) double lds_double;
+template <class T>
+using lds_t = std::conditional_t<std::is_same<T, double>::value, lds_double, lds_float>;
 
 template <class R, int LS = 64>
 struct Rows {
   using D = Dims<R>;
+  using T = real_t<R>;
   static constexpr int N = D::NY, W = N + 3;  // contact row: y | meff | target | lambda (N: robot [+ cube])
   static constexpr int MR = 3 * D::NC > 0 ? 3 * D::NC : 1;
   static constexpr int NC = D::NC > 0 ? D::NC : 1;
   static constexpr int WORDS = MR * W;  // global workspace words per env
   static constexpr int ls = LS;  // LDS stride = lanes per workgroup
   static constexpr int LIMW = D::LIMW;
-  lds_float* lds;  // LDS base + lane
-  float* gbl;      // global workspace base + env
+  lds_t<T>* lds;   // LDS base + lane
+  T* gbl;          // global workspace base + env
   int n;       // global stride (envs)
   int cap;     // contact rows resident in LDS
-  PBG_DEV lds_float& lim(int w) const { return lds[(size_t)w * ls]; }
-  PBG_DEV lds_float& mu(int c) const { return lds[(size_t)(LIMW + cap * W + c) * ls]; }
+  PBG_DEV lds_t<T>& lim(int w) const { return lds[(size_t)w * ls]; }
+  PBG_DEV lds_t<T>& mu(int c) const { return lds[(size_t)(LIMW + cap * W + c) * ls]; }
   template <class P>
-  static PBG_DEV void put_at(P p, size_t st, const float* y, float meff, float target) {
+  static PBG_DEV void put_at(P p, size_t st, const T* y, T meff, T target) {
 #pragma unroll
     for (int i = 0; i < N; i++) p[i * st] = y[i];
     p[N * st] = meff;
@@ -445,31 +475,31 @@ struct Rows {
     p[(N + 2) * st] = 0.f;
   }
   template <class P>
-  static PBG_DEV void solve_at(P p, size_t st, float* u, float lo, float hi) {
-    float yv[N];
+  static PBG_DEV void solve_at(P p, size_t st, T* u, T lo, T hi) {
+    T yv[N];
 #pragma unroll
     for (int i = 0; i < N; i++) yv[i] = p[i * st];
-    const float meff = p[N * st], tgt = p[(N + 1) * st], lam0 = p[(N + 2) * st];
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial sums: shorter dependency chain
+    const T meff = p[N * st], tgt = p[(N + 1) * st], lam0 = p[(N + 2) * st];
+    T acc[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial sums: shorter dependency chain
 #pragma unroll
     for (int i = 0; i < N; i++) acc[i & 3] += yv[i] * u[i];
-    const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    const float nl = clampf(lam0 + meff * (tgt - yu), lo, hi);
-    const float dl = nl - lam0;
+    const T yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    const T nl = clampf(lam0 + meff * (tgt - yu), lo, hi);
+    const T dl = nl - lam0;
     p[(N + 2) * st] = nl;
 #pragma unroll
     for (int i = 0; i < N; i++) u[i] += yv[i] * dl;
   }
-  PBG_DEV void put(int r, const float* y, float meff, float target) const {
+  PBG_DEV void put(int r, const T* y, T meff, T target) const {
     if (r < cap) put_at(lds + (size_t)(LIMW + r * W) * ls, (size_t)ls, y, meff, target);
     else put_at(gbl + (size_t)r * W * n, (size_t)n, y, meff, target);
   }
-  PBG_DEV float lam(int r) const {
+  PBG_DEV T lam(int r) const {
     if (r < cap) return lds[(size_t)(LIMW + r * W + N + 2) * ls];
     return gbl[((size_t)r * W + N + 2) * n];
   }
   // one projected Gauss-Seidel update of contact row r in u-space, bounds [lo, hi]
-  PBG_DEV void solve(int r, float* u, float lo, float hi) const {
+  PBG_DEV void solve(int r, T* u, T lo, T hi) const {
     if (r < cap) solve_at(lds + (size_t)(LIMW + r * W) * ls, (size_t)ls, u, lo, hi);
     else solve_at(gbl + (size_t)r * W * n, (size_t)n, u, lo, hi);
   }
@@ -482,25 +512,29 @@ struct Rows {
 // a separated row admits an approach of at most pos/dt (speculative contact), a penetrating
 // one pushes out at erp * pos / dt.  Continuous at pos = 0.
 // k_pen / k_sep: the slopes -erp/dt and -1/dt of SimP (pbg_types.h), pre-formed on the host.
-PBG_DEV float pos_target(float pos, float k_pen, float k_sep) { return (pos > 0.f ? k_sep : k_pen) * pos; }
+template <class S>
+PBG_DEV S pos_target(S pos, nd<S> k_pen, nd<S> k_sep) { return (pos > S(0) ? k_sep : k_pen) * pos; }
 
 // tau: motor torque per joint dof, held over the env step.  slot_active: floor-slot flags
 // of this sub-step's collision pass (feet contacts come from the last sub-step).
 // dof motion vectors (angular, linear-at-O) in generalized order
 template <class R>
-PBG_DEV void motion_vectors(const f3* ja, const f3* jo, f3 O, f3* sw, f3* sv) {
+PBG_DEV void motion_vectors(const V3<real_t<R>>* ja, const V3<real_t<R>>* jo, V3<real_t<R>> O, V3<real_t<R>>* sw,
+                            V3<real_t<R>>* sv) {
   using D = Dims<R>;
+  using T = real_t<R>;
+  using f3 = V3<T>;
 #pragma unroll
   for (int gi = 0; gi < R::NDOF; gi++) {
     const int d = D::dof_of(gi);
     if (d >= 0) {
       if (R::dof_jtype[d] == 0) { sw[gi] = ja[d]; sv[gi] = cross3(jo[d] - O, ja[d]); }
-      else { sw[gi] = mk3(0, 0, 0); sv[gi] = ja[d]; }
+      else { sw[gi] = mk3<T>(0, 0, 0); sv[gi] = ja[d]; }
     } else {
       const int kk = gi - R::NJ;  // 0..2 linear, 3..5 angular
-      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
-      if (kk < 3) { sw[gi] = mk3(0, 0, 0); sv[gi] = e; }
-      else { sw[gi] = e; sv[gi] = mk3(0, 0, 0); }
+      const f3 e = mk3<T>(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
+      if (kk < 3) { sw[gi] = mk3<T>(0, 0, 0); sv[gi] = e; }
+      else { sw[gi] = e; sv[gi] = mk3<T>(0, 0, 0); }
     }
   }
 }
@@ -508,8 +542,9 @@ PBG_DEV void motion_vectors(const f3* ja, const f3* jo, f3 O, f3* sw, f3* sv) {
 // Link frames and dof motion vectors about the reference point O, recomputed from the
 // positions (cheaper than keeping phase A's copies live through the factorisation).
 template <class R>
-PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, f3* sw, f3* sv, f3& O) {
+PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, V3<real_t<R>>* sw, V3<real_t<R>>* sv, V3<real_t<R>>& O) {
   using D = Dims<R>;
+  using f3 = V3<real_t<R>>;
   constexpr int NJ = R::NJ;
   const State<R> sp = opaque_positions<R>(s);
   f3 ja2[NJ > 0 ? NJ : 1], jo2[NJ > 0 ? NJ : 1];
@@ -529,49 +564,54 @@ PBG_DEV void kin_motion(const State<R>& s, Kin<R>& k, f3* sw, f3* sv, f3& O) {
 // matrix and bias, its sparse Cholesky factor L (Ld = 1/diag), the predicted velocity
 // nu = clamp(nu + dt M^-1 (tau - C)) and u = L^T nu.  Shared by the lane and gang kernels.
 template <class R>
-PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs, const SimP& P SUB_STAMP_ARGS) {
+PBG_DEV void dyn_mass(const State<R>& s, const real_t<R>* tau, real_t<R>* L, real_t<R>* rhs,
+                      const SimPT<real_t<R>>& P SUB_STAMP_ARGS) {
   using D = Dims<R>;
+  using T = real_t<R>;
+  using f3 = V3<T>;
+  using m3 = M3<T>;
+  using s6 = S6<T>;
   constexpr int NJ = R::NJ, NB = D::NB, N = R::NDOF;
-  const float g = P.gravity;
+  const T g = P.gravity;
 
   // --- phase A: one forward pass over the bodies: kinematics, velocities, bias
   // accelerations, and each body's inertia + wrench about the reference point O added
   // straight into the composites of its dof-owning ancestors.  No per-body array
   // survives the pass (register pressure); positions are recomputed for contacts.
   f3 ja[NJ > 0 ? NJ : 1], jo[NJ > 0 ? NJ : 1];
-  float cm[NB];
+  T cm[NB];
   f3 cp1[NB], cF[NB], cN[NB];
   s6 cJ[NB];
   static_for<0, NB>([&](auto b_c) {
     constexpr int b = decltype(b_c)::value;
     if constexpr (D::is_owner(b)) {
-      cm[b] = 0.f; cp1[b] = mk3(0, 0, 0); cF[b] = mk3(0, 0, 0); cN[b] = mk3(0, 0, 0);
+      cm[b] = 0.f; cp1[b] = mk3<T>(0, 0, 0); cF[b] = mk3<T>(0, 0, 0); cN[b] = mk3<T>(0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 6; i++) cJ[b].a[i] = 0.f;
     }
   });
-  f3 O = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  f3 O = mk3<T>(s.bp[0], s.bp[1], s.bp[2]);
   {
     Kin<R> k;
     f3 w[NB], v[NB], al[NB], ac[NB];
     k.Rm[0] = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
-    k.x[0] = mk3(s.bp[0], s.bp[1], s.bp[2]);
+    k.x[0] = mk3<T>(s.bp[0], s.bp[1], s.bp[2]);
     k.c[0] = k.x[0];
-    w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
-    v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
-    al[0] = mk3(0, 0, 0);
-    ac[0] = mk3(0, 0, 0);
+    w[0] = R::floating ? mk3<T>(s.bw[0], s.bw[1], s.bw[2]) : mk3<T>(0, 0, 0);
+    v[0] = R::floating ? mk3<T>(s.bv[0], s.bv[1], s.bv[2]) : mk3<T>(0, 0, 0);
+    al[0] = mk3<T>(0, 0, 0);
+    ac[0] = mk3<T>(0, 0, 0);
     static_for<0, NB>([&](auto b_c) {
       constexpr int b = decltype(b_c)::value;
       if constexpr (b > 0) {
         constexpr int l = b - 1;
         constexpr int p = R::link_parent[l] + 1;
         constexpr int jt = R::link_jtype[l], d = R::link_dof[l];
-        const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+        const m3 Ro = quat_to_m3c<T>(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
         const m3 R0 = mulc(k.Rm[p], Ro);
-        const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
-        const f3 axl = mk3((float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
-        const f3 anl = mk3((float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
+        const f3 x0 = k.x[p] + mulc(k.Rm[p], (T)R::link_offset_pos[l][0], (T)R::link_offset_pos[l][1], (T)R::link_offset_pos[l][2]);
+        const f3 axl = mk3<T>((T)R::link_axis[l][0], (T)R::link_axis[l][1], (T)R::link_axis[l][2]);
+        const f3 anl = mk3<T>((T)R::link_anchor[l][0], (T)R::link_anchor[l][1], (T)R::link_anchor[l][2]);
         if constexpr (jt == 0) {
           const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
           k.Rm[b] = mul(R0, Rj);
@@ -583,7 +623,7 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
           k.Rm[b] = R0;
           k.x[b] = x0;
         }
-        k.c[b] = k.x[b] + mulc(k.Rm[b], (float)R::link_com[l][0], (float)R::link_com[l][1], (float)R::link_com[l][2]);
+        k.c[b] = k.x[b] + mulc(k.Rm[b], (T)R::link_com[l][0], (T)R::link_com[l][1], (T)R::link_com[l][2]);
         const f3 cp = k.c[p], wp = w[p], vp = v[p], alp = al[p], acp = ac[p];
         const f3 c = k.c[b];
         if constexpr (jt == 0 || jt == 1) {
@@ -608,7 +648,7 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
             w[b] = wp;
             al[b] = alp;
             v[b] = vp + cross3(wp, r) + s.qd[d] * a;
-            ac[b] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (2.f * s.qd[d]) * cross3(wp, a);
+            ac[b] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r)) + (T(2) * s.qd[d]) * cross3(wp, a);
           }
         } else {
           const f3 r = c - cp;
@@ -620,11 +660,11 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
       }
       if (b == D::REF_BODY) O = k.c[b];
       if constexpr (D::body_mass(b) > 0.0) {
-        const float m = (float)D::body_mass(b);
+        const T m = (T)D::body_mass(b);
         constexpr typename D::Inertia6 I6 = D::template inertia<b>();
         const s6 Iw = rotate_inertia(k.Rm[b], I6.v);
         const f3 r = k.c[b] - O;
-        const float rr = dot3(r, r);
+        const T rr = dot3(r, r);
         s6 J;
         J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
         J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
@@ -633,10 +673,10 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
         J.a[4] = Iw.a[4] - m * r.x * r.z;
         J.a[5] = Iw.a[5] - m * r.y * r.z;
         const f3 Iww = mul(Iw, w[b]);
-        const f3 f = m * (ac[b] - mk3(0, 0, -g)) +
-                     (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[b]))) * v[b];
+        const f3 f = m * (ac[b] - mk3<T>(0, 0, -g)) +
+                     (m * ((T)PBG_LINEAR_DAMPING + (T)PBG_LINEAR_DAMPING * norm3(v[b]))) * v[b];
         const f3 n = mul(Iw, al[b]) + cross3(w[b], Iww) +
-                     ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
+                     ((T)PBG_ANGULAR_DAMPING + (T)PBG_ANGULAR_DAMPING * norm3(w[b])) * Iww;
         const f3 pr = m * r, Nn = n + cross3(r, f);
         static_for<0, NB>([&](auto a_c) {
           constexpr int a = decltype(a_c)::value;
@@ -682,10 +722,10 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
   // joint damping -d qd and springs -k q (mjcf.py B6 / B7), explicit from this sub-step's state
   static_for<0, NJ>([&](auto d_c) {
     constexpr int d = decltype(d_c)::value;
-    L[D::lidx(D::gj(d), D::gj(d))] += (float)R::dof_armature[d];
-    float r = tau[d];
-    if constexpr (R::dof_damping[d] != 0.0) r -= (float)R::dof_damping[d] * s.qd[d];
-    if constexpr (R::dof_stiffness[d] != 0.0) r -= (float)R::dof_stiffness[d] * s.q[d];
+    L[D::lidx(D::gj(d), D::gj(d))] += (T)R::dof_armature[d];
+    T r = tau[d];
+    if constexpr (R::dof_damping[d] != 0.0) r -= (T)R::dof_damping[d] * s.qd[d];
+    if constexpr (R::dof_stiffness[d] != 0.0) r -= (T)R::dof_stiffness[d] * s.q[d];
     rhs[D::gj(d)] += r;
   });
   STAMP(1)
@@ -694,24 +734,26 @@ PBG_DEV void dyn_mass(const State<R>& s, const float* tau, float* L, float* rhs,
 // Cholesky of the mass matrix held in L (in place, no fill-in in leaf-first order; Ld =
 // 1 / diag(L)), nu = clamp(nu + dt M^-1 rhs), u = L^T nu.
 template <class R>
-PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld, float* nu, float* u, const SimP& P) {
+PBG_DEV void dyn_solve(const State<R>& s, real_t<R>* L, const real_t<R>* rhs, real_t<R>* Ld, real_t<R>* nu, real_t<R>* u,
+                       const SimPT<real_t<R>>& P) {
   using D = Dims<R>;
+  using T = real_t<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
-  const float dt = P.dt;
+  const T dt = P.dt;
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    float sjj = L[D::lidx(j, j)];
+    T sjj = L[D::lidx(j, j)];
 #pragma unroll
     for (int kk = 0; kk < j; kk++)
       if (D::coupled(j, kk)) sjj -= L[D::lidx(j, kk)] * L[D::lidx(j, kk)];
-    const float ljj = fast_sqrt(sjj);
-    const float inv = fast_rcp(ljj);
+    const T ljj = fast_sqrt(sjj);
+    const T inv = fast_rcp(ljj);
     Ld[j] = inv;
     L[D::lidx(j, j)] = ljj;
 #pragma unroll
     for (int i = j + 1; i < N; i++) {
       if (!D::coupled(i, j)) continue;
-      float t = L[D::lidx(i, j)];
+      T t = L[D::lidx(i, j)];
 #pragma unroll
       for (int kk = 0; kk < j; kk++)
         if (D::coupled(i, kk) && D::coupled(j, kk)) t -= L[D::lidx(i, kk)] * L[D::lidx(j, kk)];
@@ -726,19 +768,19 @@ PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld,
 #pragma unroll
     for (int i = 0; i < 3; i++) { nu[NJ + i] = s.bv[i]; nu[NJ + 3 + i] = s.bw[i]; }
   }
-  float yv[N];
+  T yv[N];
 #pragma unroll
   for (int i = 0; i < N; i++) {  // forward: L y = rhs
-    float t = rhs[i];
+    T t = rhs[i];
 #pragma unroll
     for (int kk = 0; kk < i; kk++)
       if (D::coupled(i, kk)) t -= L[D::lidx(i, kk)] * yv[kk];
     yv[i] = t * Ld[i];
   }
-  float qdd[N];
+  T qdd[N];
 #pragma unroll
   for (int i = N - 1; i >= 0; i--) {  // backward: L^T x = y
-    float t = yv[i];
+    T t = yv[i];
 #pragma unroll
     for (int kk = i + 1; kk < N; kk++)
       if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * qdd[kk];
@@ -747,12 +789,12 @@ PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld,
   // u = L^T nu_pred
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    float t = nu[i] + dt * qdd[i];
-    nu[i] = clampf(t, -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    T t = nu[i] + dt * qdd[i];
+    nu[i] = clampf(t, -(T)PBG_MAX_COORD_VELOCITY, (T)PBG_MAX_COORD_VELOCITY);
   }
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    float t = 0.f;
+    T t = 0.f;
 #pragma unroll
     for (int kk = i; kk < N; kk++)
       if (D::coupled(kk, i)) t += L[D::lidx(kk, i)] * nu[kk];
@@ -761,30 +803,31 @@ PBG_DEV void dyn_solve(const State<R>& s, float* L, const float* rhs, float* Ld,
 }
 
 template <class R>
-PBG_DEV void dynamics(const State<R>& s, const float* tau, float* L, float* Ld, float* nu, float* u,
-                      const SimP& P SUB_STAMP_ARGS) {
-  float rhs[R::NDOF];
+PBG_DEV void dynamics(const State<R>& s, const real_t<R>* tau, real_t<R>* L, real_t<R>* Ld, real_t<R>* nu, real_t<R>* u,
+                      const SimPT<real_t<R>>& P SUB_STAMP_ARGS) {
+  real_t<R> rhs[R::NDOF];
   dyn_mass<R>(s, tau, L, rhs, P SUB_STAMP_PASS);
   dyn_solve<R>(s, L, rhs, Ld, nu, u, P);
 }
 
 // exponential-map quaternion update of a free body (the floating base, the cube) with its
 // world angular velocity  [EXT] btMultiBody pQuatUpdateFun
-PBG_DEV void free_body_quat(float* q, f3 wv, const SimP& P) {
-  const float dt = P.dt;
-  float ang = norm3(wv);
-  if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
-  float sh, dw;
-  sincos_fast(0.5f * ang * dt, &sh, &dw);
-  f3 ax;
-  if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
+template <class S>
+PBG_DEV void free_body_quat(S* q, V3<S> wv, const SimPT<S>& P) {
+  const S dt = P.dt;
+  S ang = norm3(wv);
+  if (ang * dt > (S)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
+  S sh, dw;
+  sincos_fast(S(0.5f) * ang * dt, &sh, &dw);
+  V3<S> ax;
+  if (ang < S(0.001)) ax = (S(0.5f) * dt - P.dt3c * ang * ang) * wv;
   else ax = (sh / ang) * wv;
-  const float x = q[0], y = q[1], z = q[2], ww = q[3];
-  const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
-  const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
-  const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
-  const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-  const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+  const S x = q[0], y = q[1], z = q[2], ww = q[3];
+  const S nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+  const S ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+  const S nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+  const S nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+  const S inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
   q[0] = nx * inv; q[1] = ny * inv; q[2] = nz * inv; q[3] = nw * inv;
 }
 
@@ -793,23 +836,27 @@ PBG_DEV void free_body_quat(float* q, f3 wv, const SimP& P) {
 // plain scalings.  Unconstrained velocity: the free-body bias of the oracle's mass_and_bias
 // (f = m (-g) + m (k1 + k2 |v|) v, tq = (k1 + k2 |w|) I w; the gyroscopic term of an isotropic
 // body vanishes), nu_c = clamp(nu_c - dt M_c^-1 (f, tq)), then u_c.
+template <class S>
 struct CubeK {
-  static PBG_DEV float sm() { return sqrtf((float)PBG_CUBE_MASS); }
-  static PBG_DEV float sI() { return sqrtf((float)PBG_CUBE_INERTIA); }
+  static PBG_DEV S sm() { return tsqrt((S)PBG_CUBE_MASS); }
+  static PBG_DEV S sI() { return tsqrt((S)PBG_CUBE_INERTIA); }
 };
 template <class R>
-PBG_DEV void cube_unconstrained(const State<R>& s, float* uc, const SimP& P) {
+PBG_DEV void cube_unconstrained(const State<R>& s, real_t<R>* uc, const SimPT<real_t<R>>& P) {
+  using T = real_t<R>;
+  using f3 = V3<T>;
+  using CK = CubeK<T>;
   if constexpr (R::harder) {
-    const f3 v = mk3(s.cube.v[0], s.cube.v[1], s.cube.v[2]), w = mk3(s.cube.w[0], s.cube.w[1], s.cube.w[2]);
-    const float kl = (float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v);
-    const float ka = (float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w);
-    const float vmax = (float)PBG_MAX_COORD_VELOCITY;
-    const float vv[3] = {v.x, v.y, v.z}, wv[3] = {w.x, w.y, w.z};
+    const f3 v = mk3<T>(s.cube.v[0], s.cube.v[1], s.cube.v[2]), w = mk3<T>(s.cube.w[0], s.cube.w[1], s.cube.w[2]);
+    const T kl = (T)PBG_LINEAR_DAMPING + (T)PBG_LINEAR_DAMPING * norm3(v);
+    const T ka = (T)PBG_ANGULAR_DAMPING + (T)PBG_ANGULAR_DAMPING * norm3(w);
+    const T vmax = (T)PBG_MAX_COORD_VELOCITY;
+    const T vv[3] = {v.x, v.y, v.z}, wv[3] = {w.x, w.y, w.z};
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-      const float acc = -(kl * vv[i]) - (i == 2 ? P.gravity : 0.f);
-      uc[i] = CubeK::sm() * clampf(vv[i] + P.dt * acc, -vmax, vmax);
-      uc[3 + i] = CubeK::sI() * clampf(wv[i] + P.dt * (-(ka * wv[i])), -vmax, vmax);
+      const T acc = -(kl * vv[i]) - (i == 2 ? P.gravity : T(0));
+      uc[i] = CK::sm() * clampf(vv[i] + P.dt * acc, -vmax, vmax);
+      uc[3 + i] = CK::sI() * clampf(wv[i] + P.dt * (-(ka * wv[i])), -vmax, vmax);
     }
   } else {
     (void)s; (void)uc; (void)P;
@@ -817,45 +864,50 @@ PBG_DEV void cube_unconstrained(const State<R>& s, float* uc, const SimP& P) {
 }
 // nu_c = L_c^-T u_c, clamp, semi-implicit Euler
 template <class R>
-PBG_DEV void cube_integrate(State<R>& s, const float* uc, const SimP& P) {
+PBG_DEV void cube_integrate(State<R>& s, const real_t<R>* uc, const SimPT<real_t<R>>& P) {
+  using T = real_t<R>;
+  using CK = CubeK<T>;
   if constexpr (R::harder) {
-    const float vmax = (float)PBG_MAX_COORD_VELOCITY;
-    const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+    const T vmax = (T)PBG_MAX_COORD_VELOCITY;
+    const T rm = T(1) / CK::sm(), rI = T(1) / CK::sI();
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       s.cube.v[i] = clampf(uc[i] * rm, -vmax, vmax);
       s.cube.w[i] = clampf(uc[3 + i] * rI, -vmax, vmax);
       s.cube.p[i] += P.dt * s.cube.v[i];
     }
-    free_body_quat(s.cube.q, mk3(s.cube.w[0], s.cube.w[1], s.cube.w[2]), P);
+    free_body_quat(s.cube.q, mk3<T>(s.cube.w[0], s.cube.w[1], s.cube.w[2]), P);
   } else {
     (void)s; (void)uc; (void)P;
   }
 }
 // signed distance of a cube-local point to the box of half extent h (oracle box_sd)
-PBG_DEV float box_sd(f3 p, float h) {
-  const float qx = fabsf(p.x) - h, qy = fabsf(p.y) - h, qz = fabsf(p.z) - h;
-  const float ox = fmaxf(qx, 0.f), oy = fmaxf(qy, 0.f), oz = fmaxf(qz, 0.f);
-  return sqrtf(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.f);
+template <class S>
+PBG_DEV S box_sd(V3<S> p, S h) {
+  const S qx = tabs(p.x) - h, qy = tabs(p.y) - h, qz = tabs(p.z) - h;
+  const S ox = tmax(qx, S(0)), oy = tmax(qy, S(0)), oz = tmax(qz, S(0));
+  return tsqrt(ox * ox + oy * oy + oz * oz) + tmin(tmax(qx, tmax(qy, qz)), S(0));
 }
 
 // nu = L^-T u, clamp, semi-implicit Euler (exponential-map base rotation).  nu: scratch.
 template <class R>
-PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float* u, float* nu, const SimP& P) {
+PBG_DEV void integrate(State<R>& s, const real_t<R>* L, const real_t<R>* Ld, const real_t<R>* u, real_t<R>* nu,
+                       const SimPT<real_t<R>>& P) {
   using D = Dims<R>;
+  using T = real_t<R>;
   constexpr int NJ = R::NJ, N = R::NDOF;
-  const float dt = P.dt;
+  const T dt = P.dt;
   // --- back to nu = L^-T u; clamp; integrate positions ----------------------------------
 #pragma unroll
   for (int i = N - 1; i >= 0; i--) {
-    float t = u[i];
+    T t = u[i];
 #pragma unroll
     for (int kk = i + 1; kk < N; kk++)
       if (D::coupled(kk, i)) t -= L[D::lidx(kk, i)] * nu[kk];
     nu[i] = t * Ld[i];
   }
 #pragma unroll
-  for (int i = 0; i < N; i++) nu[i] = clampf(nu[i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+  for (int i = 0; i < N; i++) nu[i] = clampf(nu[i], -(T)PBG_MAX_COORD_VELOCITY, (T)PBG_MAX_COORD_VELOCITY);
 #pragma unroll
   for (int d = 0; d < NJ; d++) {
     s.qd[d] = nu[D::gj(d)];
@@ -868,7 +920,7 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
       s.bw[i] = nu[NJ + 3 + i];
       s.bp[i] += dt * s.bv[i];
     }
-    free_body_quat(s.bq, mk3(s.bw[0], s.bw[1], s.bw[2]), P);
+    free_body_quat(s.bq, mk3<T>(s.bw[0], s.bw[1], s.bw[2]), P);
   }
 }
 
@@ -880,37 +932,42 @@ PBG_DEV void integrate(State<R>& s, const float* L, const float* Ld, const float
 // for the self pairs, the cube part y_c = +-(n / sqrt m, (r x n) / sqrt I).  Returns nc.
 #define PBG_CUBE_GS_ITERS 24
 template <class R, int LS>
-PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const f3* sw, const f3* sv, f3 O, const float* L,
-                          const float* Ld, const Rows<R, LS>& rw, uint32_t sub, uint32_t& csig, const SimP& P, int nc) {
+PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const V3<real_t<R>>* sw, const V3<real_t<R>>* sv,
+                          V3<real_t<R>> O, const real_t<R>* L, const real_t<R>* Ld, const Rows<R, LS>& rw, uint32_t sub,
+                          uint32_t& csig, const SimPT<real_t<R>>& P, int nc) {
   using D = Dims<R>;
+  using T = real_t<R>;
+  using f3 = V3<T>;
+  using m3 = M3<T>;
+  using CK = CubeK<T>;
   constexpr int N = R::NDOF, NY = D::NY;
-  const float h = (float)PBG_CUBE_HALF, thr = (float)PBG_CONTACT_THRESHOLD;
-  const float rm = 1.f / CubeK::sm(), rI = 1.f / CubeK::sI();
+  const T h = (T)PBG_CUBE_HALF, thr = (T)PBG_CONTACT_THRESHOLD;
+  const T rm = T(1) / CK::sm(), rI = T(1) / CK::sI();
   const m3 Rc = quat_to_m3(s.cube.q[0], s.cube.q[1], s.cube.q[2], s.cube.q[3]);
-  const f3 xc = mk3(s.cube.p[0], s.cube.p[1], s.cube.p[2]);
+  const f3 xc = mk3<T>(s.cube.p[0], s.cube.p[1], s.cube.p[2]);
   // --- corners vs floor
   static_for<0, 8>([&](auto c_c) {
     constexpr int c = decltype(c_c)::value;
-    const f3 lc = mk3((c & 1) ? h : -h, (c & 2) ? h : -h, (c & 4) ? h : -h);
+    const f3 lc = mk3<T>((c & 1) ? h : -h, (c & 2) ? h : -h, (c & 4) ? h : -h);
     const f3 p = xc + mul(Rc, lc);
     if (!(p.z < thr)) return;
     csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + c));
     const f3 rc = p - xc;
 #pragma unroll
     for (int dir = 0; dir < 3; dir++) {
-      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 nd = dir == 0 ? mk3<T>(0, 0, 1) : (dir == 1 ? mk3<T>(0, -1, 0) : mk3<T>(1, 0, 0));
       const f3 mm = cross3(rc, nd);
-      float y[NY];
+      T y[NY];
 #pragma unroll
       for (int i = 0; i < N; i++) y[i] = 0.f;
       y[N] = nd.x * rm; y[N + 1] = nd.y * rm; y[N + 2] = nd.z * rm;
       y[N + 3] = mm.x * rI; y[N + 4] = mm.y * rI; y[N + 5] = mm.z * rI;
-      float D2 = 0.f;
+      T D2 = 0.f;
 #pragma unroll
       for (int i = N; i < NY; i++) D2 += y[i] * y[i];
-      rw.put(3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f, dir == 0 ? pos_target(p.z, P.k_contact, P.k_sep) : 0.f);
+      rw.put(3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(p.z, P.k_contact, P.k_sep) : T(0));
     }
-    rw.mu(nc) = (float)R::cube_floor_mu;
+    rw.mu(nc) = (T)R::cube_floor_mu;
     nc++;
   });
   // --- robot geoms vs the box
@@ -918,64 +975,64 @@ PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const f3* sw, cons
 #pragma unroll
   for (int g = 0; g < R::NCG; g++) {
     const int b = R::cgeom_link[g] + 1;
-    G0[g] = k.x[b] + mulc(k.Rm[b], (float)R::cgeom_p0[g][0], (float)R::cgeom_p0[g][1], (float)R::cgeom_p0[g][2]);
-    G1[g] = k.x[b] + mulc(k.Rm[b], (float)R::cgeom_p1[g][0], (float)R::cgeom_p1[g][1], (float)R::cgeom_p1[g][2]);
+    G0[g] = k.x[b] + mulc(k.Rm[b], (T)R::cgeom_p0[g][0], (T)R::cgeom_p0[g][1], (T)R::cgeom_p0[g][2]);
+    G1[g] = k.x[b] + mulc(k.Rm[b], (T)R::cgeom_p1[g][0], (T)R::cgeom_p1[g][1], (T)R::cgeom_p1[g][2]);
   }
   m3 Rt;
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++) Rt.m[3 * i + j] = Rc.m[3 * j + i];
-  const float bound = (float)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
+  const T bound = (T)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
 #pragma unroll 1
   for (int g = 0; g < R::NCG; g++) {
-    const float r = (float)R::cgeom_r[g];
+    const T r = (T)R::cgeom_r[g];
     const f3 p0 = mul(Rt, G0[g] - xc), p1 = mul(Rt, G1[g] - xc), d = p1 - p0;
-    const float dd = dot3(d, d);
-    const float t0 = dd > 1e-12f ? fminf(fmaxf(-dot3(p0, d) / dd, 0.f), 1.f) : 0.f;
+    const T dd = dot3(d, d);
+    const T t0 = dd > T(1e-12) ? tmin(tmax(-dot3(p0, d) / dd, T(0)), T(1)) : T(0);
     if (!(norm3(p0 + t0 * d) < bound + r + thr)) continue;
-    float t = 0.f;
-    if (dd > 1e-12f) {
-      const float phi = 0.6180339887498949f;
-      float a = 0.f, bb = 1.f;
-      float x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
-      float f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
+    T t = 0.f;
+    if (dd > T(1e-12)) {
+      const T phi = T(0.6180339887498949);
+      T a = 0.f, bb = 1.f;
+      T x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
+      T f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
 #pragma unroll 1
       for (int it = 0; it < PBG_CUBE_GS_ITERS; it++) {
         if (f1 <= f2) { bb = x2; x2 = x1; f2 = f1; x1 = bb - phi * (bb - a); f1 = box_sd(p0 + x1 * d, h); }
         else { a = x1; x1 = x2; f1 = f2; x2 = a + phi * (bb - a); f2 = box_sd(p0 + x2 * d, h); }
       }
-      t = 0.5f * (a + bb);
+      t = T(0.5f) * (a + bb);
     }
     const f3 ps = p0 + t * d;
-    const float dist = box_sd(ps, h) - r;
+    const T dist = box_sd(ps, h) - r;
     if (!(dist < thr)) continue;
     f3 nb, qb;
-    const float qx = fabsf(ps.x) - h, qy = fabsf(ps.y) - h, qz = fabsf(ps.z) - h;
-    if (fmaxf(qx, fmaxf(qy, qz)) > 0.f) {
-      qb = mk3(fminf(fmaxf(ps.x, -h), h), fminf(fmaxf(ps.y, -h), h), fminf(fmaxf(ps.z, -h), h));
+    const T qx = tabs(ps.x) - h, qy = tabs(ps.y) - h, qz = tabs(ps.z) - h;
+    if (tmax(qx, tmax(qy, qz)) > T(0)) {
+      qb = mk3<T>(tmin(tmax(ps.x, -h), h), tmin(tmax(ps.y, -h), h), tmin(tmax(ps.z, -h), h));
       const f3 dv = ps - qb;
-      const float l = norm3(dv);
-      nb = l > 1e-9f ? (1.f / l) * dv : mk3(0, 0, 1);
+      const T l = norm3(dv);
+      nb = l > T(1e-9) ? (T(1) / l) * dv : mk3<T>(0, 0, 1);
     } else {
       const int ax = (qx >= qy && qx >= qz) ? 0 : (qy >= qz ? 1 : 2);
-      const float cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
-      const float sg = cc < 0.f ? -1.f : 1.f;
-      nb = mk3(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
-      qb = mk3(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
+      const T cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
+      const T sg = cc < T(0) ? T(-1) : T(1);
+      nb = mk3<T>(ax == 0 ? sg : T(0), ax == 1 ? sg : T(0), ax == 2 ? sg : T(0));
+      qb = mk3<T>(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
     }
     csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + 8 + g));
     const f3 nrm = mul(Rc, nb);
     const f3 PA = xc + mul(Rc, ps) - r * nrm, PB = xc + mul(Rc, qb);
     f3 t1, t2;  // btPlaneSpace1(nrm)
-    if (fabsf(nrm.z) > 0.7071067811865476f) {
-      const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
-      t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
-      t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+    if (tabs(nrm.z) > T(0.7071067811865476)) {
+      const T a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
+      t1 = mk3<T>(0, -nrm.z * kinv, nrm.y * kinv);
+      t2 = mk3<T>(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
     } else {
-      const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
-      t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
-      t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+      const T a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
+      t1 = mk3<T>(-nrm.y * kinv, nrm.x * kinv, 0);
+      t2 = mk3<T>(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
     }
     const int lnk = R::cgeom_link[g];
     const uint32_t ma = lnk >= 0 ? R::link_chain_mask[lnk] : 0u;
@@ -984,13 +1041,13 @@ PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const f3* sw, cons
     for (int dir = 0; dir < 3; dir++) {
       const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
       const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
-      float y[NY];
-      float D2 = 0.f;
+      T y[NY];
+      T D2 = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) {
         const int di = D::dof_of(i);
         const bool inA = di < 0 || ((ma >> di) & 1u);
-        float tt = inA ? dot3(nd, sv[i]) + dot3(mA, sw[i]) : 0.f;
+        T tt = inA ? dot3(nd, sv[i]) + dot3(mA, sw[i]) : T(0);
 #pragma unroll
         for (int kk = 0; kk < i; kk++)
           if (D::coupled(i, kk)) tt -= L[D::lidx(i, kk)] * y[kk];
@@ -1001,22 +1058,24 @@ PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const f3* sw, cons
       y[N + 3] = -mB.x * rI; y[N + 4] = -mB.y * rI; y[N + 5] = -mB.z * rI;
 #pragma unroll
       for (int i = N; i < NY; i++) D2 += y[i] * y[i];
-      rw.put(3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f, dir == 0 ? pos_target(dist, P.k_contact, P.k_sep) : 0.f);
+      rw.put(3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(dist, P.k_contact, P.k_sep) : T(0));
     }
-    rw.mu(nc) = (float)R::cgeom_mu[g];
+    rw.mu(nc) = (T)R::cgeom_mu[g];
     nc++;
   }
   return nc;
 }
 
 template <class R, int LS>
-PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const Rows<R, LS>& rw, uint32_t sub,
-                    uint32_t& csig, const SimP& P SUB_STAMP_ARGS) {
+PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, const Rows<R, LS>& rw, uint32_t sub,
+                    uint32_t& csig, const SimPT<real_t<R>>& P SUB_STAMP_ARGS) {
   using D = Dims<R>;
+  using T = real_t<R>;
+  using f3 = V3<T>;
   constexpr int NJ = R::NJ, N = R::NDOF;
   constexpr int NY = D::NY;  // rows and u: the robot's N (+ HumanoidFlagrunHarder's cube 6)
-  float L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
-  float Ld[N], nu[N], u[NY];
+  T L[D::NNZ];  // coupled lower-triangle entries only (packed, compile-time indexed)
+  T Ld[N], nu[N], u[NY];
   dynamics<R>(s, tau, L, Ld, nu, u, P SUB_STAMP_PASS);
   cube_unconstrained<R>(s, u + N, P);
   f3 O;
@@ -1027,24 +1086,24 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     constexpr int d = D::LIM.v[li][0], np = D::LIM.v[li][1], off = D::LIM.v[li][2];
     constexpr int gd = D::gj(d);
     // y = L^-1 e_gd, non-zero only on the pattern (the dof, its ancestors, the base)
-    float y[N];
+    T y[N];
 #pragma unroll
     for (int i = 0; i < N; i++) {
       if (i < gd || !D::coupled(i, gd)) { y[i] = 0.f; continue; }
-      float t = i == gd ? 1.f : 0.f;
+      T t = i == gd ? 1.f : 0.f;
 #pragma unroll
       for (int kk = gd; kk < i; kk++)
         if (D::coupled(i, kk) && D::coupled(kk, gd)) t -= L[D::lidx(i, kk)] * y[kk];
       y[i] = t * Ld[i];
     }
-    float D2 = 0.f;
+    T D2 = 0.f;
 #pragma unroll
     for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
-    const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
+    const T meff = D2 > T(1e-12) ? fast_rcp(D2) : T(0);
     // lower row J = +e_d (pos = q - lo), upper row J = -e_d (pos = hi - q)
-    const float plo = s.q[d] - (float)R::dof_lower[d], phi = (float)R::dof_upper[d] - s.q[d];
-    const float tlo = pos_target(plo, P.k_limit, P.k_sep);
-    const float thi = pos_target(phi, P.k_limit, P.k_sep);
+    const T plo = s.q[d] - (T)R::dof_lower[d], phi = (T)R::dof_upper[d] - s.q[d];
+    const T tlo = pos_target(plo, P.k_limit, P.k_sep);
+    const T thi = pos_target(phi, P.k_limit, P.k_sep);
 #pragma unroll
     for (int i = 0; i < N; i++)
       if (D::LIMPOS.v[li][i] >= 0) rw.lim(off + D::LIMPOS.v[li][i]) = y[i];
@@ -1068,43 +1127,43 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
   static_for<0, R::NS>([&](auto sl_c) {
     constexpr int sl = decltype(sl_c)::value;
     constexpr int b = R::slot_link[sl] + 1;
-    const f3 cc = k.x[b] + mulc(k.Rm[b], (float)R::slot_point[sl][0], (float)R::slot_point[sl][1], (float)R::slot_point[sl][2]);
-    const float rad = (float)R::slot_radius[sl];
-    const float dist = cc.z - rad;
-    const bool act = dist < (float)PBG_CONTACT_THRESHOLD;
+    const f3 cc = k.x[b] + mulc(k.Rm[b], (T)R::slot_point[sl][0], (T)R::slot_point[sl][1], (T)R::slot_point[sl][2]);
+    const T rad = (T)R::slot_radius[sl];
+    const T dist = cc.z - rad;
+    const bool act = dist < (T)PBG_CONTACT_THRESHOLD;
     slot_active[sl] = act;
     if (!act) return;
     csig += pbg_contact_hash(sub, (uint32_t)sl);
-    const f3 cp = mk3(cc.x, cc.y, cc.z - rad);
+    const f3 cp = mk3<T>(cc.x, cc.y, cc.z - rad);
     const f3 rP = cp - O;
     const int lnk = R::slot_link[sl];
 #pragma unroll
     for (int dir = 0; dir < 3; dir++) {
       // n = +z, t1 = (0,-1,0), t2 = (1,0,0)  (btPlaneSpace1 of +z)
-      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 nd = dir == 0 ? mk3<T>(0, 0, 1) : (dir == 1 ? mk3<T>(0, -1, 0) : mk3<T>(1, 0, 0));
       const f3 mm = cross3(rP, nd);
-      float Jr[N];
+      T Jr[N];
 #pragma unroll
-      for (int i = 0; i < N; i++) Jr[i] = D::in_chain(i, lnk) ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : 0.f;
-      float y[NY];
+      for (int i = 0; i < N; i++) Jr[i] = D::in_chain(i, lnk) ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : T(0);
+      T y[NY];
 #pragma unroll
       for (int i = N; i < NY; i++) y[i] = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) {
         if (!D::in_chain(i, lnk)) { y[i] = 0.f; continue; }
-        float t = Jr[i];
+        T t = Jr[i];
 #pragma unroll
         for (int kk = 0; kk < i; kk++)
           if (D::coupled(i, kk) && D::in_chain(kk, lnk)) t -= L[D::lidx(i, kk)] * y[kk];
         y[i] = t * Ld[i];
       }
-      float D2 = 0.f;
+      T D2 = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
-      rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f);
+      rw.put(first_normal + 3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0),
+             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : T(0));
     }
-    rw.mu(nc) = (float)R::slot_mu[sl];
+    rw.mu(nc) = (T)R::slot_mu[sl];
     nc++;
   });
   // self-collision pairs (capsule-capsule / sphere) -- Humanoid.  World endpoints per
@@ -1114,8 +1173,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
 #pragma unroll
     for (int gg = 0; gg < R::NG; gg++) {
       const int b = R::geom_link[gg] + 1;
-      G0[gg] = k.x[b] + mulc(k.Rm[b], (float)R::geom_p0[gg][0], (float)R::geom_p0[gg][1], (float)R::geom_p0[gg][2]);
-      G1[gg] = k.x[b] + mulc(k.Rm[b], (float)R::geom_p1[gg][0], (float)R::geom_p1[gg][1], (float)R::geom_p1[gg][2]);
+      G0[gg] = k.x[b] + mulc(k.Rm[b], (T)R::geom_p0[gg][0], (T)R::geom_p0[gg][1], (T)R::geom_p0[gg][2]);
+      G1[gg] = k.x[b] + mulc(k.Rm[b], (T)R::geom_p1[gg][0], (T)R::geom_p1[gg][1], (T)R::geom_p1[gg][2]);
     }
 #pragma unroll 1
     for (int pp = 0; pp < R::NPAIR; pp++) {
@@ -1126,40 +1185,40 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       const f3 dc = (a0 + a1) - (b0 + b1);  // twice the centre distance
       if (dot3(dc, dc) > D::PAIR_BOUND2.v[pp][0]) continue;
       const f3 d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
-      const float aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
-      float ss, tt;
-      const float eps = 1e-12f;
+      const T aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
+      T ss, tt;
+      const T eps = T(1e-12);
       if (aa <= eps && ee <= eps) { ss = tt = 0.f; }
-      else if (aa <= eps) { ss = 0.f; tt = fminf(fmaxf(ff / ee, 0.f), 1.f); }
+      else if (aa <= eps) { ss = 0.f; tt = tmin(tmax(ff / ee, T(0)), T(1)); }
       else {
-        const float cc2 = dot3(d1, r0);
-        if (ee <= eps) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+        const T cc2 = dot3(d1, r0);
+        if (ee <= eps) { tt = 0.f; ss = tmin(tmax(-cc2 / aa, T(0)), T(1)); }
         else {
-          const float bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
-          ss = den > eps ? fminf(fmaxf((bb2 * ff - cc2 * ee) / den, 0.f), 1.f) : 0.f;
+          const T bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
+          ss = den > eps ? tmin(tmax((bb2 * ff - cc2 * ee) / den, T(0)), T(1)) : T(0);
           tt = (bb2 * ss + ff) / ee;
-          if (tt < 0.f) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
-          else if (tt > 1.f) { tt = 1.f; ss = fminf(fmaxf((bb2 - cc2) / aa, 0.f), 1.f); }
+          if (tt < T(0)) { tt = 0.f; ss = tmin(tmax(-cc2 / aa, T(0)), T(1)); }
+          else if (tt > T(1)) { tt = 1.f; ss = tmin(tmax((bb2 - cc2) / aa, T(0)), T(1)); }
         }
       }
       const f3 ca = a0 + ss * d1, cb = b0 + tt * d2;
       const f3 dv = ca - cb;
-      const float dd = norm3(dv);
-      const float ra = (float)R::geom_r[ga], rb = (float)R::geom_r[gb];
-      const float dist = dd - ra - rb;
-      if (!(dist < (float)PBG_CONTACT_THRESHOLD)) continue;
+      const T dd = norm3(dv);
+      const T ra = (T)R::geom_r[ga], rb = (T)R::geom_r[gb];
+      const T dist = dd - ra - rb;
+      if (!(dist < (T)PBG_CONTACT_THRESHOLD)) continue;
       csig += pbg_contact_hash(sub, (uint32_t)(R::NS + pp));
-      const f3 nrm = dd > 1e-9f ? fast_rcp(dd) * dv : mk3(0, 0, 1);
+      const f3 nrm = dd > T(1e-9) ? fast_rcp(dd) * dv : mk3<T>(0, 0, 1);
       const f3 PA = ca - ra * nrm, PB = cb + rb * nrm;
       f3 t1, t2;  // btPlaneSpace1(nrm)
-      if (fabsf(nrm.z) > 0.7071067811865476f) {
-        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
-        t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
-        t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+      if (tabs(nrm.z) > T(0.7071067811865476)) {
+        const T a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
+        t1 = mk3<T>(0, -nrm.z * kinv, nrm.y * kinv);
+        t2 = mk3<T>(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
       } else {
-        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
-        t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
-        t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+        const T a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
+        t1 = mk3<T>(-nrm.y * kinv, nrm.x * kinv, 0);
+        t2 = mk3<T>(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
       }
       const uint32_t ma = R::link_chain_mask[R::geom_link[ga]], mb = R::link_chain_mask[R::geom_link[gb]];
       const f3 rA = PA - O, rB = PB - O;
@@ -1167,15 +1226,15 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
       for (int dir = 0; dir < 3; dir++) {
         const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
         const f3 mA = cross3(rA, nd), mB = cross3(rB, nd);
-        float y[NY];
+        T y[NY];
 #pragma unroll
         for (int i = N; i < NY; i++) y[i] = 0.f;
-        float D2 = 0.f;
+        T D2 = 0.f;
 #pragma unroll
         for (int i = 0; i < N; i++) {
           const int di = D::dof_of(i);
           const bool inA = di < 0 || ((ma >> di) & 1u), inB = di < 0 || ((mb >> di) & 1u);
-          float t = 0.f;
+          T t = 0.f;
           if (inA) t += dot3(nd, sv[i]) + dot3(mA, sw[i]);
           if (inB) t -= dot3(nd, sv[i]) + dot3(mB, sw[i]);
 #pragma unroll
@@ -1185,10 +1244,10 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
           D2 += y[i] * y[i];
          
         }
-        rw.put(first_normal + 3 * nc + dir, y, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-               dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f);
+        rw.put(first_normal + 3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0),
+               dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : T(0));
       }
-      rw.mu(nc) = (float)R::pair_mu[pp];
+      rw.mu(nc) = (T)R::pair_mu[pp];
       nc++;
     }
   }
@@ -1201,8 +1260,8 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
     static_for<0, D::NLIM>([&](auto li_c) {
       constexpr int li = decltype(li_c)::value;
       constexpr int np = D::LIM.v[li][1], off = D::LIM.v[li][2];
-      float yv[N];
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      T yv[N];
+      T acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < N; i++) {
         const int j = D::LIMPOS.v[li][i];
@@ -1210,27 +1269,27 @@ PBG_DEV int substep(State<R>& s, const float* tau, uint32_t* slot_active, const 
         yv[i] = rw.lim(off + j);
         acc[j & 3] += yv[i] * u[i];
       }
-      const float meff = rw.lim(off + np), tlo = rw.lim(off + np + 1), thi = rw.lim(off + np + 2);
-      const float llo = rw.lim(off + np + 3), lhi = rw.lim(off + np + 4);
-      const float yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      const float nlo = clampf(llo + meff * (tlo - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-      const float dlo = nlo - llo;
+      const T meff = rw.lim(off + np), tlo = rw.lim(off + np + 1), thi = rw.lim(off + np + 2);
+      const T llo = rw.lim(off + np + 3), lhi = rw.lim(off + np + 4);
+      const T yu = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      const T nlo = clampf(llo + meff * (tlo - yu), T(0), (T)PBG_LIMIT_MAX_IMPULSE);
+      const T dlo = nlo - llo;
       // upper row sees u after the lower update: (-y).u' = -(yu + (y.y) dlo) = -(yu + dlo / meff)
-      const float yu2 = meff > 0.f ? yu + dlo * fast_rcp(meff) : yu;
-      const float nhi = clampf(lhi + meff * (thi + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-      const float dhi = nhi - lhi;
+      const T yu2 = meff > T(0) ? yu + dlo * fast_rcp(meff) : yu;
+      const T nhi = clampf(lhi + meff * (thi + yu2), T(0), (T)PBG_LIMIT_MAX_IMPULSE);
+      const T dhi = nhi - lhi;
       rw.lim(off + np + 3) = nlo;
       rw.lim(off + np + 4) = nhi;
-      const float dl = dlo - dhi;
+      const T dl = dlo - dhi;
 #pragma unroll
       for (int i = 0; i < N; i++)
         if (D::LIMPOS.v[li][i] >= 0) u[i] += yv[i] * dl;
     });
-    for (int c = 0; c < nc; c++) rw.solve(first_normal + 3 * c, u, 0.f, 3.0e38f);   // contact normals
+    for (int c = 0; c < nc; c++) rw.solve(first_normal + 3 * c, u, T(0), T(3.0e38f));   // contact normals
     for (int c = 0; c < nc; c++) {                                                  // frictions
-      const float ln = rw.lam(first_normal + 3 * c);
-      if (!(ln > 0.f)) continue;  // [EXT] friction rows only under a positive normal impulse
-      const float lim = rw.mu(c) * ln;
+      const T ln = rw.lam(first_normal + 3 * c);
+      if (!(ln > T(0))) continue;  // [EXT] friction rows only under a positive normal impulse
+      const T lim = rw.mu(c) * ln;
       rw.solve(first_normal + 3 * c + 1, u, -lim, lim);
       rw.solve(first_normal + 3 * c + 2, u, -lim, lim);
     }
@@ -1785,6 +1844,25 @@ PBG_DEV void m3_to_quat_f(const m3& mf, double* q) {
   }
   q[0] = x; q[1] = y; q[2] = z; q[3] = w;
 }
+// the float64 state's link rotation -> quaternion in float64 (the oracle's m3_to_quat, what
+// pybullet's getLinkState computes from its double frame)
+PBG_DEV void m3_to_quat_f(const M3<double>& md, double* q) {
+  const double* m = md.m;
+  const double t = m[0] + m[4] + m[8];
+  if (t > 0) {
+    const double s = sqrt(t + 1.0) * 2;
+    q[3] = 0.25 * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    const double s = sqrt(1.0 + m[0] - m[4] - m[8]) * 2;
+    q[3] = (m[7] - m[5]) / s; q[0] = 0.25 * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+  } else if (m[4] > m[8]) {
+    const double s = sqrt(1.0 + m[4] - m[0] - m[8]) * 2;
+    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = 0.25 * s; q[2] = (m[5] + m[7]) / s;
+  } else {
+    const double s = sqrt(1.0 + m[8] - m[0] - m[4]) * 2;
+    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = 0.25 * s;
+  }
+}
 
 // Gather pack inputs from the physical state (what pybullet's queries would return).
 // st(integral_constant<int, i>): diagnostic phase stamps between the parts (no-op by default)
@@ -1794,6 +1872,9 @@ struct NoStamp {
 };
 template <class R, class St = NoStamp>
 PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in, St st = St()) {
+  using T = real_t<R>;
+  using f3 = V3<T>;
+  using m3 = M3<T>;
   Kin<R> k;
   fk_pos<R>(s, k);
   st(std::integral_constant<int, 14>{});
@@ -1820,23 +1901,23 @@ PBG_DEV void gather(const State<R>& s, bool has_floor, PackIn<R>& in, St st = St
   // robot_body COM velocity
   f3 vel;
   if constexpr (b == 0) {
-    vel = mk3(s.bv[0], s.bv[1], s.bv[2]);
+    vel = mk3<T>(s.bv[0], s.bv[1], s.bv[2]);
   } else {
     // velocity of link b's COM: rigid/joint chain from the base (recomputed here)
     f3 w[R::NL + 1], v[R::NL + 1];
-    w[0] = R::floating ? mk3(s.bw[0], s.bw[1], s.bw[2]) : mk3(0, 0, 0);
-    v[0] = R::floating ? mk3(s.bv[0], s.bv[1], s.bv[2]) : mk3(0, 0, 0);
+    w[0] = R::floating ? mk3<T>(s.bw[0], s.bw[1], s.bw[2]) : mk3<T>(0, 0, 0);
+    v[0] = R::floating ? mk3<T>(s.bv[0], s.bv[1], s.bv[2]) : mk3<T>(0, 0, 0);
 #pragma unroll
     for (int l = 0; l < R::NL; l++) {
       const int p = R::link_parent[l] + 1, jt = R::link_jtype[l], d = R::link_dof[l];
       const f3 cp = k.c[p], c = k.c[l + 1];
       if (jt == 0 || jt == 1) {
-        const m3 Ro = quat_to_m3c(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
+        const m3 Ro = quat_to_m3c<T>(R::link_offset_quat[l][0], R::link_offset_quat[l][1], R::link_offset_quat[l][2], R::link_offset_quat[l][3]);
         const m3 R0 = mulc(k.Rm[p], Ro);
-        const f3 a = mulc(R0, (float)R::link_axis[l][0], (float)R::link_axis[l][1], (float)R::link_axis[l][2]);
-        const f3 x0 = k.x[p] + mulc(k.Rm[p], (float)R::link_offset_pos[l][0], (float)R::link_offset_pos[l][1], (float)R::link_offset_pos[l][2]);
+        const f3 a = mulc(R0, (T)R::link_axis[l][0], (T)R::link_axis[l][1], (T)R::link_axis[l][2]);
+        const f3 x0 = k.x[p] + mulc(k.Rm[p], (T)R::link_offset_pos[l][0], (T)R::link_offset_pos[l][1], (T)R::link_offset_pos[l][2]);
         if (jt == 0) {
-          const f3 o = x0 + mulc(R0, (float)R::link_anchor[l][0], (float)R::link_anchor[l][1], (float)R::link_anchor[l][2]);
+          const f3 o = x0 + mulc(R0, (T)R::link_anchor[l][0], (T)R::link_anchor[l][1], (T)R::link_anchor[l][2]);
           const f3 vo = v[p] + cross3(w[p], o - cp);
           w[l + 1] = w[p] + s.qd[d] * a;
           v[l + 1] = vo + cross3(w[l + 1], c - o);
@@ -1867,7 +1948,7 @@ PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
   if constexpr (R::tip_link >= 0) {
     Kin<R> k;
     fk_pos<R>(s, k);
-    const f3 c = k.c[R::tip_link + 1];
+    const V3<real_t<R>> c = k.c[R::tip_link + 1];
     tip[0] = c.x; tip[1] = c.y; tip[2] = c.z;
   }
   pendulum_obs<R>(jq, jqd, tip, obs, po);
@@ -1877,11 +1958,12 @@ PBG_DEV void pendulum_pack(const State<R>& s, float* obs, PackOut& po) {
 // Q = 4: the pack's transcendentals dealt over a DPP quad (quad / gang kernels, `lane`).
 template <class R, int Q = 1>
 PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                           double& pot, float& z0, uint32_t epi, Flag& fl, HarderBk* hb = nullptr, int lane = 0) {
+                           double& pot, real_t<R>& z0, uint32_t epi, Flag& fl, HarderBk* hb = nullptr, int lane = 0) {
+  using T = real_t<R>;
   snapshot_state<R>(s);
   if (init_q) {
 #pragma unroll
-    for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = (float)R::reset_offset[r] + init_q[(size_t)e * R::NR + r];
+    for (int r = 0; r < R::NR; r++) s.q[R::reset_dof[r]] = (T)R::reset_offset[r] + (T)init_q[(size_t)e * R::NR + r];
   } else {
     // np_random.uniform(-0.1, 0.1) per ordered joint (robot_locomotors.py:18-19) -> Philox
     const uint32_t gid = (uint32_t)(B.env_offset + e);
@@ -1893,7 +1975,7 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int r = 4 * blk + t;
-        if (r < R::NR) s.q[R::reset_dof[r]] = (float)R::reset_offset[r] + fmaf(0.2f, u01(rr[t]), -0.1f);
+        if (r < R::NR) s.q[R::reset_dof[r]] = (T)R::reset_offset[r] + (T)fmaf(0.2f, u01(rr[t]), -0.1f);
       }
     }
   }
@@ -1925,14 +2007,14 @@ PBG_DEV void reset_env_epi(const Buffers& B, int e, State<R>& s, const float* in
   else flag_pack<R, Q>(in, nullptr, obs, po, fl, draw, lane, hb);
   if constexpr (R::harder) po.potential = harder_potential(*hb, po.potential, po.body_xyz[2]);  // env_bases.py:70
   pot = po.potential;
-  z0 = (float)po.initial_z;
+  z0 = (T)po.initial_z;
   has_floor = true;  // gym_locomotion_envs.py:30-31: the floor joins robot.parts
   }
 }
 
 template <class R>
 PBG_DEV void reset_env(const Buffers& B, int e, State<R>& s, const float* init_q, float* obs, bool& has_floor,
-                       double& pot, float& z0) {
+                       double& pot, real_t<R>& z0) {
   const uint32_t epi = B.episode[e];
   B.episode[e] = epi + 1;
   Flag fl = load_flag<R>(B, e);
@@ -1950,12 +2032,12 @@ __global__ __launch_bounds__(64) void reset_kernel(Buffers B, ResetIO io) {
   State<R> s;
   bool has_floor = B.flags[e] & 1u;
   double pot;
-  float z0;
+  real_t<R> z0;
   float obs[R::OBS];
   reset_env<R>(B, e, s, io.init_q, obs, has_floor, pot, z0);
-  store_state<R>(s, B.st, B.n, e);
+  store_state<R>(s, st_of<R>(B), B.n, e);
   B.pot[e] = pot;
-  B.z0[e] = z0;
+  z0_of<R>(B)[e] = z0;
   B.elapsed[e] = 0;
   B.flags[e] = has_floor ? 1u : 0u;  // feet_contact cleared (robot_locomotors.py:22)
 #pragma unroll
@@ -1968,31 +2050,33 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
   STAMP_DECL
+  using T = real_t<R>;
   State<R> s;
-  load_state<R>(s, B.st, B.n, e);
+  load_state<R>(s, st_of<R>(B), B.n, e);
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
   // apply_action: tau = power * power_coef * clip(a, -1, 1)   (robot_locomotors.py:26-29)
-  float tau[R::NJ];
+  T tau[R::NJ];
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) tau[d] = 0.f;
 #pragma unroll
   for (int i = 0; i < R::NA; i++) {
     const float c = fminf(fmaxf(act[i], -1.f), 1.f);
-    tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
+    tau[R::act_dof[i]] += (T)(R::act_gain[i] * (double)c);
   }
   uint32_t slot_active[R::NS > 0 ? R::NS : 1];
   Rows<R, LS> rw;
-  rw.lds = (lds_float*)lds_dyn + threadIdx.x;
-  rw.gbl = scratch + e;
+  rw.lds = (lds_t<T>*)lds_dyn + threadIdx.x;
+  rw.gbl = (T*)scratch + e;
   rw.n = B.n;
   rw.cap = lds_rows;
   int nc = 0;
   uint32_t csig = 0;
   STAMP(7)
-  for (int sub = 0; sub < B.sp.substeps; sub++)
-    nc = substep<R, LS>(s, tau, slot_active, rw, (uint32_t)sub, csig, B.sp SUB_STAMP_PASS);
+  const SimPT<T>& P = sp_of<R>(B);
+  for (int sub = 0; sub < P.substeps; sub++)
+    nc = substep<R, LS>(s, tau, slot_active, rw, (uint32_t)sub, csig, P SUB_STAMP_PASS);
   if (io.ncontact) io.ncontact[e] = nc;
   if (io.csig) io.csig[e] = csig;
   const int el = B.elapsed[e] + 1;
@@ -2021,7 +2105,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     }
     in.feet_new = fnew;
     in.potential_old = B.pot[e];
-    in.initial_z = B.z0[e];
+    in.initial_z = z0_of<R>(B)[e];
     Flag fl = load_flag<R>(B, e);
     HarderBk hb = load_harder<R>(B, e);
     if constexpr (R::kind == 3) mujoco3d_pack<R>(in, act, obs, po);
@@ -2030,7 +2114,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
       double pos[3], vel[3];
       if (harder_step<R>(B, e, in, obs, po, hb, pos, vel, nullptr)) {  // resetBasePosition / Velocity
 #pragma unroll
-        for (int i = 0; i < 3; i++) { s.cube.p[i] = (float)pos[i]; s.cube.v[i] = (float)vel[i]; s.cube.w[i] = 0.f; }
+        for (int i = 0; i < 3; i++) { s.cube.p[i] = (T)pos[i]; s.cube.v[i] = (T)vel[i]; s.cube.w[i] = 0.f; }
       }
       store_harder<R>(B, e, hb);
     }
@@ -2056,10 +2140,10 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     }
     bool has_floor = flags & 1u;
     double pot;
-    float z0;
+    T z0;
     reset_env<R>(B, e, s, nullptr, obs, has_floor, pot, z0);
     B.pot[e] = pot;
-    B.z0[e] = z0;
+    z0_of<R>(B)[e] = z0;
     B.elapsed[e] = 0;
     B.flags[e] = has_floor ? 1u : 0u;
   } else {
@@ -2067,7 +2151,7 @@ __global__ __launch_bounds__(64) void step_kernel(Buffers B, StepIO io, float* _
     B.elapsed[e] = el;
     B.flags[e] = flags;
   }
-  store_state<R>(s, B.st, B.n, e);
+  store_state<R>(s, st_of<R>(B), B.n, e);
 #pragma unroll
   for (int i = 0; i < R::OBS; i++) io.obs[(size_t)e * R::OBS + i] = obs[i];
   STAMP(9)
@@ -2174,10 +2258,11 @@ __global__ __launch_bounds__(64) void get_state_kernel(Buffers B, double* __rest
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
   constexpr int SD = Dims<R>::SD, AD = Records<R>::AD;
-  for (int i = 0; i < SD; i++) phys[(size_t)e * SD + i] = (double)B.st[(size_t)i * B.n + e];
+  const real_t<R>* st = st_of<R>(B);
+  for (int i = 0; i < SD; i++) phys[(size_t)e * SD + i] = (double)st[(size_t)i * B.n + e];
   double* a = aux + (size_t)e * AD;
   a[0] = B.pot[e];
-  a[1] = (double)B.z0[e];
+  a[1] = (double)z0_of<R>(B)[e];
   a[2] = (double)B.elapsed[e];
   a[3] = (double)(B.flags[e] & 1u);
   for (int f = 0; f < R::NF; f++) a[4 + f] = (double)((B.flags[e] >> (8 + f)) & 1u);
@@ -2197,11 +2282,13 @@ __global__ __launch_bounds__(64) void set_state_kernel(Buffers B, const double* 
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B.n) return;
   constexpr int SD = Dims<R>::SD, AD = Records<R>::AD;
-  for (int i = 0; i < SD; i++) B.st[(size_t)i * B.n + e] = (float)phys[(size_t)e * SD + i];
+  using T = real_t<R>;
+  T* st = st_of<R>(B);
+  for (int i = 0; i < SD; i++) st[(size_t)i * B.n + e] = (T)phys[(size_t)e * SD + i];
   if (aux) {
     const double* a = aux + (size_t)e * AD;
     B.pot[e] = a[0];
-    B.z0[e] = (float)a[1];
+    z0_of<R>(B)[e] = (T)a[1];
     B.elapsed[e] = (int)a[2];
     uint32_t fl = a[3] != 0.0 ? 1u : 0u;
     for (int f = 0; f < R::NF; f++) fl |= (a[4 + f] != 0.0 ? 1u : 0u) << (8 + f);

@@ -1279,23 +1279,23 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   STAMP_DECL
   TState<R> s;
 #pragma unroll
-  for (int i = 0; i < 3; i++) s.bp[i] = B.st[(size_t)i * B.n + e];
+  for (int i = 0; i < 3; i++) s.bp[i] = st_of<R>(B)[(size_t)i * B.n + e];
 #pragma unroll
-  for (int i = 0; i < 4; i++) s.bq[i] = B.st[(size_t)(3 + i) * B.n + e];
+  for (int i = 0; i < 4; i++) s.bq[i] = st_of<R>(B)[(size_t)(3 + i) * B.n + e];
 #pragma unroll
-  for (int i = 0; i < 3; i++) s.bv[i] = B.st[(size_t)(7 + i) * B.n + e];
+  for (int i = 0; i < 3; i++) s.bv[i] = st_of<R>(B)[(size_t)(7 + i) * B.n + e];
 #pragma unroll
-  for (int i = 0; i < 3; i++) s.bw[i] = B.st[(size_t)(10 + i) * B.n + e];
+  for (int i = 0; i < 3; i++) s.bw[i] = st_of<R>(B)[(size_t)(10 + i) * B.n + e];
 #pragma unroll
   for (int j = 0; j < NDB; j++) {
-    s.q[j] = B.st[(size_t)(SB + kb * NDB + j) * B.n + e];
-    s.qd[j] = B.st[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e];
+    s.q[j] = st_of<R>(B)[(size_t)(SB + kb * NDB + j) * B.n + e];
+    s.qd[j] = st_of<R>(B)[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e];
   }
   // the pack's bookkeeping loads, issued here so their latency overlaps the physics
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   const double pot_old = B.pot[e];
-  const float z0_old = B.z0[e];
+  const float z0_old = z0_of<R>(B)[e];
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
@@ -1382,7 +1382,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     team_reset<R, ES>(B, e, L, s, rw, obs, has_floor, pot, z0);
     if (kb == 0) {
       B.pot[e] = pot;
-      B.z0[e] = z0;
+      z0_of<R>(B)[e] = z0;
       B.elapsed[e] = 0;
       B.flags[e] = has_floor ? 1u : 0u;
     }
@@ -1398,14 +1398,14 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     static_for<0, (PBG_BASE_WORDS + 3) / 4>([&](auto m_c) {
       constexpr int m = decltype(m_c)::value;
       const float v = lanes_pick<4, m, PBG_BASE_WORDS>(bw, kb);
-      if (4 * m + kb < PBG_BASE_WORDS) B.st[(size_t)(4 * m + kb) * B.n + e] = v;
+      if (4 * m + kb < PBG_BASE_WORDS) st_of<R>(B)[(size_t)(4 * m + kb) * B.n + e] = v;
     });
     lanes_store_row<R, 4>(obs, io.obs, e, kb);
   }
 #pragma unroll
   for (int j = 0; j < NDB; j++) {
-    B.st[(size_t)(SB + kb * NDB + j) * B.n + e] = s.q[j];
-    B.st[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e] = s.qd[j];
+    st_of<R>(B)[(size_t)(SB + kb * NDB + j) * B.n + e] = s.q[j];
+    st_of<R>(B)[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e] = s.qd[j];
   }
   STAMP(9)
   STAMP_FLUSH

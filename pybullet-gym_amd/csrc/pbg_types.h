@@ -2,36 +2,44 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace pbg {
 // Scene / World parameters of a handle (include/pbg.h pbg_sim_params_t; scene_bases.py:8-18,
 // 58-73), resolved once on the host at create into the constants the kernels use.  Every
 // derived float is formed in float arithmetic exactly as the kernels formed it when these
 // were compile-time constants, so default parameters reproduce the old bits.
-struct SimP {
-  float dt;          // Scene.timestep: one stepSimulation sub-step
-  float gravity;     // World.gravity: setGravity(0, 0, -gravity)
-  float k_sep;       // position-target slope of a separated row: -1 / dt (pos_target)
-  float k_contact;   // ... of a penetrating contact normal: -contact_erp / dt
-  float k_limit;     // ... of a violated joint limit: -limit_erp / dt
-  float ang_max;     // [EXT] angular motion threshold / dt (exponential-map integration)
-  float dt3c;        // dt^3 / 48 (small-angle quaternion series)
+template <class S>
+struct SimPT {
+  S dt;              // Scene.timestep: one stepSimulation sub-step
+  S gravity;         // World.gravity: setGravity(0, 0, -gravity)
+  S k_sep;           // position-target slope of a separated row: -1 / dt (pos_target)
+  S k_contact;       // ... of a penetrating contact normal: -contact_erp / dt
+  S k_limit;         // ... of a violated joint limit: -limit_erp / dt
+  S ang_max;         // [EXT] angular motion threshold / dt (exponential-map integration)
+  S dt3c;            // dt^3 / 48 (small-angle quaternion series)
   int substeps;      // Scene.frame_skip = numSubSteps
   int iterations;    // World.numSolverIterations
   int flag_timeout;  // HumanoidFlagrun: 600 / frame_skip steps, rounded up (robot_locomotors.py:218-223)
   double env_dt;     // Scene.dt = timestep * frame_skip (the potential's divisor, scene_bases.py:17)
 };
+using SimP = SimPT<float>;
 
-inline SimP resolve_sim_params(double timestep, int frame_skip, int iterations, double gravity, double contact_erp,
-                               double limit_erp, double angular_motion_threshold) {
-  SimP p;
-  p.dt = (float)timestep;
-  const float inv_dt = (float)(1.0 / timestep);
-  p.gravity = (float)gravity;
+// The same parameters formed in S arithmetic: S = float reproduces the bits of the compile-time
+// constants the float32 kernels once folded; S = double is the scene at btScalar precision
+// (scene_bases.py:75-76), as the float64 oracle forms it.
+template <class S = float>
+inline SimPT<S> resolve_sim_params(double timestep, int frame_skip, int iterations, double gravity, double contact_erp,
+                                   double limit_erp, double angular_motion_threshold) {
+  SimPT<S> p;
+  p.dt = (S)timestep;
+  const S inv_dt = (S)(1.0 / timestep);
+  p.gravity = (S)gravity;
   p.k_sep = -inv_dt;
-  p.k_contact = -(float)contact_erp * inv_dt;
-  p.k_limit = -(float)limit_erp * inv_dt;
-  p.ang_max = (float)angular_motion_threshold / p.dt;
-  p.dt3c = p.dt * p.dt * p.dt * 0.020833333333f;
+  p.k_contact = -(S)contact_erp * inv_dt;
+  p.k_limit = -(S)limit_erp * inv_dt;
+  p.ang_max = (S)angular_motion_threshold / p.dt;
+  p.dt3c = p.dt * p.dt * p.dt * (sizeof(S) == 4 ? (S)0.020833333333f : (S)0.020833333333);
   p.substeps = frame_skip;
   p.iterations = iterations;
   p.flag_timeout = (600 + frame_skip - 1) / frame_skip;
@@ -39,11 +47,29 @@ inline SimP resolve_sim_params(double timestep, int frame_skip, int iterations, 
   return p;
 }
 
+// Scalar of a robot's physics state and arithmetic: float (the float32 kernels) or double
+// (F64<R>: the reference-precision path, pbg_create_ex precision 64).  F64<R> is the robot R
+// with `real = double`; every model table is R's.
+template <class R, class = void>
+struct RealOf {
+  using type = float;
+};
+template <class R>
+struct RealOf<R, std::void_t<typename R::real>> {
+  using type = typename R::real;
+};
+template <class R>
+using real_t = typename RealOf<R>::type;
+template <class R0>
+struct F64 : R0 {
+  using real = double;
+};
+
 struct Buffers {
   int n;                   // envs on this device
-  float* st;               // [SD][n] physical state, SoA
+  void* st;                // [SD][n] physical state, SoA, in the handle's precision (st_of<R>)
   double* pot;             // [n] potential
-  float* z0;               // [n] initial_z
+  void* z0;                // [n] initial_z, in the handle's precision (z0_of<R>)
   int* elapsed;            // [n] steps in episode
   uint32_t* flags;         // [n] bit0 floor-in-parts, bits 8.. feet_contact
   uint32_t* episode;       // [n] resets so far (RNG counter)
@@ -53,7 +79,8 @@ struct Buffers {
   int32_t* hki;            // [3][n] frame, on_ground_frame_counter, cube launches so far (Harder)
   uint64_t seed;
   int env_offset;          // global id of env 0 (multi-GPU sharding)
-  SimP sp;                 // the handle's scene parameters (kernel arguments)
+  SimP sp;                 // the handle's scene parameters (kernel arguments), float32 kernels
+  SimPT<double> sp64;      // the same scene in float64 (the reference-precision kernels)
 };
 
 struct StepIO {

@@ -49,6 +49,10 @@ class VecEnv:
     pbg_sim_params_t, scene_bases.py:8-18,58-73), or a ``_native.SimParams``; None = the
     reference's values (``self.sim_params`` holds the ones in force).
 
+    ``precision``: 32 (float32 physics, the fast kernels) or 64 (float64 physics state and
+    arithmetic, the reference's btScalar precision; pbg_create_v2).  Observations stay float32 and
+    the reward pack float64 in both, as the reference's (robot_locomotors.py:64, gym_locomotion_envs.py:99-105).
+
     ``kernel`` / ``lds_rows`` / ``gang_dist`` / ``gang_lanes`` are test and diagnostic launch
     options (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
     a cap on LDS-resident contact rows, forced replicated (0) / distributed (1) gang dynamics, the
@@ -57,7 +61,7 @@ class VecEnv:
 
     def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
                  autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1,
-                 sim_params=None, gang_lanes: int = -1):
+                 sim_params=None, gang_lanes: int = -1, precision: int = 32):
         if not torch.cuda.is_available():
             raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.env_id = env_id
@@ -67,11 +71,12 @@ class VecEnv:
         L = _native.lib()
         h = ctypes.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        opts = _native.DebugOpts(int(kernel), int(lds_rows), int(gang_dist), int(gang_lanes))
+        opts = _native.CreateOpts(int(precision), int(kernel), int(lds_rows), int(gang_dist), int(gang_lanes))
         sp = sim_params if isinstance(sim_params, _native.SimParams) else _native.sim_params(env_id, sim_params)
-        _native.check(L.pbg_create_ex(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
+        _native.check(L.pbg_create_v2(_native.env_id_bytes(env_id), self.num_envs, idx, seed, env_offset,
                                       ctypes.byref(sp), ctypes.byref(opts), ctypes.byref(h)), "pbg_create")
         self._h = h
+        self.precision = L.pbg_precision(h)
         self.sim_params = _native.SimParams()
         _native.check(L.pbg_get_sim_params(h, ctypes.byref(self.sim_params)), "pbg_get_sim_params")
         info = _native.Info()

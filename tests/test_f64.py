@@ -1,0 +1,256 @@
+"""Reference-precision (float64) physics path: parity against the float64 oracle.
+
+pybullet steps in double (btScalar; stepSimulation, /root/reference/pybulletgym/envs/roboschool/
+scene_bases.py:75-76).  ``VecEnv(..., precision=64)`` (pbg_create_v2) keeps the physical state in
+float64 and runs the same algorithm as the float32 kernels -- and as the oracle -- in float64
+arithmetic, with IEEE division / sqrt and the device library's sin / cos.  Against the float64
+oracle the remaining differences are float64 rounding (summation orders, the kernels' inertia-
+about-O formulation of M), so the bounds here are nine orders tighter than the float32 tests':
+
+  * teacher-forced env steps, split like tests/test_gpu.py (same contact-set signature and
+    discrete reward terms; conditioning probes at PROBE_REL64 = 1e-12 relative): class A --
+    the float64 STATE after the step (pbg_get_state) within STATE_REL64 = 1e-9 relative of the
+    oracle's in >= 99.9 % of the env-steps with a hard maximum of 1e-6, the float64 reward within
+    1e-9, the float32 observation equal to the oracle's float32 observation up to one float32
+    rounding (2^-23 relative: both round float64 values that agree to ~1e-15), done flags and
+    contact counts identical; class B (the oracle's own 1e-12 perturbation spread above 1e-10) at
+    most 10 % of the env-steps, within 10 x that spread at the 99th percentile; class C (another
+    contact set) at most 1 %.
+  * free running at the north-star horizon: from the same float64 reset state and the same 1,000
+    action batches the float64 GPU leaves the float64 oracle's trajectory (obs error above 1e-4)
+    far later than float32 arithmetic of the same algorithm does (the oracle's IEEE-float32
+    instantiation): median first step at least F64_FREE_FACTOR x float32's.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import pybulletgym_amd  # noqa: F401
+from pybulletgym_amd.vec_env import VecEnv, sample_actions
+from test_gpu import ENVS, _discrete_terms, _first_exceed, _rel, _report
+
+pytestmark = pytest.mark.gpu
+
+ENVS64 = [e for e in ENVS if e != "AtlasPyBulletEnv-v0"]  # Atlas: no float64 kernel (include/pbg.h)
+STATE_REL64 = 1e-9
+HARD_MAX64 = 1e-6
+SHARE64 = 0.999
+OBS_ULP = 2.0 ** -23
+PROBE_REL64, PROBE_ABS64, COND_EPS64 = 1e-12, 1e-14, 1e-10
+COND_FRAC64, LOOSE_FRAC64, SPREAD_RATIO64 = 0.10, 0.01, 10.0
+F64_FREE_FACTOR = 2.0
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _state_rel(a, b):
+    return (np.abs(a - b) / np.maximum(1.0, np.abs(b))).max(axis=1)
+
+
+def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None):
+    """The GPU float64 handle steps all n envs (auto-reset, Philox actions); before each step the
+    sampled envs' float64 state records go to the oracle (and to N probes perturbed by 1e-12
+    relative), which steps them; compared as in the module docstring."""
+    if sim is not None:
+        sp = VecEnv.default_sim_params(env_id)
+        sp.update(sim)
+        oracle.set_sim_params(sp)
+    try:
+        env = VecEnv(env_id, n, seed=seed, autoreset=True, precision=64, sim_params=sim)
+        assert env.precision == 64
+        env.reset()
+        idx = np.arange(n) if sample is None else np.linspace(0, n - 1, sample).astype(np.int64)
+        tidx = torch.from_numpy(idx).cuda()
+        th = min(16, os.cpu_count() or 1)
+        orc = oracle.OracleEnvs(env_id, len(idx), nthreads=th, seed=seed)
+        prb = [oracle.OracleEnvs(env_id, len(idx), nthreads=th, seed=seed) for _ in range(3)]
+        pert = np.random.default_rng(seed)
+        kind = "harder" if "Harder" in env_id else orc.info.kind
+        acts = sample_actions(env.info.action_dim, n, steps, seed=seed)
+        errA, rewA, obsA, spreadB = [], [], [], []
+        nA = nB = nC = dmis = cmis = 0
+        t0 = time.time()
+        for t in range(steps):
+            if t % 20 == 0:
+                print(f"  f64 {name or env_id}: step {t}/{steps} {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+            phys, aux = env.get_state()
+            orc.state[:] = phys.index_select(0, tidx).cpu().numpy()
+            orc.aux[:] = aux.index_select(0, tidx).cpu().numpy()
+            for p in prb:
+                p.state[:] = orc.state + pert.uniform(-1, 1, orc.state.shape) * (PROBE_REL64 * np.abs(orc.state) + PROBE_ABS64)
+                p.aux[:] = orc.aux
+            res = env.step(acts[t], want_reward64=True, want_contacts=True, want_terms=True)
+            done_g = res.done.bool()
+            og = torch.where(done_g[:, None], res.terminal_obs, res.obs).index_select(0, tidx).cpu().numpy()
+            dg = (done_g & ~res.truncated.bool()).index_select(0, tidx).cpu().numpy()
+            rg = env.reward64.index_select(0, tidx).cpu().numpy()
+            cg = env.ncontact.index_select(0, tidx).cpu().numpy()
+            sg = env.contact_sig.index_select(0, tidx).cpu().numpy().view(np.uint32)
+            tg = env.reward_terms.index_select(0, tidx).cpu().numpy()
+            ph2, _ = env.get_state()
+            sgpu = ph2.index_select(0, tidx).cpu().numpy()
+            a = acts[t].index_select(0, tidx).cpu().numpy()
+            oo, ro, do, co = orc.step(a)
+            spread = np.zeros(len(idx))
+            cond = np.ones(len(idx), bool)
+            for p in prb:
+                p.step(a)
+                spread = np.maximum(spread, _state_rel(p.state, orc.state))
+                cond &= p.csig == orc.csig
+            cond &= spread <= COND_EPS64
+            same = (sg == orc.csig) & (_discrete_terms(tg, kind) == _discrete_terms(orc.terms, kind)).all(axis=1)
+            live = ~done_g.index_select(0, tidx).cpu().numpy()  # the GPU auto-reset the others' state
+            A = same & cond
+            B = same & ~cond
+            nA += int(A.sum())
+            nB += int(B.sum())
+            nC += int((~same).sum())
+            serr = _state_rel(sgpu, orc.state)
+            errA.append(serr[A & live])
+            rewA.append(np.abs(rg - ro)[A] / np.maximum(1.0, np.abs(ro[A])))
+            obsA.append(_rel(og, oo)[A])
+            dmis += int((dg[A] != do[A]).sum())
+            cmis += int((cg[A] != co[A]).sum())
+            if (B & live).any():
+                spreadB.append(serr[B & live] / np.maximum(spread[B & live], COND_EPS64))
+        env.close()
+    finally:
+        if sim is not None:
+            oracle.set_sim_params(None)
+    n_all = nA + nB + nC
+    eA = np.concatenate(errA) if errA else np.zeros(1)
+    rA = np.concatenate(rewA) if rewA else np.zeros(1)
+    oA = np.concatenate(obsA) if obsA else np.zeros(1)
+    rB = np.concatenate(spreadB) if spreadB else np.zeros(1)
+    rec = dict(test=name or f"f64_teacher_forced[{env_id},{n}x{steps}]", env_steps=n_all, classA_frac=nA / n_all,
+               classA_state_share_within_1e-9=float((eA <= STATE_REL64).mean()), classA_state_max_rel=float(eA.max()),
+               classA_state_p50_rel=float(np.median(eA)), classA_reward_max_rel=float(rA.max()),
+               classA_obs_max_rel=float(oA.max()), classA_done_mismatch=dmis, classA_contact_count_mismatch=cmis,
+               classB_frac=nB / n_all, classB_ratio_to_spread_p99=float(np.percentile(rB, 99)),
+               classC_frac=nC / n_all)
+    _report(rec)
+    assert nA > 0
+    assert rec["classA_state_share_within_1e-9"] >= SHARE64 and rec["classA_state_max_rel"] <= HARD_MAX64, rec
+    assert float((rA <= STATE_REL64).mean()) >= SHARE64, rec
+    assert rec["classA_obs_max_rel"] <= 1.01 * OBS_ULP, rec
+    assert dmis == 0 and cmis == 0, rec
+    assert rec["classB_frac"] <= COND_FRAC64 and rec["classB_ratio_to_spread_p99"] <= SPREAD_RATIO64, rec
+    assert rec["classC_frac"] <= LOOSE_FRAC64, rec
+    return rec
+
+
+@pytest.mark.parametrize("env_id", ENVS64)
+def test_f64_reset_matches_oracle(env_id):
+    """Reset from the same float32 init_q: float64 state records equal to the oracle's to 1e-13,
+    observations equal up to one float32 rounding."""
+    n = 128
+    env = VecEnv(env_id, n, seed=5, autoreset=False, precision=64)
+    orc = oracle.OracleEnvs(env_id, n, seed=5)
+    q0 = np.random.default_rng(0).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
+    obs = env.reset(init_q=torch.from_numpy(q0)).cpu().numpy()
+    obs_o = orc.reset(q0.astype(np.float64))
+    assert _rel(obs, obs_o).max() <= 1.01 * OBS_ULP
+    phys, aux = env.get_state()
+    np.testing.assert_allclose(phys.cpu().numpy(), orc.state, rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(aux.cpu().numpy(), orc.aux, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("env_id", ENVS64)
+def test_f64_step_teacher_forced_parity(env_id):
+    """Every float64 env id, 256 envs x 60 teacher-forced steps."""
+    _teacher_forced64(env_id, 256, 60)
+
+
+CONFIGS64 = [("InvertedPendulumPyBulletEnv-v0", 1024, None), ("HopperPyBulletEnv-v0", 4096, 512),
+             ("AntPyBulletEnv-v0", 16384, 512), ("HalfCheetahPyBulletEnv-v0", 8192, 384),
+             ("HumanoidPyBulletEnv-v0", 4096, 192)]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("env_id,n,sample", CONFIGS64)
+def test_f64_config_parity(env_id, n, sample):
+    """The BASELINE.json per-GPU config sizes, 200 teacher-forced steps, an evenly spread sample."""
+    _teacher_forced64(env_id, n, 200, sample=sample, seed=7, name=f"f64_config[{env_id},{n}x200]")
+
+
+def test_f64_sim_params_teacher_forced():
+    """A changed scene reaches the float64 kernels at float64 precision (SimPT<double>)."""
+    _teacher_forced64("AntPyBulletEnv-v0", 128, 30, sim={"gravity": 4.9, "solver_iterations": 8},
+                      name="f64_sim_params[Ant,g=4.9,it=8]")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("env_id,n,sample", [("AntPyBulletEnv-v0", 16384, 512), ("HumanoidPyBulletEnv-v0", 4096, 192)])
+def test_f64_free_running_divergence_far_later_than_float32(env_id, n, sample, steps=1000):
+    env = VecEnv(env_id, n, seed=17, autoreset=False, precision=64)
+    env.reset()
+    idx = np.linspace(0, n - 1, sample).astype(np.int64)
+    tidx = torch.from_numpy(idx).cuda()
+    th = min(16, os.cpu_count() or 1)
+    phys, aux = env.get_state()
+    orcs = {}
+    for name, prec in (("f64", 64), ("f32", 32)):
+        o = oracle.OracleEnvs(env_id, sample, nthreads=th, seed=17, precision=prec)
+        o.state[:] = phys.index_select(0, tidx).cpu().numpy()  # the same float64 reset state
+        o.aux[:] = aux.index_select(0, tidx).cpu().numpy()
+        orcs[name] = o
+    acts = sample_actions(env.info.action_dim, n, steps, seed=0xF4EE)
+    err = {k: np.zeros((steps, sample)) for k in ("gpu", "f32")}
+    t0 = time.time()
+    for t in range(steps):
+        if t % 100 == 0:
+            print(f"  f64 free_running[{env_id}]: step {t}/{steps} {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+        res = env.step(acts[t])
+        og = res.obs.index_select(0, tidx).cpu().numpy()
+        a = acts[t].index_select(0, tidx).cpu().numpy()
+        o64, _, _, _ = orcs["f64"].step(a)
+        o32, _, _, _ = orcs["f32"].step(a)
+        err["gpu"][t] = _rel(og, o64)
+        err["f32"][t] = _rel(o32, o64)
+    env.close()
+    rec = dict(test=f"f64_free_running[{env_id},{n},{sample}x{steps}]")
+    first = {}
+    for thr in (1e-4, 1e-2):
+        for k in ("gpu", "f32"):
+            f = _first_exceed(err[k], thr)
+            first[(k, thr)] = f
+            rec[f"{k}_first_above_{thr:g}_p10_p50_p90"] = [float(np.percentile(f, q)) for q in (10, 50, 90)]
+            rec[f"{k}_never_above_{thr:g}_frac"] = float((f == steps).mean())
+    _report(rec)
+    for thr in (1e-4, 1e-2):
+        g, f = np.median(first[("gpu", thr)]), np.median(first[("f32", thr)])
+        assert g >= F64_FREE_FACTOR * f, (thr, g, f, rec)
+
+
+def test_f64_determinism_and_env_offset_invariance():
+    """Bitwise reruns and shard invariance of the float64 handle (the multi-GPU split)."""
+    def run(n, off):
+        env = VecEnv("HopperPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True, precision=64)
+        env.reset()
+        g = torch.Generator(device="cuda").manual_seed(0)
+        acts = torch.rand((30, 64, 3), device="cuda", generator=g) * 2 - 1
+        out = [env.step(acts[t][off:off + n].contiguous()).obs.clone() for t in range(30)]
+        st = env.get_state()[0].cpu().numpy()
+        return torch.stack(out).cpu().numpy(), st
+    a, sa = run(64, 0)
+    b, sb = run(64, 0)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(sa, sb)
+    c, sc = run(32, 32)
+    np.testing.assert_array_equal(a[:, 32:], c)
+    np.testing.assert_array_equal(sa[32:], sc)
+
+
+def test_f64_atlas_is_refused():
+    from pybulletgym_amd._native import PbgError
+    with pytest.raises(PbgError):
+        VecEnv("AtlasPyBulletEnv-v0", 4, precision=64)

@@ -86,3 +86,29 @@ def test_default_sim_params_are_the_reference_scenes():
         _native.sim_params("AntPyBulletEnv-v0", {"gravty": 1.0})
     with pytest.raises(_native.PbgError):
         _native.default_sim_params("NoSuchEnv-v0")
+
+
+def test_create_opts_struct_matches_header():
+    """_native.CreateOpts mirrors pbg_create_opts_t (struct_size first, then ints) and fills
+    struct_size with its own size (the versioning rule of pbg_create_v2)."""
+    src = open(HEADER).read()
+    body = src[src.rindex("typedef struct {", 0, src.index("} pbg_create_opts_t;")):src.index("} pbg_create_opts_t;")]
+    fields = re.findall(r"\b(uint32_t|int)\s+([a-z_0-9]+);", body)
+    ct = {"uint32_t": ctypes.c_uint32, "int": ctypes.c_int}
+    assert [(n, ct[t]) for t, n in fields] == list(_native.CreateOpts._fields_)
+    o = _native.CreateOpts(precision=64)
+    assert o.struct_size == ctypes.sizeof(_native.CreateOpts) and o.precision == 64 and o.kernel == -1
+
+
+@pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="libpbg_amd.so not built")
+def test_create_v2_refuses_bad_options_without_gpu():
+    """pbg_create_v2 validates its versioned options before it touches a device: a struct_size that
+    is no pbg_create_opts_t size and a precision other than 32 / 64 are PBG_E_ARG."""
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    for o in (_native.CreateOpts(precision=16), _native.CreateOpts(precision=64)):
+        if o.precision == 64:
+            o.struct_size = 4  # shorter than struct_size + precision
+        rc = L.pbg_create_v2(b"AntPyBulletEnv-v0", 4, 0, 0, 0, None, ctypes.byref(o), ctypes.byref(h))
+        assert rc == -1, rc
+        assert not h.value
