@@ -132,14 +132,14 @@ def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None
     oA = np.concatenate(obsA) if obsA else np.zeros(1)
     rB = np.concatenate(spreadB) if spreadB else np.zeros(1)
     rec = dict(test=name or f"f64_teacher_forced[{env_id},{n}x{steps}]", env_steps=n_all, classA_frac=nA / n_all,
-               classA_state_share_within_1e-9=float((eA <= STATE_REL64).mean()), classA_state_max_rel=float(eA.max()),
+               classA_state_share_within_1e_9=float((eA <= STATE_REL64).mean()), classA_state_max_rel=float(eA.max()),
                classA_state_p50_rel=float(np.median(eA)), classA_reward_max_rel=float(rA.max()),
                classA_obs_max_rel=float(oA.max()), classA_done_mismatch=dmis, classA_contact_count_mismatch=cmis,
                classB_frac=nB / n_all, classB_ratio_to_spread_p99=float(np.percentile(rB, 99)),
                classC_frac=nC / n_all)
     _report(rec)
     assert nA > 0
-    assert rec["classA_state_share_within_1e-9"] >= SHARE64 and rec["classA_state_max_rel"] <= HARD_MAX64, rec
+    assert rec["classA_state_share_within_1e_9"] >= SHARE64 and rec["classA_state_max_rel"] <= HARD_MAX64, rec
     assert float((rA <= STATE_REL64).mean()) >= SHARE64, rec
     assert rec["classA_obs_max_rel"] <= 1.01 * OBS_ULP, rec
     assert dmis == 0 and cmis == 0, rec
