@@ -38,17 +38,23 @@ ENVS_PER_GPU = 16384
 ACTION_SEED = 0x5EED
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (non-matrix) peak
+FP64_PEAK_TFLOPS = 78.6  # MI355X spec sheet: FP64 vector peak (the guide lists no FP64 figure)
 SHORT = {"InvertedPendulumPyBulletEnv-v0": "pendulum", "HopperPyBulletEnv-v0": "hopper",
          "HalfCheetahPyBulletEnv-v0": "halfcheetah", "AntPyBulletEnv-v0": "ant",
          "HumanoidPyBulletEnv-v0": "humanoid", "Walker2DPyBulletEnv-v0": "walker2d"}
-# BASELINE.json configs timed beside the headline (per-GPU env counts)
-EXTRA_LEGS = "HumanoidPyBulletEnv-v0:4096,HopperPyBulletEnv-v0:4096,HalfCheetahPyBulletEnv-v0:8192"
+# BASELINE.json configs timed beside the headline (per-GPU env counts); a third field 64 = the
+# reference-precision (float64 physics) handle of that config
+EXTRA_LEGS = ("AntPyBulletEnv-v0:16384:64,HumanoidPyBulletEnv-v0:4096:64,"
+              "HumanoidPyBulletEnv-v0:4096,HopperPyBulletEnv-v0:4096,HalfCheetahPyBulletEnv-v0:8192")
 
 
-def alg_bytes_per_env_step(info):
+def alg_bytes_per_env_step(info, precision=32):
     """Minimum HBM bytes per env-step (BASELINE.md section 4 / SURVEY.md 8d): 4 * (2S + n + D + 2),
-    S = 13 (floating base) + 2 * joint dofs + 6 per-env scalars; Ant: S = 35 -> 432 B."""
+    S = 13 (floating base) + 2 * joint dofs + 6 per-env scalars; Ant: S = 35 -> 432 B.  The float64
+    handle reads and writes its state in 8-byte words: 8 * 2S + 4 * (n + D + 2) (Ant 712 B)."""
     S = 13 * int(info.floating) + 2 * info.n_joints + 6
+    if precision == 64:
+        return 8 * 2 * S + 4 * (info.action_dim + info.obs_dim + 2)
     return 4 * (2 * S + info.action_dim + info.obs_dim + 2)
 
 
@@ -183,7 +189,8 @@ def kernel_name(env):
     lpe = env.info.lanes_per_env
     k = {1: "pbg::step_kernel", 4: "pbg::team_step_kernel", 16: "pbg::gang_step_kernel",
          32: "pbg::gang_step_kernel"}.get(lpe, "pbg::step_kernel")
-    return f"{k}<{env.env_id}>"
+    f64 = getattr(env, "precision", 32) == 64
+    return f"{k}<{'F64<' if f64 else ''}{env.env_id}{'>' if f64 else ''}>"
 
 
 class DryRunEnv:
@@ -292,12 +299,15 @@ def timed_rollout(make_env, env_id, n, steps, warmup, preroll, dev, rank, world,
 
 def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
     """value / roofline block of one workload (HBM line from the algorithmic bytes; FP32 line
-    from the counted flops when profiles/flops_per_env_step.json has the robot)."""
+    from the counted flops when profiles/flops_per_env_step.json has the robot; float64 handles:
+    the same counted flops against the FP64 vector peak)."""
     import torch
-    alg = alg_bytes_per_env_step(env.info)
+    prec = getattr(env, "precision", 32)
+    alg = alg_bytes_per_env_step(env.info, prec)
     achieved = alg * n / (kernel_ms * 1e-3) / 1e9
-    pmc = load_pmc(env.env_id, n)
+    pmc = load_pmc(env.env_id, n) if prec == 32 else None
     d = {"env": env.env_id, "envs_per_gpu": n, "global_envs": world * n, "steps": steps,
+         "dtype": "f64" if prec == 64 else "f32",
          "value": world * n * steps / elapsed, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
          "kernel": kernel_name(env), "kernel_ms": kernel_ms, "occupancy": occupancy(env),
          "obs_finite": bool(torch.isfinite(env.obs).all()),
@@ -309,12 +319,13 @@ def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
                       "kernel": kernel_name(env), "kernel_ms": kernel_ms, "alg_bytes_per_env_step": alg,
                       # the step is FP32-VALU (issue / latency) bound, not HBM bound (SURVEY.md 8d,
                       # BASELINE.md 4): the binding roofline is the `flop_roofline` block beside this one
-                      "binding": "valu-fp32", "binding_line": "flop_roofline"}}
+                      "binding": "valu-fp64" if prec == 64 else "valu-fp32", "binding_line": "flop_roofline"}}
     f = flops.get(SHORT.get(env.env_id, env.env_id))
     if f:
+        peak = FP64_PEAK_TFLOPS if prec == 64 else FP32_PEAK_TFLOPS
         tf = f["flops_per_env_step"] * n / (kernel_ms * 1e-3) / 1e12
-        d["flop_roofline"] = {"bound": "valu-fp32", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": tf / FP32_PEAK_TFLOPS, "flops_per_env_step": f["flops_per_env_step"],
+        d["flop_roofline"] = {"bound": "valu-fp64" if prec == 64 else "valu-fp32", "achieved": tf, "peak": peak,
+                              "unit": "TFLOP/s", "frac": tf / peak, "flops_per_env_step": f["flops_per_env_step"],
                               "source": "pybullet-gym_amd/perf/flops_per_env_step.json (counted, tools/count_flops.py)"}
     if pmc and pmc.get("valu_insts_per_launch"):
         d["valu_roofline"] = valu_roofline(pmc, kernel_ms, n)
@@ -342,6 +353,8 @@ def main():
     ap.add_argument("--dry-run-cpu", action="store_true", help="CI: N > 1 control flow on CPU/gloo, no physics")
     ap.add_argument("--gang-lanes", type=int, default=-1,
                     help="A/B: gang width for the gang-kernel robots (16 or 32; -1 = the plan's choice)")
+    ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
+                    help="the headline handle's physics precision (64: float64, the reference's btScalar)")
     args = ap.parse_args()
     if args.second_env == "none":
         args.legs = "none"
@@ -368,10 +381,11 @@ def main():
     if not args.dry_run_cpu:
         from pybulletgym_amd.vec_env import VecEnv
 
-        def make_env(env_id, n, dev, seed, env_offset, autoreset):
-            lanes = args.gang_lanes if env_id.startswith("Humanoid") else -1
+        def make_env(env_id, n, dev, seed, env_offset, autoreset, precision=None):
+            precision = precision or args.precision
+            lanes = args.gang_lanes if env_id.startswith("Humanoid") and precision == 32 else -1
             return VecEnv(env_id, n, device=dev, seed=seed, env_offset=env_offset, autoreset=autoreset,
-                          gang_lanes=lanes)
+                          gang_lanes=lanes, precision=precision)
 
     flops = load_flops()
     n = args.envs_per_gpu
@@ -394,12 +408,15 @@ def main():
     legs = {}
     if args.legs not in ("", "none"):
         for spec in args.legs.split(","):
-            eid, cnt = spec.split(":")
-            if eid == args.env:
+            eid, cnt, *pr = spec.split(":")
+            prec = int(pr[0]) if pr else 32
+            if (eid, int(cnt), prec) == (args.env, n, args.precision) or (args.dry_run_cpu and prec != 32):
                 continue
-            e2, el2, km2, _, _ = timed_rollout(make_env, eid, int(cnt), args.leg_steps, min(args.warmup, 20),
+            mk = (lambda *a, _p=prec: make_env(*a, precision=_p)) if not args.dry_run_cpu else make_env
+            e2, el2, km2, _, _ = timed_rollout(mk, eid, int(cnt), args.leg_steps, min(args.warmup, 20),
                                                args.preroll, dev, rank, world, args.no_graph)
-            legs[SHORT.get(eid, eid)] = leg_summary(e2, world, int(cnt), args.leg_steps, el2, km2, flops)
+            legs[SHORT.get(eid, eid) + ("_f64" if prec == 64 else "")] = \
+                leg_summary(e2, world, int(cnt), args.leg_steps, el2, km2, flops)
             e2.close()
 
     if rank == 0:
@@ -416,7 +433,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64" if args.precision == 64 else "f32",
             "data": "synthetic: Philox4x32-10 U(-1,1) float32 actions (key 0x5EED, counter (step, global env)) "
                     "generated in HBM before the timed region; robot compiled from the reference MJCF",
             "config": {"workload": f"{args.env} random-action rollout, auto-reset (TimeLimit 1000)",

@@ -100,8 +100,11 @@ typedef struct {
                      every walker (Ant included); -1 / 1: default (quad for Ant, gang otherwise) */
   int lds_rows;   /* k >= 0: at most k contact rows (gang: contacts) per env resident in LDS,
                      the rest in the device workspace (bitwise-equality tests of that path) */
-  int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics */
-  int gang_lanes; /* 16 / 32: gang width (32: the Humanoid family only; PBG_E_HIP for the others) */
+  int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics (PBG_E_ARG when the planned
+                     kernel is no gang kernel or has no such variant: 32-lane gangs and
+                     HumanoidFlagrunHarder are distributed only) */
+  int gang_lanes; /* 16 / 32: gang width (32: the Humanoid family only); PBG_E_ARG when the planned
+                     kernel is not a gang kernel of that width (Ant's quad plan, kernel = 0) */
 } pbg_debug_opts_t;
 
 /* Scene / World parameters (scene_bases.py:8-18 Scene(gravity, timestep, frame_skip), 58-73

@@ -260,6 +260,24 @@ int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int
     delete h;
     return PBG_E_HIP;
   }
+  // diagnostic options that the chosen kernel cannot honour are refused, not ignored: an A/B
+  // run must never measure another kernel than the one it asked for
+  const char* bad = nullptr;
+  if (!e && opts->gang_lanes == 32 && h->geo.team != 32)
+    bad = "gang_lanes = 32 needs the 32-lane gang kernel (the Humanoid family on the default / gang plan)";
+  else if (e && opts->gang_lanes == 32)
+    bad = "gang_lanes = 32: this robot has no 32-lane gang kernel";
+  else if (!e && opts->gang_lanes == 16 && h->geo.team != 16)
+    bad = "gang_lanes = 16 needs a gang plan (kernel = 0 and Ant's quad plan are not gang kernels)";
+  else if (!e && (opts->gang_dist == 0 || opts->gang_dist == 1) && h->geo.team < 16)
+    bad = "gang_dist applies to the gang kernel only";
+  else if (!e && (opts->gang_dist == 0 || opts->gang_dist == 1) && h->geo.gang_dist != opts->gang_dist)
+    bad = "gang_dist: this robot / gang width has no replicated-dynamics variant";
+  if (bad) {
+    snprintf(g_err, sizeof(g_err), "pbg_create: %s", bad);
+    delete h;
+    return PBG_E_ARG;
+  }
   // cap on the LDS-resident contact rows (tests of the device-workspace path)
   if (opts && opts->lds_rows >= 0 && opts->lds_rows < h->geo.lds_rows) h->geo.lds_rows = opts->lds_rows;
   const size_t wb = co.precision == 64 ? sizeof(double) : sizeof(float);  // state / z0 / workspace word

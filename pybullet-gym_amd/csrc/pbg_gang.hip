@@ -63,13 +63,17 @@ PBG_DEV float dpp_f(float x) {
 // gfx950 v_permlane16_swap_b32 a, b: the odd rows of a trade places with the even rows of b.
 // With a = b = x (x uniform within each row) a ends up holding the even row's value and b the odd
 // row's, in both rows of each pair.  Inline asm because this ROCm's builtin
-// (__builtin_amdgcn_permlane16_swap) returns the first register for both of its results; the
-// s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see inside the asm.
+// (__builtin_amdgcn_permlane16_swap) returns the first register for both of its results.  The
+// compiler's hazard recognizer cannot see inside the asm, so the s_nop 3 (4 wait states) covers
+// both hazards a preceding VALU instruction can leave for a permlane: a VALU write of an operand
+// register, and a VALU write of EXEC (v_cmpx) -- the latter needs 4 wait states on gfx950.
+// gang_sum<32> is only called from the 32-lane kernel's row reductions, all reached with the
+// gang's full EXEC mask (wave-uniform control flow).
 PBG_DEV void row_pair_swap(float& a, float& b) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  asm volatile("s_nop 3\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
 PBG_DEV void row_pair_swap_u(uint32_t& a, uint32_t& b) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  asm volatile("s_nop 3\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
 // all-reduce over the T (4, 8, 16 or 32) lanes of a DPP row segment (T = 32: a row pair);
 // identical bits in every lane (each step adds a value and its mirror image: a + b == b + a;

@@ -216,9 +216,9 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
   }
 }
 
-// mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers);
-// 2 = gang for every walker (parity tests of the gang kernel on Ant).  HumanoidFlagrunHarder
-// (a second free body per env) runs on the lane kernel only.
+// mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers -- HumanoidFlagrunHarder
+// and Atlas included: the cube robot runs the gang kernel's front path, distributed dynamics only);
+// 2 = gang for every walker (parity tests of the gang kernel on Ant).
 int PBG_FN(plan_)(int n_envs, int cus, int mode, Geometry* g) {
   if (Team<R>::ok && mode == 1) return plan_team<R>(n_envs, cus, g);
   if (R::kind != 1 && (mode >= 1 || !lane_ok<R>())) return plan_gang<R>(n_envs, cus, g, g->gang_lanes);

@@ -7,15 +7,16 @@ arithmetic, with IEEE division / sqrt and the device library's sin / cos.  Again
 oracle the remaining differences are float64 rounding (summation orders, the kernels' inertia-
 about-O formulation of M), so the bounds here are nine orders tighter than the float32 tests':
 
-  * teacher-forced env steps, split like tests/test_gpu.py (same contact-set signature and
-    discrete reward terms; conditioning probes at PROBE_REL64 = 1e-12 relative): class A --
-    the float64 STATE after the step (pbg_get_state) within STATE_REL64 = 1e-9 relative of the
-    oracle's in >= 99.9 % of the env-steps with a hard maximum of 1e-6, the float64 reward within
-    1e-9, the float32 observation equal to the oracle's float32 observation up to one float32
-    rounding (2^-23 relative: both round float64 values that agree to ~1e-15), done flags and
-    contact counts identical; class B (the oracle's own 1e-12 perturbation spread above 1e-10) at
-    most 10 % of the env-steps, within 10 x that spread at the 99th percentile; class C (another
-    contact set) at most 1 %.
+  * teacher-forced env steps, split like tests/test_gpu.py by discrete state (same contact-set
+    signature and discrete reward terms) and reported by conditioning (probes at PROBE_REL64 =
+    1e-12 relative; class B: the oracle's own spread above 1e-10).  Unlike the float32 tests,
+    conditioning exempts nothing: EVERY env-step with the oracle's discrete state (classes A and
+    B) must have the float64 STATE after the step (pbg_get_state) within STATE_REL64 = 1e-9
+    relative of the oracle's in >= 99.9 % of the env-steps, with a hard maximum of 1e-6; the
+    float64 reward within 1e-9; the float32 observation equal to the oracle's float32 observation
+    up to one float32 rounding (2^-23 relative: both round float64 values that agree to ~1e-15);
+    done flags and contact counts identical.  Class C (another contact set) at most 1 %.
+    (First GPU run, r05b: every env id's largest state error 4.3e-12, class C empty.)
   * free running at the north-star horizon: from the same float64 reset state and the same 1,000
     action batches the float64 GPU leaves the float64 oracle's trajectory (obs error above 1e-4)
     far later than float32 arithmetic of the same algorithm does (the oracle's IEEE-float32
@@ -42,7 +43,7 @@ HARD_MAX64 = 1e-6
 SHARE64 = 0.999
 OBS_ULP = 2.0 ** -23
 PROBE_REL64, PROBE_ABS64, COND_EPS64 = 1e-12, 1e-14, 1e-10
-COND_FRAC64, LOOSE_FRAC64, SPREAD_RATIO64 = 0.10, 0.01, 10.0
+LOOSE_FRAC64 = 0.01
 F64_FREE_FACTOR = 2.0
 
 
@@ -109,9 +110,9 @@ def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None
             cond &= spread <= COND_EPS64
             same = (sg == orc.csig) & (_discrete_terms(tg, kind) == _discrete_terms(orc.terms, kind)).all(axis=1)
             live = ~done_g.index_select(0, tidx).cpu().numpy()  # the GPU auto-reset the others' state
-            A = same & cond
-            B = same & ~cond
-            nA += int(A.sum())
+            A = same  # every env-step of the oracle's discrete state is held to the bound
+            B = same & ~cond  # (reported: ill conditioned at 1e-12)
+            nA += int((same & cond).sum())
             nB += int(B.sum())
             nC += int((~same).sum())
             serr = _state_rel(sgpu, orc.state)
@@ -132,18 +133,17 @@ def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None
     oA = np.concatenate(obsA) if obsA else np.zeros(1)
     rB = np.concatenate(spreadB) if spreadB else np.zeros(1)
     rec = dict(test=name or f"f64_teacher_forced[{env_id},{n}x{steps}]", env_steps=n_all, classA_frac=nA / n_all,
-               classA_state_share_within_1e_9=float((eA <= STATE_REL64).mean()), classA_state_max_rel=float(eA.max()),
-               classA_state_p50_rel=float(np.median(eA)), classA_reward_max_rel=float(rA.max()),
-               classA_obs_max_rel=float(oA.max()), classA_done_mismatch=dmis, classA_contact_count_mismatch=cmis,
-               classB_frac=nB / n_all, classB_ratio_to_spread_p99=float(np.percentile(rB, 99)),
-               classC_frac=nC / n_all)
+               classB_frac=nB / n_all, classC_frac=nC / n_all,
+               same_state_share_within_1e_9=float((eA <= STATE_REL64).mean()), same_state_max_rel=float(eA.max()),
+               same_state_p50_rel=float(np.median(eA)), same_reward_max_rel=float(rA.max()),
+               same_obs_max_rel=float(oA.max()), same_done_mismatch=dmis, same_contact_count_mismatch=cmis,
+               classB_ratio_to_spread_p99=float(np.percentile(rB, 99)))
     _report(rec)
-    assert nA > 0
-    assert rec["classA_state_share_within_1e_9"] >= SHARE64 and rec["classA_state_max_rel"] <= HARD_MAX64, rec
+    assert nA + nB > 0
+    assert rec["same_state_share_within_1e_9"] >= SHARE64 and rec["same_state_max_rel"] <= HARD_MAX64, rec
     assert float((rA <= STATE_REL64).mean()) >= SHARE64, rec
-    assert rec["classA_obs_max_rel"] <= 1.01 * OBS_ULP, rec
+    assert rec["same_obs_max_rel"] <= 1.01 * OBS_ULP, rec
     assert dmis == 0 and cmis == 0, rec
-    assert rec["classB_frac"] <= COND_FRAC64 and rec["classB_ratio_to_spread_p99"] <= SPREAD_RATIO64, rec
     assert rec["classC_frac"] <= LOOSE_FRAC64, rec
     return rec
 

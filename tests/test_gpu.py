@@ -577,8 +577,14 @@ def test_config_parity_1000_steps(env_id, n, sample):
 # 1e-4 (and 1e-2), for the GPU and for the oracle's IEEE float32 instantiation.  Asserted: the
 # GPU's median divergence step is at least FREE_MEDIAN_FACTOR x float32's at both thresholds, and
 # done flags and contact counts equal float64's in every env-step before the earlier of the two
-# 1e-4 divergence steps of that env.
+# 1e-4 divergence steps of that env.  This is a proxy: the literal north-star bound (1e-4 over all
+# 1,000 steps) is met by no float32 implementation of these dynamics, this one included (DESIGN.md
+# 6; the float64 path, tests/test_f64.py, holds it far longer).  After divergence the trajectories
+# are independent samples of the same dynamics, so the rest of the horizon is checked as
+# distributions: per env, the first step with done set and the mean contact count over
+# the 1,000 steps, GPU against the float64 oracle, two-sample Kolmogorov-Smirnov p >= FREE_KS_P.
 FREE_MEDIAN_FACTOR = 0.8
+FREE_KS_P = 0.01
 FREE_CONFIGS = [("AntPyBulletEnv-v0", 16384, 512), ("HumanoidPyBulletEnv-v0", 4096, 192)]
 
 
@@ -606,6 +612,8 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
     err = {k: np.zeros((steps, sample)) for k in ("gpu", "f32")}
     dmis = np.zeros((steps, sample), bool)
     cmis = np.zeros((steps, sample), bool)
+    done_hist = {k: np.zeros((steps, sample), bool) for k in ("gpu", "f64")}
+    cnt_hist = {k: np.zeros((steps, sample)) for k in ("gpu", "f64")}
     t0 = time.time()
     for t in range(steps):
         if t % 100 == 0:
@@ -621,6 +629,8 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
         err["f32"][t] = _rel(o32, o64)
         dmis[t] = dg != d64.astype(bool)
         cmis[t] = cg != c64
+        done_hist["gpu"][t], done_hist["f64"][t] = dg, d64.astype(bool)
+        cnt_hist["gpu"][t], cnt_hist["f64"][t] = cg, c64
     env.close()
     rec = dict(test=f"free_running[{env_id},{n},{sample}x{steps}]")
     first = {}
@@ -640,11 +650,21 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
     before32 = np.arange(steps)[:, None] < first[("f32", 1e-4)][None, :]
     rec["done_mismatch_before_f32_divergence"] = int((dmis & before32).sum())
     rec["contact_count_mismatch_before_f32_divergence"] = int((cmis & before32).sum())
+    # the whole horizon as distributions: first done step (steps = never) and mean contact count per env
+    from scipy import stats
+    fd = {k: _first_exceed(done_hist[k].astype(float), 0.5) for k in ("gpu", "f64")}
+    mc = {k: cnt_hist[k].mean(axis=0) for k in ("gpu", "f64")}
+    rec["first_done_mean_gpu_f64"] = [float(fd["gpu"].mean()), float(fd["f64"].mean())]
+    rec["mean_contacts_gpu_f64"] = [float(mc["gpu"].mean()), float(mc["f64"].mean())]
+    same_fd = (fd["gpu"] == fd["f64"]).all()
+    rec["ks_p_first_done"] = 1.0 if same_fd else float(stats.ks_2samp(fd["gpu"], fd["f64"]).pvalue)
+    rec["ks_p_mean_contacts"] = float(stats.ks_2samp(mc["gpu"], mc["f64"]).pvalue)
     _report(rec)
     for thr in (1e-4, 1e-2):
         g, f = np.median(first[("gpu", thr)]), np.median(first[("f32", thr)])
         assert g >= FREE_MEDIAN_FACTOR * f, (thr, g, f, rec)
     assert rec["done_mismatch_before_divergence"] == 0 and rec["contact_count_mismatch_before_divergence"] == 0, rec
+    assert rec["ks_p_first_done"] >= FREE_KS_P and rec["ks_p_mean_contacts"] >= FREE_KS_P, rec
 
 
 def test_free_running_short_horizon_ant():
@@ -1161,3 +1181,15 @@ def test_sim_params_flagrun_timeout_follows_frame_skip():
             np.testing.assert_array_equal(aux[:, 4 + NF:], orc.aux[:, 4 + NF:])
         finally:
             oracle.set_sim_params(None)
+
+
+@pytest.mark.parametrize("opts", [{"gang_lanes": 32}, {"gang_lanes": 16}, {"kernel": 0, "gang_lanes": 32},
+                                  {"kernel": 0, "gang_dist": 0}, {"gang_lanes": 32, "gang_dist": 0}])
+def test_debug_options_the_plan_cannot_honour_are_refused(opts):
+    """gang_lanes = 32 for Ant (quad plan) or with kernel = 0, gang_lanes = 16 on the quad
+    plan, gang_dist on the lane kernel, and replicated dynamics on 32-lane gangs are PBG_E_ARG --
+    never a silent run of another kernel."""
+    from pybulletgym_amd._native import PbgError
+    env_id = "HumanoidPyBulletEnv-v0" if opts.get("gang_dist") == 0 and "kernel" not in opts else "AntPyBulletEnv-v0"
+    with pytest.raises(PbgError, match="pbg_create"):
+        VecEnv(env_id, 64, **opts)
