@@ -52,13 +52,21 @@ namespace pbg {
 // not fit, and one-wave workgroups (87 KB: one per CU) left three SIMDs of each CU idle
 // (4.72 -> 3.05 ms per step at 4,096 envs, A/B)
 template <class R>
-constexpr int gang_block() { return PBG_GANG_BLOCK; }
+constexpr int gang_block();  // (after the layout: the float64 regions decide it)
 
 // bound_ctrl set: every permutation used here reads a valid lane, and with it the
 // compiler folds `x + mov_dpp(x)` into one v_add_f32_dpp (no mov, no DPP hazard nop).
 template <int CTRL>
 PBG_DEV float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+// float64: the two dwords moved by the same permutation
+template <int CTRL>
+PBG_DEV double dpp_f(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 // gfx950 v_permlane16_swap_b32 a, b: the odd rows of a trade places with the even rows of b.
 // With a = b = x (x uniform within each row) a ends up holding the even row's value and b the odd
@@ -75,23 +83,39 @@ PBG_DEV void row_pair_swap(float& a, float& b) {
 PBG_DEV void row_pair_swap_u(uint32_t& a, uint32_t& b) {
   asm volatile("s_nop 3\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
+PBG_DEV void row_pair_swap(double& a, double& b) {  // the two dwords of each
+  uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  uint32_t al = (uint32_t)ua, ah = (uint32_t)(ua >> 32), bl = (uint32_t)ub, bh = (uint32_t)(ub >> 32);
+  row_pair_swap_u(al, bl);
+  row_pair_swap_u(ah, bh);
+  a = __builtin_bit_cast(double, ((uint64_t)ah << 32) | al);
+  b = __builtin_bit_cast(double, ((uint64_t)bh << 32) | bl);
+}
 // all-reduce over the T (4, 8, 16 or 32) lanes of a DPP row segment (T = 32: a row pair);
 // identical bits in every lane (each step adds a value and its mirror image: a + b == b + a;
 // the row-pair step adds the even row's sum to the odd row's in that order in both rows)
-template <int T>
-PBG_DEV float gang_sum(float x) {
+template <int T, class V>
+PBG_DEV V gang_sum(V x) {
   x = x + dpp_f<0xB1>(x);  // quad_perm [1,0,3,2]
   x = x + dpp_f<0x4E>(x);  // quad_perm [2,3,0,1]
   if constexpr (T >= 8) x = x + dpp_f<0x141>(x);   // row_half_mirror
   if constexpr (T >= 16) x = x + dpp_f<0x140>(x);  // row_mirror
   if constexpr (T >= 32) {
-    float a = x, b = x;
+    V a = x, b = x;
     row_pair_swap(a, b);  // a: the even row's value, b: the odd row's, in both rows of the pair
     x = a + b;
   }
   return x;
 }
 PBG_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
+// a 32-bit chain mask stored in a word of the contact descriptor (its bits, not a number)
+template <class S>
+PBG_DEV S mask_word(uint32_t m) {
+  if constexpr (sizeof(S) == 8) return __builtin_bit_cast(S, (uint64_t)m);
+  else return __builtin_bit_cast(S, m);
+}
+PBG_DEV uint32_t word_mask(float w) { return __builtin_bit_cast(uint32_t, w); }
+PBG_DEV uint32_t word_mask(double w) { return (uint32_t)__builtin_bit_cast(uint64_t, w); }
 template <int CTRL>
 PBG_DEV uint32_t dpp_u(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
@@ -123,19 +147,20 @@ constexpr int gang_waves_per_simd() { return T >= 32 ? 2 : 1; }
 // ------------------------------------------------------------------ constant tables
 template <class R>
 struct GangTab {
+  using Sc = real_t<R>;
   static constexpr int NS1 = R::NS > 0 ? R::NS : 1, NP1 = R::NPAIR > 0 ? R::NPAIR : 1;
   static constexpr int NG1 = R::NG > 0 ? R::NG : 1, NB = R::NL + 1;
   static constexpr int NL1 = Dims<R>::NLIM > 0 ? Dims<R>::NLIM : 1;
-  float gp0[NG1][4];   // capsule end 0 | radius
-  float gp1[NG1][4];   // capsule end 1
+  Sc gp0[NG1][4];   // capsule end 0 | radius
+  Sc gp1[NG1][4];   // capsule end 1
   int geom_body[NG1];
   int pga[NP1], pgb[NP1];
-  float pmu[NP1], pbound2[NP1];
+  Sc pmu[NP1], pbound2[NP1];
   uint32_t chain[NB];  // joint dofs moving body b (0: the base)
   int lim_g[NL1];      // generalized index of limit row li
   // floor slots last: robots with many (Atlas) keep them out of the workgroup's LDS copy
-  float slot[NS1][4];  // point (link frame) | radius
-  float slot_mu[NS1];
+  Sc slot[NS1][4];  // point (link frame) | radius
+  Sc slot_mu[NS1];
   int slot_body[NS1];
 };
 // The gang kernel records floor contact for the first 64 slots only (the slot pass's 64-bit
@@ -158,20 +183,20 @@ constexpr GangTab<R> make_gang_tab() {
   using D = Dims<R>;
   GangTab<R> t{};
   for (int s = 0; s < R::NS; s++) {
-    for (int c = 0; c < 3; c++) t.slot[s][c] = (float)R::slot_point[s][c];
-    t.slot[s][3] = (float)R::slot_radius[s];
-    t.slot_mu[s] = (float)R::slot_mu[s];
+    for (int c = 0; c < 3; c++) t.slot[s][c] = (real_t<R>)R::slot_point[s][c];
+    t.slot[s][3] = (real_t<R>)R::slot_radius[s];
+    t.slot_mu[s] = (real_t<R>)R::slot_mu[s];
     t.slot_body[s] = R::slot_link[s] + 1;
   }
   for (int g = 0; g < R::NG; g++) {
-    for (int c = 0; c < 3; c++) { t.gp0[g][c] = (float)R::geom_p0[g][c]; t.gp1[g][c] = (float)R::geom_p1[g][c]; }
-    t.gp0[g][3] = (float)R::geom_r[g];
+    for (int c = 0; c < 3; c++) { t.gp0[g][c] = (real_t<R>)R::geom_p0[g][c]; t.gp1[g][c] = (real_t<R>)R::geom_p1[g][c]; }
+    t.gp0[g][3] = (real_t<R>)R::geom_r[g];
     t.geom_body[g] = R::geom_link[g] + 1;
   }
   for (int p = 0; p < R::NPAIR; p++) {
     t.pga[p] = R::pair_ga[p];
     t.pgb[p] = R::pair_gb[p];
-    t.pmu[p] = (float)R::pair_mu[p];
+    t.pmu[p] = (real_t<R>)R::pair_mu[p];
     t.pbound2[p] = D::PAIR_BOUND2.v[p][0];
   }
   t.chain[0] = 0;
@@ -185,15 +210,16 @@ __constant__ GangTab<R> g_gang_tab = make_gang_tab<R>();
 // body tree for the distributed dynamics: body 0 = base, body l+1 = link l
 template <class R>
 struct GangDynTab {
+  using Sc = real_t<R>;
   static constexpr int NB = R::NL + 1, N = R::NDOF, NNZ = Dims<R>::NNZ, NJ1 = R::NJ > 0 ? R::NJ : 1;
   int parent[NB], jt[NB], dof[NB];
   int lev_start[NB + 2], lev_body[NB];  // bodies grouped by depth
   int child_start[NB + 1], child[NB];
-  float ro[NB][9], opos[NB][3], axis[NB][3], anchor[NB][3], com[NB][3], mass[NB], inertia[NB][6];
+  Sc ro[NB][9], opos[NB][3], axis[NB][3], anchor[NB][3], com[NB][3], mass[NB], inertia[NB][6];
   int me_i[NNZ], me_k[NNZ], me_b[NNZ];  // packed lower-triangle entries of M: rows, cols, composite
-  float me_arm[NNZ];                     // armature on joint diagonals
+  Sc me_arm[NNZ];                     // armature on joint diagonals
   int g_body[N], g_dof[N];               // composite owning generalized index i; its joint dof (-1: base)
-  float damping[NJ1], stiffness[NJ1];
+  Sc damping[NJ1], stiffness[NJ1];
 };
 template <class R>
 constexpr int body_depth(int b) {
@@ -216,20 +242,20 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
     t.parent[b] = b == 0 ? -1 : R::link_parent[b - 1] + 1;
     t.jt[b] = b == 0 ? 4 : R::link_jtype[b - 1];
     t.dof[b] = b == 0 ? -1 : R::link_dof[b - 1];
-    t.mass[b] = (float)D::body_mass(b);
-    for (int i = 0; i < 6; i++) t.inertia[b][i] = (float)(b == 0 ? R::base_inertia[i] : R::link_inertia[b - 1][i]);
+    t.mass[b] = (real_t<R>)D::body_mass(b);
+    for (int i = 0; i < 6; i++) t.inertia[b][i] = (real_t<R>)(b == 0 ? R::base_inertia[i] : R::link_inertia[b - 1][i]);
     if (b > 0) {
       const int l = b - 1;
       const double x = R::link_offset_quat[l][0], y = R::link_offset_quat[l][1], z = R::link_offset_quat[l][2], w = R::link_offset_quat[l][3];
       const double m[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
                            2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
                            2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
-      for (int i = 0; i < 9; i++) t.ro[b][i] = (float)m[i];
+      for (int i = 0; i < 9; i++) t.ro[b][i] = (real_t<R>)m[i];
       for (int c = 0; c < 3; c++) {
-        t.opos[b][c] = (float)R::link_offset_pos[l][c];
-        t.axis[b][c] = (float)R::link_axis[l][c];
-        t.anchor[b][c] = (float)R::link_anchor[l][c];
-        t.com[b][c] = (float)R::link_com[l][c];
+        t.opos[b][c] = (real_t<R>)R::link_offset_pos[l][c];
+        t.axis[b][c] = (real_t<R>)R::link_axis[l][c];
+        t.anchor[b][c] = (real_t<R>)R::link_anchor[l][c];
+        t.com[b][c] = (real_t<R>)R::link_com[l][c];
       }
     }
   }
@@ -258,7 +284,7 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
         t.me_i[e] = a;
         t.me_k[e] = b;
         t.me_b[e] = dk >= 0 ? R::dof_link[dk] + 1 : 0;
-        t.me_arm[e] = (a == b && da >= 0) ? (float)R::dof_armature[da] : 0.f;
+        t.me_arm[e] = (a == b && da >= 0) ? (real_t<R>)R::dof_armature[da] : 0.f;
       }
   for (int i = 0; i < R::NDOF; i++) {
     const int di = D::dof_of(i);
@@ -266,8 +292,8 @@ constexpr GangDynTab<R> make_gang_dyn_tab() {
     t.g_body[i] = di >= 0 ? R::dof_link[di] + 1 : 0;
   }
   for (int d = 0; d < R::NJ; d++) {
-    t.damping[d] = (float)R::dof_damping[d];
-    t.stiffness[d] = (float)R::dof_stiffness[d];
+    t.damping[d] = (real_t<R>)R::dof_damping[d];
+    t.stiffness[d] = (real_t<R>)R::dof_stiffness[d];
   }
   return t;
 }
@@ -300,7 +326,7 @@ struct LevSrc {
   static constexpr int at(int k) { return GangDT<R>::v.lev_body[K0 + k]; }
 };
 template <class R, int K0, int KN, class F>
-PBG_DEV float lvsel(int t, F&& fn) { return ksel<LevSrc<R, K0>, KN, float>(t, fn); }
+PBG_DEV real_t<R> lvsel(int t, F&& fn) { return ksel<LevSrc<R, K0>, KN, real_t<R>>(t, fn); }
 template <class R, int K0, int KN, class F>
 PBG_DEV int lvsel_i(int t, F&& fn) { return ksel<LevSrc<R, K0>, KN, int>(t, fn); }
 // opaque copy of the lane index: the lane compares of the selects stay where they are used
@@ -353,8 +379,9 @@ constexpr int lv_jt(int k0, int kn) {
   return j;
 }
 // A * B where B's entries may be compile-time constants (its zeros fold away)
-PBG_DEV m3 mul_kb(const m3& A, const m3& B) {
-  m3 C;
+template <class S>
+PBG_DEV M3<S> mul_kb(const M3<S>& A, const M3<S>& B) {
+  M3<S> C;
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
@@ -440,23 +467,26 @@ struct Gang {
 };
 
 // per-lane view of the env's LDS region and device workspace
-struct GangCtx {
-  lds_float* tabs;  // workgroup copy of GangTab<R> | GangDynTab<R>
-  lds_float* l;  // env LDS region
-  float* g;      // env device workspace
+template <class S>
+struct GangCtxT {
+  lds_float* tabs;  // workgroup copy of GangTab<R> | GangDynTab<R> (4-byte words)
+  lds_t<S>* l;   // env LDS region (words of the physics scalar S)
+  S* g;          // env device workspace
   int cap;       // contacts resident in LDS
 #ifdef PBG_DEV_CHECKS
   int env_words;  // the env region's words (contact_at's bound check)
 #endif
   int t;         // lane in the gang
   int le;        // gang in the wave
-  SimP P;        // scene parameters (kernel arguments)
+  SimPT<S> P;    // scene parameters (kernel arguments)
 };
+template <class R>
+using GangCtx = GangCtxT<real_t<R>>;
 // n words (n % 4 == 0) from / to a 16-byte aligned LDS address as b128 accesses (front path:
 // the composite records; the compiler split them into ds_read2_b32 pairs with an address add each)
-template <int n>
-PBG_DEV void lds_ld4(const lds_float* p, float* v) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
+template <int n, class S>
+PBG_DEV void lds_ld4(const lds_t<S>* p, S* v) {
+  typedef S v4f __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) const v4f lds_v4f;
 #pragma unroll
   for (int k = 0; k < n / 4; k++) {
@@ -464,18 +494,20 @@ PBG_DEV void lds_ld4(const lds_float* p, float* v) {
     v[4 * k] = a.x; v[4 * k + 1] = a.y; v[4 * k + 2] = a.z; v[4 * k + 3] = a.w;
   }
 }
-template <int n>
-PBG_DEV void lds_st4(lds_float* p, const float* v) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
+template <int n, class S>
+PBG_DEV void lds_st4(lds_t<S>* p, const S* v) {
+  typedef S v4f __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) v4f lds_v4f;
 #pragma unroll
   for (int k = 0; k < n / 4; k++) ((lds_v4f*)p)[k] = v4f{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
 }
 // word w (0..26) of body b's record: frame part (w < 12) or kinematic part
 template <class R, int T>
-PBG_DEV lds_float* body_word(const lds_float* l, int b, int w) {
+PBG_DEV lds_t<real_t<R>>* body_word(const lds_t<real_t<R>>* l, int b, int w) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
-  return (lds_float*)l + (w < G::FW ? G::O_FR + G::FW * b + w : G::O_KV + G::KW * b + (w - G::FW));
+  return (LW*)l + (w < G::FW ? G::O_FR + G::FW * b + w : G::O_KV + G::KW * b + (w - G::FW));
 }
 // model tables, copied once per workgroup into LDS (vector-memory loads of a __constant__
 // table indexed by lane cost hundreds of cycles each; the level loops chain several)
@@ -484,12 +516,23 @@ struct GangTabs {
   typedef __attribute__((address_space(3))) const GangTab<R> Tab;
   typedef __attribute__((address_space(3))) const GangDynTab<R> Dyn;
   static constexpr int TAB_COPY = (int)((gang_big<R>() ? offsetof(GangTab<R>, slot) : sizeof(GangTab<R>)) / 4);
-  static constexpr int TAB_WORDS = (TAB_COPY + 3) / 4 * 4;
-  static constexpr int DYN_WORDS = (int)((sizeof(GangDynTab<R>) + 15) / 16) * 4;
+  // 4-byte words; the tables end on a 16-byte (float32) or 32-byte (float64 regions: 4 words of 8
+  // bytes) boundary, the alignment the env regions after them need
+  static constexpr int AW = sizeof(real_t<R>) == 8 ? 8 : 4;
+  static constexpr int TAB_WORDS = (TAB_COPY + AW - 1) / AW * AW;
+  static constexpr int DYN_WORDS = (int)((sizeof(GangDynTab<R>) + 4 * AW - 1) / (4 * AW)) * AW;
   static constexpr int WORDS = TAB_WORDS + DYN_WORDS;
   static PBG_DEV Tab& tab(const lds_float* p) { return *(Tab*)p; }
   static PBG_DEV Dyn& dyn(const lds_float* p) { return *(Dyn*)(p + TAB_WORDS); }
 };
+// Lanes per workgroup: 4 waves of 16-lane gangs; the float64 path (F64<R>: every region word 8
+// bytes) takes 2 waves when 16 envs' fixed words and four contacts each would not fit one CU's LDS
+template <class R>
+constexpr int gang_block() {
+  using G = Gang<R, 16>;
+  constexpr long need = 4L * GangTabs<R>::WORDS + 16L * (long)sizeof(real_t<R>) * (G::FIXED + 4L * G::PERC);
+  return sizeof(real_t<R>) == 8 && need > 163840L ? PBG_GANG_BLOCK / 2 : PBG_GANG_BLOCK;
+}
 #define PBG_GANG_SYNC                                    \
   {                                                      \
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
@@ -501,6 +544,8 @@ struct GangTabs {
 // for the row addresses is a multi-pass instruction, two per normal row of the sweep)
 template <class R, int T>
 PBG_DEV int coff(int c) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   return (int)__umul24((unsigned)c, (unsigned)Gang<R, T>::PERC);
 }
 // f(p) with p the first word of contact c: its LDS record if resident, else its device
@@ -508,7 +553,9 @@ PBG_DEV int coff(int c) {
 // accessor left one divergent branch per word in the code: 442 branches in the detection
 // pass, 186 in the rows pass)
 template <class R, int T, class F>
-PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
+PBG_DEV void contact_at(const GangCtx<R>& X, int c, F&& f) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
 #ifdef PBG_DEV_CHECKS  // diagnostic build: a contact record inside its LDS region / workspace slice
   assert(c >= 0 && c < G::MAXC && (c >= X.cap || G::FIXED + (c + 1) * G::PERC <= X.env_words));
@@ -519,7 +566,9 @@ PBG_DEV void contact_at(const GangCtx& X, int c, F&& f) {
 
 // f(p) with p the first word of joint-limit row li (LDS, or the workspace for LIM_WS models)
 template <class R, int T, class F>
-PBG_DEV void limit_at(const GangCtx& X, int li, F&& f) {
+PBG_DEV void limit_at(const GangCtx<R>& X, int li, F&& f) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   if constexpr (G::LIM_WS) f(X.g + G::GW_LR + li * G::LRW);
   else f(X.l + G::O_LR + li * G::LRW);
@@ -529,18 +578,21 @@ PBG_DEV void limit_at(const GangCtx& X, int li, F&& f) {
 // pipelining): this lane's slice of y, m_eff, target, lambda.
 template <class R, int T>
 struct GRow {
-  float y[Gang<R, T>::NSL], meff, tgt, lam;
+  using Sc = real_t<R>;
+  Sc y[Gang<R, T>::NSL], meff, tgt, lam;
 };
 // row (c, dir); LDS: the caller knows every row of the wave is LDS-resident (no branch, so
 // the compiler's LDS wait before the next update counts only this row's loads)
 template <class R, int T, bool LDS>
-PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
+PBG_DEV void gang_load_row(const GangCtx<R>& X, int c, int dir, GRow<R, T>& r) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
-  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef Sc v2f __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) const v2f lds_v2f;
   const int w0 = G::RW0 + dir * G::CRW;
   if (LDS || c < X.cap) {
-    const lds_float* p = X.l + G::FIXED + coff<R, T>(c) + w0;
+    const LW* p = X.l + G::FIXED + coff<R, T>(c) + w0;
     if constexpr (G::Y64) {
       static_assert((G::FIXED + G::RW0) % 2 == 0 && G::PERC % 2 == 0 && G::CRW % 2 == 0, "b64 rows");
       const v2f a = *(lds_v2f*)(p + 2 * X.t);
@@ -551,7 +603,7 @@ PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
     }
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
   } else {
-    const float* p = X.g + coff<R, T>(c) + w0;
+    const Sc* p = X.g + coff<R, T>(c) + w0;
 #pragma unroll
     for (int m = 0; m < G::NSL; m++) r.y[m] = p[X.t * G::NSL + m];
     r.meff = p[G::YS]; r.tgt = p[G::YS + 1]; r.lam = p[G::YS + 2];
@@ -559,20 +611,24 @@ PBG_DEV void gang_load_row(const GangCtx& X, int c, int dir, GRow<R, T>& r) {
 }
 // friction bound of contact c: mu * lambda of its normal row
 template <class R, int T, bool LDS>
-PBG_DEV float gang_fric_limit(const GangCtx& X, int c) {
+PBG_DEV real_t<R> gang_fric_limit(const GangCtx<R>& X, int c) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
-  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef Sc v2f __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) const v2f lds_v2f;
   constexpr int w = G::RW0 + G::YS + 2;
   if (LDS || c < X.cap) {
-    const lds_float* p = X.l + G::FIXED + coff<R, T>(c);
+    const LW* p = X.l + G::FIXED + coff<R, T>(c);
     return p[G::DW] * p[w];
   }
-  const float* p = X.g + coff<R, T>(c);
+  const Sc* p = X.g + coff<R, T>(c);
   return p[G::DW] * p[w];
 }
 template <class R, int T, bool LDS>
-PBG_DEV void gang_set_lam(const GangCtx& X, int c, int dir, float v) {
+PBG_DEV void gang_set_lam(const GangCtx<R>& X, int c, int dir, real_t<R> v) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   const int w = G::RW0 + dir * G::CRW + G::YS + 2;
   if (X.t == 0) {
@@ -583,13 +639,15 @@ PBG_DEV void gang_set_lam(const GangCtx& X, int c, int dir, float v) {
 // PGS update of a loaded row with u sliced over the gang; the new impulse has the same bits
 // in every lane
 template <class R, int T>
-PBG_DEV float gang_update(const GRow<R, T>& r, float* us, float lo, float hi) {
-  float part = 0.f;
+PBG_DEV real_t<R> gang_update(const GRow<R, T>& r, real_t<R>* us, real_t<R> lo, real_t<R> hi) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
+  Sc part = 0.f;
 #pragma unroll
   for (int m = 0; m < Gang<R, T>::NSL; m++) part += r.y[m] * us[m];
-  const float yu = gang_sum<T>(part);
-  const float nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
-  const float dl = nl - r.lam;
+  const Sc yu = gang_sum<T>(part);
+  const Sc nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
+  const Sc dl = nl - r.lam;
 #pragma unroll
   for (int m = 0; m < Gang<R, T>::NSL; m++) us[m] += r.y[m] * dl;
   return nl;
@@ -607,7 +665,9 @@ PBG_DEV float gang_update(const GRow<R, T>& r, float* us, float lo, float hi) {
 // NW: 32-bit words of the positive-impulse mask (the caller takes NW = 1 when no env of the wave
 // has more than 32 contacts, the model's full width otherwise)
 template <class R, int T, bool LDS, int NW>
-PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
+PBG_DEV void gang_contact_sweep(const GangCtx<R>& X, int nc, real_t<R>* us) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   using Row = GRow<R, T>;
   if (nc <= 0) return;
@@ -624,7 +684,7 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
       gang_set_lam<R, T, LDS>(X, c, 0, gang_update<R, T>(A, us, 0.f, 3.0e38f));
     }
     for (int c = 0; c < nc; c++) {
-      const float lim = gang_fric_limit<R, T, LDS>(X, c);
+      const Sc lim = gang_fric_limit<R, T, LDS>(X, c);
       if (!(lim > 0.f)) continue;  // mu * lambda_n: lambda_n > 0 (mu > 0)
       Row A1, A2;
       gang_load_row<R, T, LDS>(X, c, 1, A1);
@@ -642,7 +702,7 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
     else if constexpr (w == 2) return pw2;
     else return pw3;
   };
-  auto mark = [&](int c, float nl) {
+  auto mark = [&](int c, Sc nl) {
     const uint32_t bit = nl > 0.f ? 1u << (c & 31) : 0u;
     if constexpr (NW == 1) {
       pw0 |= bit;
@@ -660,7 +720,7 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
       int c = 0;
       while (true) {
         gang_load_row<R, T, LDS>(X, min(c + 1, nc - 1), 0, B);
-        float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+        Sc nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
         gang_set_lam<R, T, LDS>(X, c, 0, nl);
         mark(c, nl);
         if (++c >= nc) break;
@@ -680,7 +740,7 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
       int c = 0;
       while (true) {
         gang_load_row<R, T, LDS>(X, min(c + 2, nc - 1), 0, C);
-        float nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
+        Sc nl = gang_update<R, T>(A, us, 0.f, 3.0e38f);
         gang_set_lam<R, T, LDS>(X, c, 0, nl);
         mark(c, nl);
         if (++c >= nc) break;
@@ -720,7 +780,7 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
   Row A1, A2, B1, B2;
   gang_load_row<R, T, LDS>(X, c, 1, A1);
   gang_load_row<R, T, LDS>(X, c, 2, A2);
-  float limA = gang_fric_limit<R, T, LDS>(X, c), limB;
+  Sc limA = gang_fric_limit<R, T, LDS>(X, c), limB;
   while (true) {
     int c2 = next();
     const bool more = c2 >= 0;
@@ -753,11 +813,13 @@ PBG_DEV void gang_contact_sweep(const GangCtx& X, int nc, float* us) {
 // (frames for the collision pass), motion vectors sw / sv, M at O_L, the right-hand side
 // at O_RHS.  Same formulas as dyn_mass with run-time model constants.
 template <class R, int T>
-PBG_DEV f3 gang_O(const GangCtx& X) {
+PBG_DEV V3<real_t<R>> gang_O(const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   constexpr int rb = Dims<R>::REF_BODY;
-  const lds_float* p = body_word<R, T>(X.l, rb, 12);
-  return mk3(p[0], p[1], p[2]);
+  const LW* p = body_word<R, T>(X.l, rb, 12);
+  return mk3<Sc>(p[0], p[1], p[2]);
 }
 // Forward kinematics / velocities / bias accelerations of one round of a tree level: lane
 // t < KN owns body lev_body[K0 + t] (compile-time), reads its parent's record from LDS and
@@ -766,17 +828,19 @@ PBG_DEV f3 gang_O(const GangCtx& X) {
 #define PBG_LV(expr) lvsel<R, K0, KN>(t, [&](auto bc_) { constexpr int b = decltype(bc_)::value; return (expr); })
 #define PBG_LVI(expr) lvsel_i<R, K0, KN>(t, [&](auto bc_) { constexpr int b = decltype(bc_)::value; return (expr); })
 template <class R, int T, int K0, int KN>
-PBG_DEV void gang_fk_round(const GangCtx& X) {
+PBG_DEV void gang_fk_round(const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   using DTh = GangDT<R>;
   constexpr int JT = lv_jt<R>(K0, KN);
   const int t = opaque_lane(X.t);
   if (t >= KN) return;
   const int body = PBG_LVI(b), p = PBG_LVI(DTh::v.parent[b]), d = PBG_LVI(DTh::v.dof[b]);
-  const lds_float* P = body_word<R, T>(X.l, p, 0);
-  const lds_float* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
-  m3 Rp, Ro;
-  float pr[G::FW + G::KW];  // the parent's record: frame | kinematic part
+  const LW* P = body_word<R, T>(X.l, p, 0);
+  const LW* PK = body_word<R, T>(X.l, p, G::FW) - G::FW;  // PK[12..26]
+  M3<Sc> Rp, Ro;
+  Sc pr[G::FW + G::KW];  // the parent's record: frame | kinematic part
   if constexpr (G::KAL) {
     lds_ld4<G::FW>(P, pr);
     lds_ld4<G::KW>(PK + G::FW, pr + G::FW);
@@ -792,50 +856,50 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
     constexpr int i = decltype(i_c)::value;
     Ro.m[i] = PBG_LV(DTh::v.ro[b][i]);
   });
-  const f3 xp = mk3(pr[9], pr[10], pr[11]), cp = mk3(pr[12], pr[13], pr[14]), wp = mk3(pr[15], pr[16], pr[17]);
-  const f3 vp = mk3(pr[18], pr[19], pr[20]), alp = mk3(pr[21], pr[22], pr[23]), acp = mk3(pr[24], pr[25], pr[26]);
-  const m3 R0 = mul_kb(Rp, Ro);
-  const f3 x0 = xp + mulc(Rp, PBG_LV(DTh::v.opos[b][0]), PBG_LV(DTh::v.opos[b][1]), PBG_LV(DTh::v.opos[b][2]));
-  const f3 axl = mk3(PBG_LV(DTh::v.axis[b][0]), PBG_LV(DTh::v.axis[b][1]), PBG_LV(DTh::v.axis[b][2]));
-  const f3 anl = mk3(PBG_LV(DTh::v.anchor[b][0]), PBG_LV(DTh::v.anchor[b][1]), PBG_LV(DTh::v.anchor[b][2]));
-  const f3 com = mk3(PBG_LV(DTh::v.com[b][0]), PBG_LV(DTh::v.com[b][1]), PBG_LV(DTh::v.com[b][2]));
+  const V3<Sc> xp = mk3<Sc>(pr[9], pr[10], pr[11]), cp = mk3<Sc>(pr[12], pr[13], pr[14]), wp = mk3<Sc>(pr[15], pr[16], pr[17]);
+  const V3<Sc> vp = mk3<Sc>(pr[18], pr[19], pr[20]), alp = mk3<Sc>(pr[21], pr[22], pr[23]), acp = mk3<Sc>(pr[24], pr[25], pr[26]);
+  const M3<Sc> R0 = mul_kb(Rp, Ro);
+  const V3<Sc> x0 = xp + mulc(Rp, PBG_LV(DTh::v.opos[b][0]), PBG_LV(DTh::v.opos[b][1]), PBG_LV(DTh::v.opos[b][2]));
+  const V3<Sc> axl = mk3<Sc>(PBG_LV(DTh::v.axis[b][0]), PBG_LV(DTh::v.axis[b][1]), PBG_LV(DTh::v.axis[b][2]));
+  const V3<Sc> anl = mk3<Sc>(PBG_LV(DTh::v.anchor[b][0]), PBG_LV(DTh::v.anchor[b][1]), PBG_LV(DTh::v.anchor[b][2]));
+  const V3<Sc> com = mk3<Sc>(PBG_LV(DTh::v.com[b][0]), PBG_LV(DTh::v.com[b][1]), PBG_LV(DTh::v.com[b][2]));
   auto kin = [&](auto jt_c) {
     constexpr int jt = decltype(jt_c)::value;
-    const float q = jt != 4 ? X.l[G::O_Q + d] : 0.f, qd = jt != 4 ? X.l[G::O_QD + d] : 0.f;
-    m3 Rm = R0;
-    f3 x = x0, w, v, al, ac, c;
+    const Sc q = jt != 4 ? X.l[G::O_Q + d] : 0.f, qd = jt != 4 ? X.l[G::O_QD + d] : 0.f;
+    M3<Sc> Rm = R0;
+    V3<Sc> x = x0, w, v, al, ac, c;
     if constexpr (jt == 0) {
-      float sn, cs;
+      Sc sn, cs;
       sincos_fast(q, &sn, &cs);
-      const float t1 = 1.f - cs;
-      m3 Rj;
-      const float axx = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][0]), ayy = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][1]);
-      const float azz = PBG_LV(DTh::v.axis[b][2] * DTh::v.axis[b][2]), axy = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][1]);
-      const float axz = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][2]), ayz = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][2]);
+      const Sc t1 = 1.f - cs;
+      M3<Sc> Rj;
+      const Sc axx = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][0]), ayy = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][1]);
+      const Sc azz = PBG_LV(DTh::v.axis[b][2] * DTh::v.axis[b][2]), axy = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][1]);
+      const Sc axz = PBG_LV(DTh::v.axis[b][0] * DTh::v.axis[b][2]), ayz = PBG_LV(DTh::v.axis[b][1] * DTh::v.axis[b][2]);
       Rj.m[0] = kmul(axx, t1) + cs;                 Rj.m[1] = kmul(axy, t1) - kmul(axl.z, sn); Rj.m[2] = kmul(axz, t1) + kmul(axl.y, sn);
       Rj.m[3] = kmul(axy, t1) + kmul(axl.z, sn);    Rj.m[4] = kmul(ayy, t1) + cs;              Rj.m[5] = kmul(ayz, t1) - kmul(axl.x, sn);
       Rj.m[6] = kmul(axz, t1) - kmul(axl.y, sn);    Rj.m[7] = kmul(ayz, t1) + kmul(axl.x, sn); Rj.m[8] = kmul(azz, t1) + cs;
       Rm = mul_kb(R0, Rj);
-      const f3 rja = mulc(Rj, anl);
+      const V3<Sc> rja = mulc(Rj, anl);
       x = x0 + mulc(R0, anl - rja);
       c = x + mulc(Rm, com);
-      const f3 a = mulc(R0, axl);
-      const f3 o = x0 + mulc(R0, anl);
-      const f3 ro = o - cp;
-      const f3 vo = vp + cross3(wp, ro);
-      const f3 ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
+      const V3<Sc> a = mulc(R0, axl);
+      const V3<Sc> o = x0 + mulc(R0, anl);
+      const V3<Sc> ro = o - cp;
+      const V3<Sc> vo = vp + cross3(wp, ro);
+      const V3<Sc> ao = acp + cross3(alp, ro) + cross3(wp, cross3(wp, ro));
       w = wp + qd * a;
       al = alp + qd * cross3(wp, a);
-      const f3 rc = c - o;
+      const V3<Sc> rc = c - o;
       v = vo + cross3(w, rc);
       ac = ao + cross3(al, rc) + cross3(w, cross3(w, rc));
       X.l[G::O_JA + G::SS * d] = a.x; X.l[G::O_JA + G::SS * d + 1] = a.y; X.l[G::O_JA + G::SS * d + 2] = a.z;
       X.l[G::O_JO + G::SS * d] = o.x; X.l[G::O_JO + G::SS * d + 1] = o.y; X.l[G::O_JO + G::SS * d + 2] = o.z;
     } else if constexpr (jt == 1) {
-      const f3 a = mulc(R0, axl);
+      const V3<Sc> a = mulc(R0, axl);
       x = x0 + q * a;
       c = x + mulc(Rm, com);
-      const f3 r = c - cp;
+      const V3<Sc> r = c - cp;
       w = wp;
       al = alp;
       v = vp + cross3(wp, r) + qd * a;
@@ -844,13 +908,13 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
       X.l[G::O_JO + G::SS * d] = x0.x; X.l[G::O_JO + G::SS * d + 1] = x0.y; X.l[G::O_JO + G::SS * d + 2] = x0.z;
     } else {
       c = x + mulc(Rm, com);
-      const f3 r = c - cp;
+      const V3<Sc> r = c - cp;
       w = wp;
       al = alp;
       v = vp + cross3(wp, r);
       ac = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
     }
-    const float rec[G::BW + 1] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
+    const Sc rec[G::BW + 1] = {Rm.m[0], Rm.m[1], Rm.m[2], Rm.m[3], Rm.m[4], Rm.m[5], Rm.m[6], Rm.m[7], Rm.m[8],
                                   x.x, x.y, x.z, c.x, c.y, c.z, w.x, w.y, w.z, v.x, v.y, v.z, al.x, al.y, al.z, ac.x, ac.y, ac.z, 0.f};
     if constexpr (G::KAL) {
       lds_st4<G::FW>(body_word<R, T>(X.l, body, 0), rec);
@@ -871,17 +935,19 @@ PBG_DEV void gang_fk_round(const GangCtx& X) {
 }
 
 template <class R, int T>
-PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
+PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx<R>& X SUB_STAMP_ARGS) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using D = Dims<R>;
   using G = Gang<R, T>;
   auto& TD = GangTabs<R>::dyn(X.tabs);
   constexpr int NB = D::NB, N = R::NDOF, NLEV = gang_nlev<R>();
-  const float g = X.P.gravity;
+  const Sc g = X.P.gravity;
   const bool w0 = X.t == 0;
   // base record and joint state (replicated registers -> LDS; the front path keeps the state in
   // LDS: q / qd are there, the base words at O_BS)
   if (w0) {
-    float bp[3], bq[4], bv[3], bw[3];
+    Sc bp[3], bq[4], bv[3], bw[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       bp[i] = G::LST ? X.l[G::O_BS + i] : s.bp[i];
@@ -890,8 +956,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) bq[i] = G::LST ? X.l[G::O_BS + 3 + i] : s.bq[i];
-    const m3 Rb = quat_to_m3(bq[0], bq[1], bq[2], bq[3]);
-    const float rec[G::BW] = {Rb.m[0], Rb.m[1], Rb.m[2], Rb.m[3], Rb.m[4], Rb.m[5], Rb.m[6], Rb.m[7], Rb.m[8],
+    const M3<Sc> Rb = quat_to_m3(bq[0], bq[1], bq[2], bq[3]);
+    const Sc rec[G::BW] = {Rb.m[0], Rb.m[1], Rb.m[2], Rb.m[3], Rb.m[4], Rb.m[5], Rb.m[6], Rb.m[7], Rb.m[8],
                               bp[0], bp[1], bp[2], bp[0], bp[1], bp[2],
                               R::floating ? bw[0] : 0.f, R::floating ? bw[1] : 0.f, R::floating ? bw[2] : 0.f,
                               R::floating ? bv[0] : 0.f, R::floating ? bv[1] : 0.f, R::floating ? bv[2] : 0.f,
@@ -915,36 +981,36 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     PBG_GANG_SYNC
   });
   STAMP(0)
-  const f3 O = gang_O<R, T>(X);
+  const V3<Sc> O = gang_O<R, T>(X);
   // per-body inertia and wrench about O; motion vectors about O
 #pragma unroll
   for (int r_ = 0; r_ < (NB + T - 1) / T; r_++) {  // rounds unrolled: table loads of all rounds overlap
     const int b = r_ * T + X.t;
     if (b >= NB) continue;
-    const lds_float* P = body_word<R, T>(X.l, b, 0);
-    const lds_float* PK = body_word<R, T>(X.l, b, G::FW) - G::FW;
-    m3 Rm;
+    const LW* P = body_word<R, T>(X.l, b, 0);
+    const LW* PK = body_word<R, T>(X.l, b, G::FW) - G::FW;
+    M3<Sc> Rm;
 #pragma unroll
     for (int i = 0; i < 9; i++) Rm.m[i] = P[i];
-    const f3 c = mk3(PK[12], PK[13], PK[14]), w = mk3(PK[15], PK[16], PK[17]), v = mk3(PK[18], PK[19], PK[20]);
-    const f3 al = mk3(PK[21], PK[22], PK[23]), ac = mk3(PK[24], PK[25], PK[26]);
-    const float m = TD.mass[b];
-    float I6[6];
+    const V3<Sc> c = mk3<Sc>(PK[12], PK[13], PK[14]), w = mk3<Sc>(PK[15], PK[16], PK[17]), v = mk3<Sc>(PK[18], PK[19], PK[20]);
+    const V3<Sc> al = mk3<Sc>(PK[21], PK[22], PK[23]), ac = mk3<Sc>(PK[24], PK[25], PK[26]);
+    const Sc m = TD.mass[b];
+    Sc I6[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) I6[i] = TD.inertia[b][i];
-    const s6 Iw = rotate_inertia(Rm, I6);
-    const f3 r = c - O;
-    const float rr = dot3(r, r);
-    const f3 Iww = mul(Iw, w);
-    const f3 f = m * (ac - mk3(0, 0, -g)) + (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v))) * v;
-    const f3 n = mul(Iw, al) + cross3(w, Iww) + ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w)) * Iww;
-    const f3 pr = m * r, Nn = n + cross3(r, f);
-    const float cmp[G::CW] = {Iw.a[0] + m * (rr - r.x * r.x), Iw.a[1] + m * (rr - r.y * r.y), Iw.a[2] + m * (rr - r.z * r.z),
+    const S6<Sc> Iw = rotate_inertia(Rm, I6);
+    const V3<Sc> r = c - O;
+    const Sc rr = dot3(r, r);
+    const V3<Sc> Iww = mul(Iw, w);
+    const V3<Sc> f = m * (ac - mk3<Sc>(0, 0, -g)) + (m * ((Sc)PBG_LINEAR_DAMPING + (Sc)PBG_LINEAR_DAMPING * norm3(v))) * v;
+    const V3<Sc> n = mul(Iw, al) + cross3(w, Iww) + ((Sc)PBG_ANGULAR_DAMPING + (Sc)PBG_ANGULAR_DAMPING * norm3(w)) * Iww;
+    const V3<Sc> pr = m * r, Nn = n + cross3(r, f);
+    const Sc cmp[G::CW] = {Iw.a[0] + m * (rr - r.x * r.x), Iw.a[1] + m * (rr - r.y * r.y), Iw.a[2] + m * (rr - r.z * r.z),
                               Iw.a[3] - m * r.x * r.y, Iw.a[4] - m * r.x * r.z, Iw.a[5] - m * r.y * r.z,
                               pr.x, pr.y, pr.z, f.x, f.y, f.z, Nn.x, Nn.y, Nn.z, m};
-    lds_float* C = X.l + G::O_CP + G::CW * b;
+    LW* C = X.l + G::O_CP + G::CW * b;
     const bool massive = m > 0.f;
-    float cv[G::CW];
+    Sc cv[G::CW];
 #pragma unroll
     for (int i = 0; i < G::CW; i++) cv[i] = massive ? cmp[i] : 0.f;
     if constexpr (G::AL) lds_st4<G::CW>(C, cv);
@@ -958,18 +1024,18 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int i = r_ * T + X.t;
     if (i >= N) continue;
     const int d = TD.g_dof[i];
-    f3 sw, sv;
+    V3<Sc> sw, sv;
     if (d >= 0) {
-      const f3 a = mk3(X.l[G::O_JA + G::SS * d], X.l[G::O_JA + G::SS * d + 1], X.l[G::O_JA + G::SS * d + 2]);
-      const f3 o = mk3(X.l[G::O_JO + G::SS * d], X.l[G::O_JO + G::SS * d + 1], X.l[G::O_JO + G::SS * d + 2]);
+      const V3<Sc> a = mk3<Sc>(X.l[G::O_JA + G::SS * d], X.l[G::O_JA + G::SS * d + 1], X.l[G::O_JA + G::SS * d + 2]);
+      const V3<Sc> o = mk3<Sc>(X.l[G::O_JO + G::SS * d], X.l[G::O_JO + G::SS * d + 1], X.l[G::O_JO + G::SS * d + 2]);
       const bool rev = TD.jt[TD.g_body[i]] == 0;
-      sw = rev ? a : mk3(0, 0, 0);
+      sw = rev ? a : mk3<Sc>(0, 0, 0);
       sv = rev ? cross3(o - O, a) : a;
     } else {
       const int kk = i - R::NJ;  // 0..2 linear, 3..5 angular
-      const f3 e = mk3(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
-      sw = kk < 3 ? mk3(0, 0, 0) : e;
-      sv = kk < 3 ? e : mk3(0, 0, 0);
+      const V3<Sc> e = mk3<Sc>(kk % 3 == 0, kk % 3 == 1, kk % 3 == 2);
+      sw = kk < 3 ? mk3<Sc>(0, 0, 0) : e;
+      sv = kk < 3 ? e : mk3<Sc>(0, 0, 0);
     }
     X.l[G::O_SW + G::SS * i] = sw.x; X.l[G::O_SW + G::SS * i + 1] = sw.y; X.l[G::O_SW + G::SS * i + 2] = sw.z;
     X.l[G::O_SV + G::SS * i] = sv.x; X.l[G::O_SV + G::SS * i + 1] = sv.y; X.l[G::O_SV + G::SS * i + 2] = sv.z;
@@ -988,8 +1054,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
       const int t = opaque_lane(X.t);
       if (t < KN) {
         const int b = ksel<S, KN, int>(t, [&](auto bc) { return decltype(bc)::value; });
-        lds_float* C = X.l + G::O_CP + G::CW * b;
-        float acc[G::CW];
+        LW* C = X.l + G::O_CP + G::CW * b;
+        Sc acc[G::CW];
         if constexpr (G::AL) lds_ld4<G::CW>(C, acc);
         else {
 #pragma unroll
@@ -999,8 +1065,8 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
           constexpr int j = decltype(j_c)::value;
           const int c = ksel<S, KN, int>(t, [&](auto bc) { return j < GC::v.nch[decltype(bc)::value] ? GC::v.ch[decltype(bc)::value][j] : -1; });
           if (c >= 0) {
-            const lds_float* K = X.l + G::O_CP + G::CW * c;
-            float kv[G::CW];
+            const LW* K = X.l + G::O_CP + G::CW * c;
+            Sc kv[G::CW];
             if constexpr (G::AL) lds_ld4<G::CW>(K, kv);
             else {
 #pragma unroll
@@ -1030,26 +1096,26 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int k = r_ * T + X.t;
     if (k >= N) continue;
     const int bk = TD.g_body[k], d = TD.g_dof[k];
-    const lds_float* Cp = X.l + G::O_CP + G::CW * bk;
-    float C[G::CW];
+    const LW* Cp = X.l + G::O_CP + G::CW * bk;
+    Sc C[G::CW];
     if constexpr (G::AL) lds_ld4<G::CW>(Cp, C);
     else {
 #pragma unroll
       for (int i = 0; i < G::CW; i++) C[i] = Cp[i];
     }
-    s6 J;
+    S6<Sc> J;
 #pragma unroll
     for (int i = 0; i < 6; i++) J.a[i] = C[i];
-    const f3 p1 = mk3(C[6], C[7], C[8]);
-    const float cm = C[15];
-    const f3 swk = mk3(X.l[G::O_SW + G::SS * k], X.l[G::O_SW + G::SS * k + 1], X.l[G::O_SW + G::SS * k + 2]);
-    const f3 svk = mk3(X.l[G::O_SV + G::SS * k], X.l[G::O_SV + G::SS * k + 1], X.l[G::O_SV + G::SS * k + 2]);
-    const f3 Jw_ = mul(J, swk) + cross3(p1, svk);
-    const f3 Fv = cm * svk - cross3(p1, swk);
-    lds_float* f = X.l + O_FK + 6 * k;
+    const V3<Sc> p1 = mk3<Sc>(C[6], C[7], C[8]);
+    const Sc cm = C[15];
+    const V3<Sc> swk = mk3<Sc>(X.l[G::O_SW + G::SS * k], X.l[G::O_SW + G::SS * k + 1], X.l[G::O_SW + G::SS * k + 2]);
+    const V3<Sc> svk = mk3<Sc>(X.l[G::O_SV + G::SS * k], X.l[G::O_SV + G::SS * k + 1], X.l[G::O_SV + G::SS * k + 2]);
+    const V3<Sc> Jw_ = mul(J, swk) + cross3(p1, svk);
+    const V3<Sc> Fv = cm * svk - cross3(p1, swk);
+    LW* f = X.l + O_FK + 6 * k;
     f[0] = Jw_.x; f[1] = Jw_.y; f[2] = Jw_.z; f[3] = Fv.x; f[4] = Fv.y; f[5] = Fv.z;
-    const f3 F = mk3(C[9], C[10], C[11]), Nn = mk3(C[12], C[13], C[14]);
-    float r = -(dot3(swk, Nn) + dot3(svk, F));
+    const V3<Sc> F = mk3<Sc>(C[9], C[10], C[11]), Nn = mk3<Sc>(C[12], C[13], C[14]);
+    Sc r = -(dot3(swk, Nn) + dot3(svk, F));
     if (d >= 0) {
       r += X.l[G::O_TAU + d] - TD.damping[d] * X.l[G::O_QD + d];
       if constexpr (has_springs<R>()) r -= TD.stiffness[d] * X.l[G::O_Q + d];  // mjcf.py B7
@@ -1063,10 +1129,10 @@ PBG_DEV void gang_dyn_mass(const State<R>& s, const GangCtx& X SUB_STAMP_ARGS) {
     const int j = r_ * T + X.t;
     if (j >= D::NNZ) continue;
     const int gi = TD.me_i[j], gk = TD.me_k[j];
-    const lds_float* f = X.l + O_FK + 6 * gk;
-    const f3 Jw_ = mk3(f[0], f[1], f[2]), Fv = mk3(f[3], f[4], f[5]);
-    const f3 swi = mk3(X.l[G::O_SW + G::SS * gi], X.l[G::O_SW + G::SS * gi + 1], X.l[G::O_SW + G::SS * gi + 2]);
-    const f3 svi = mk3(X.l[G::O_SV + G::SS * gi], X.l[G::O_SV + G::SS * gi + 1], X.l[G::O_SV + G::SS * gi + 2]);
+    const LW* f = X.l + O_FK + 6 * gk;
+    const V3<Sc> Jw_ = mk3<Sc>(f[0], f[1], f[2]), Fv = mk3<Sc>(f[3], f[4], f[5]);
+    const V3<Sc> swi = mk3<Sc>(X.l[G::O_SW + G::SS * gi], X.l[G::O_SW + G::SS * gi + 1], X.l[G::O_SW + G::SS * gi + 2]);
+    const V3<Sc> svi = mk3<Sc>(X.l[G::O_SV + G::SS * gi], X.l[G::O_SV + G::SS * gi + 1], X.l[G::O_SV + G::SS * gi + 2]);
     X.l[G::O_L + j] = (dot3(swi, Jw_) + dot3(svi, Fv)) + TD.me_arm[j];
   }
   PBG_GANG_SYNC
@@ -1110,11 +1176,15 @@ struct FrontSrc {
 };
 template <class R, class F>
 PBG_DEV int front_pick(int q, F&& fn) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   return ksel<FrontSrc<R>, FP<R>::NF, int>(q, [&](auto fc) { return fn(decltype(fc)::value); });
 }
 // the trunk index t's joint velocity / base velocity from the env's LDS state (compile-time t)
 template <class R, int T, int t>
-PBG_DEV float trunk_nu(const GangCtx& X) {
+PBG_DEV real_t<R> trunk_nu(const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   constexpr int g = FP<R>::v.tg[t], d = Dims<R>::dof_of(g);
   if constexpr (d >= 0) return X.l[G::O_QD + d];
@@ -1125,19 +1195,21 @@ PBG_DEV float trunk_nu(const GangCtx& X) {
 // (O_RHS) from LDS; factor, nu_pred = clamp(nu + dt M^-1 rhs), u = L^T nu_pred; stages L (in
 // place, the same word order), 1 / diag(L) (O_LD), u (O_U) and the limit positions (O_LP).
 template <class R, int T>
-PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
+PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using D = Dims<R>;
   using G = Gang<R, T>;
   using TT = TrunkTab<R>;
   constexpr int NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NT2 = TT::NT2, BM = TT::BMAX(), NM = TT::NMAX();
-  const float dt = X.P.dt;
+  const Sc dt = X.P.dt;
   const int q = opaque_lane(X.t) % GRP;
   const int cls = q < NF ? front_pick<R>(q, [](int f) { return FP<R>::v.cls[f]; }) : -1;
   const int boff = front_pick<R>(q, [](int f) { return FP<R>::v.off[f]; });
   const int g0 = front_pick<R>(q, [](int f) { return FP<R>::v.g0[f]; });
-  const lds_float* blk = X.l + G::O_L + boff;
-  float Fb[BM], Fd[NM], Fy[NM];  // the lane's front block (factored in place), 1 / diag, forward solve
-  float S[NT2], z[NT];           // Schur terms W W^T (trunk pairs) and trunk right-hand-side terms
+  const LW* blk = X.l + G::O_L + boff;
+  Sc Fb[BM], Fd[NM], Fy[NM];  // the lane's front block (factored in place), 1 / diag, forward solve
+  Sc S[NT2], z[NT];           // Schur terms W W^T (trunk pairs) and trunk right-hand-side terms
 #pragma unroll
   for (int i = 0; i < NT2; i++) S[i] = 0.f;
 #pragma unroll
@@ -1153,8 +1225,8 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     for (int i = 0; i < bs; i++) Fb[i] = blk[i];
     static_for<0, n>([&](auto a_c) {
       constexpr int a = decltype(a_c)::value;
-      const float d = fast_sqrt(Fb[FC::a_off(a, a)]);
-      const float r = fast_rcp(d);
+      const Sc d = fast_sqrt(Fb[FC::a_off(a, a)]);
+      const Sc r = fast_rcp(d);
       Fb[FC::a_off(a, a)] = d;
       Fd[a] = r;
       static_for<a + 1, n>([&](auto b_c) {
@@ -1191,7 +1263,7 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     // forward solve L_f y_f = rhs_f; trunk terms z_t += L_(t,a) y_a
     static_for<0, n>([&](auto a_c) {
       constexpr int a = decltype(a_c)::value;
-      float v = X.l[G::O_RHS + g0 + a];
+      Sc v = X.l[G::O_RHS + g0 + a];
       static_for<0, a>([&](auto b_c) {
         constexpr int b = decltype(b_c)::value;
         if constexpr (FC::cpl(a, b)) v -= Fb[FC::a_off(a, b)] * Fy[b];
@@ -1204,14 +1276,14 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     });
   });
   // --- trunk: T - sum_f W_f W_f^T, factor, forward + backward solve ---------------------------
-  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
-  float Lt[NT2], Ldt[NT], yt[NT], xt[NT];
+  const LW* tb = X.l + G::O_L + FP<R>::v.toff;
+  Sc Lt[NT2], Ldt[NT], yt[NT], xt[NT];
 #pragma unroll
   for (int i = 0; i < NT2; i++) Lt[i] = tb[i] - gang_sum<GRP>(S[i]);
   static_for<0, NT>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
-    const float d = fast_sqrt(Lt[TT::pos(j, j)]);
-    const float r = fast_rcp(d);
+    const Sc d = fast_sqrt(Lt[TT::pos(j, j)]);
+    const Sc r = fast_rcp(d);
     Lt[TT::pos(j, j)] = d;
     Ldt[j] = r;
     static_for<j + 1, NT>([&](auto i_c) {
@@ -1230,7 +1302,7 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
   });
   static_for<0, NT>([&](auto t_c) {
     constexpr int t = decltype(t_c)::value;
-    float v = X.l[G::O_RHS + FP<R>::v.tg[t]] - gang_sum<GRP>(z[t]);
+    Sc v = X.l[G::O_RHS + FP<R>::v.tg[t]] - gang_sum<GRP>(z[t]);
     static_for<0, t>([&](auto k_c) {
       constexpr int k = decltype(k_c)::value;
       if constexpr (TT::pos(t, k) >= 0) v -= Lt[TT::pos(t, k)] * yt[k];
@@ -1239,7 +1311,7 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
   });
   static_for<0, NT>([&](auto r_c) {
     constexpr int t = NT - 1 - decltype(r_c)::value;
-    float v = yt[t];
+    Sc v = yt[t];
     static_for<t + 1, NT>([&](auto k_c) {
       constexpr int k = decltype(k_c)::value;
       if constexpr (TT::pos(k, t) >= 0) v -= Lt[TT::pos(k, t)] * xt[k];
@@ -1247,10 +1319,10 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     xt[t] = v * Ldt[t];
   });
   // trunk nu_pred and u_t = L_t^T nu_t
-  float nut[NT];
+  Sc nut[NT];
   static_for<0, NT>([&](auto t_c) {
     constexpr int t = decltype(t_c)::value;
-    nut[t] = clampf(trunk_nu<R, T, t>(X) + dt * xt[t], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    nut[t] = clampf(trunk_nu<R, T, t>(X) + dt * xt[t], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
   });
   const bool wf = X.t < GRP && q < NF;  // the gang's front writers
   // --- fronts: backward solve, nu_pred, u_f; store --------------------------------------------
@@ -1259,10 +1331,10 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     using FC = FrontCls<R, C>;
     constexpr int n = FC::n;
     if (cls != C) return;
-    float xf[n], nuf[n];
+    Sc xf[n], nuf[n];
     static_for<0, n>([&](auto r_c) {
       constexpr int a = n - 1 - decltype(r_c)::value;
-      float v = Fy[a];
+      Sc v = Fy[a];
       static_for<a + 1, n>([&](auto b_c) {
         constexpr int b = decltype(b_c)::value;
         if constexpr (FC::cpl(b, a)) v -= Fb[FC::a_off(b, a)] * xf[b];
@@ -1274,19 +1346,19 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
       xf[a] = v * Fd[a];
     });
     // joint dof of local a: NJ - 1 - (g0 + a); its velocity from the gang's LDS copy of qd
-    const lds_float* qd = X.l + G::O_QD + (R::NJ - 1 - g0);
+    const LW* qd = X.l + G::O_QD + (R::NJ - 1 - g0);
     static_for<0, n>([&](auto a_c) {
       constexpr int a = decltype(a_c)::value;
-      nuf[a] = clampf(qd[-a] + dt * xf[a], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+      nuf[a] = clampf(qd[-a] + dt * xf[a], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
     });
     if (wf) {
-      lds_float* wb = X.l + G::O_L + boff;
+      LW* wb = X.l + G::O_L + boff;
       constexpr int bs = FP<R>::v.bsz[FC::f];
 #pragma unroll
       for (int i = 0; i < bs; i++) wb[i] = Fb[i];
       static_for<0, n>([&](auto a_c) {
         constexpr int a = decltype(a_c)::value;
-        float u = 0.f;
+        Sc u = 0.f;
         static_for<a, n>([&](auto b_c) {
           constexpr int b = decltype(b_c)::value;
           if constexpr (FC::cpl(b, a)) u += Fb[FC::a_off(b, a)] * nuf[b];
@@ -1301,12 +1373,12 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     }
   });
   if (X.t == 0) {
-    lds_float* wt = X.l + G::O_L + FP<R>::v.toff;
+    LW* wt = X.l + G::O_L + FP<R>::v.toff;
 #pragma unroll
     for (int i = 0; i < NT2; i++) wt[i] = Lt[i];
     static_for<0, NT>([&](auto t_c) {
       constexpr int t = decltype(t_c)::value;
-      float u = 0.f;
+      Sc u = 0.f;
       static_for<t, NT>([&](auto k_c) {
         constexpr int k = decltype(k_c)::value;
         if constexpr (TT::pos(k, t) >= 0) u += Lt[TT::pos(k, t)] * nut[k];
@@ -1320,7 +1392,7 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
       State<R> cs;
 #pragma unroll
       for (int i = 0; i < 3; i++) { cs.cube.v[i] = X.l[G::O_CS + 7 + i]; cs.cube.w[i] = X.l[G::O_CS + 10 + i]; }
-      float uc[6];
+      Sc uc[6];
       cube_unconstrained<R>(cs, uc, X.P);
 #pragma unroll
       for (int i = 0; i < 6; i++) X.l[G::O_U + R::NDOF + i] = uc[i];
@@ -1330,8 +1402,8 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
     static_for<0, D::NLIM>([&](auto li_c) {
       constexpr int li = decltype(li_c)::value;
       constexpr int d = D::LIM.v[li][0];
-      X.l[G::O_LP + 2 * li] = X.l[G::O_Q + d] - (float)R::dof_lower[d];
-      X.l[G::O_LP + 2 * li + 1] = (float)R::dof_upper[d] - X.l[G::O_Q + d];
+      X.l[G::O_LP + 2 * li] = X.l[G::O_Q + d] - (Sc)R::dof_lower[d];
+      X.l[G::O_LP + 2 * li + 1] = (Sc)R::dof_upper[d] - X.l[G::O_Q + d];
     });
   }
   (void)NM;
@@ -1340,9 +1412,11 @@ PBG_DEV void gang_front_solve(const State<R>& s, const GangCtx& X) {
 
 // The staged factor (word order pbg_fronts.h) and 1 / diag(L) into registers, as 16-byte LDS loads
 template <class R, int T>
-PBG_DEV void gang_load_factor(const GangCtx& X, float* L, float* Ld) {
+PBG_DEV void gang_load_factor(const GangCtx<R>& X, real_t<R>* L, real_t<R>* Ld) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
-  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef Sc v4f __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) const v4f lds_v4f;
   const lds_v4f* pl = (const lds_v4f*)(X.l + G::O_L);
 #pragma unroll
@@ -1365,29 +1439,31 @@ PBG_DEV void gang_load_factor(const GangCtx& X, float* L, float* Ld) {
 // their fronts' joints, lane 0 the trunk joints, the base and the cube; the next sub-step reads
 // them after its first gang sync)
 template <class R, int T>
-PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
+PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   using D = Dims<R>;
   using TT = TrunkTab<R>;
   constexpr int NJ = R::NJ, N = R::NDOF, NF = FP<R>::NF, GRP = FP<R>::GRP, NT = FP<R>::NT, NT2 = TT::NT2;
-  const float dt = X.P.dt;
-  const float vmax = (float)PBG_MAX_COORD_VELOCITY;
+  const Sc dt = X.P.dt;
+  const Sc vmax = (Sc)PBG_MAX_COORD_VELOCITY;
   // --- trunk ---------------------------------------------------------------------------------
-  const lds_float* tb = X.l + G::O_L + FP<R>::v.toff;
-  float Lt[NT2], xt[NT];
+  const LW* tb = X.l + G::O_L + FP<R>::v.toff;
+  Sc Lt[NT2], xt[NT];
 #pragma unroll
   for (int i = 0; i < NT2; i++) Lt[i] = tb[i];
   static_for<0, NT>([&](auto r_c) {
     constexpr int t = NT - 1 - decltype(r_c)::value;
     constexpr int g = FP<R>::v.tg[t];
-    float v = X.l[G::O_U + g];
+    Sc v = X.l[G::O_U + g];
     static_for<t + 1, NT>([&](auto k_c) {
       constexpr int k = decltype(k_c)::value;
       if constexpr (TT::pos(k, t) >= 0) v -= Lt[TT::pos(k, t)] * xt[k];
     });
     xt[t] = v * X.l[G::O_LD + g];
   });
-  float nut[NT];
+  Sc nut[NT];
 #pragma unroll
   for (int t = 0; t < NT; t++) nut[t] = clampf(xt[t], -vmax, vmax);
   // --- fronts --------------------------------------------------------------------------------
@@ -1401,11 +1477,11 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
     using FC = FrontCls<R, C>;
     constexpr int n = FC::n;
     if (cls != C) return;
-    const lds_float* blk = X.l + G::O_L + boff;
-    float xf[n];
+    const LW* blk = X.l + G::O_L + boff;
+    Sc xf[n];
     static_for<0, n>([&](auto r_c) {
       constexpr int a = n - 1 - decltype(r_c)::value;
-      float v = X.l[G::O_U + g0 + a];
+      Sc v = X.l[G::O_U + g0 + a];
       static_for<a + 1, n>([&](auto b_c) {
         constexpr int b = decltype(b_c)::value;
         if constexpr (FC::cpl(b, a)) v -= blk[FC::a_off(b, a)] * xf[b];
@@ -1418,17 +1494,17 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
     });
     if (wf) {
       // joint dof of local a: NJ - 1 - (g0 + a) (leaf-first order)
-      lds_float* qd = X.l + G::O_QD + (NJ - 1 - g0);
-      lds_float* qq = X.l + G::O_Q + (NJ - 1 - g0);
+      LW* qd = X.l + G::O_QD + (NJ - 1 - g0);
+      LW* qq = X.l + G::O_Q + (NJ - 1 - g0);
       static_for<0, n>([&](auto a_c) {
         constexpr int a = decltype(a_c)::value;
-        const float v = clampf(xf[a], -vmax, vmax);
+        const Sc v = clampf(xf[a], -vmax, vmax);
         qd[-a] = v;
         qq[-a] += dt * v;
       });
     }
   });
-  float nu[N];  // the trunk part (compile-time indices; the fronts' entries are not used below)
+  Sc nu[N];  // the trunk part (compile-time indices; the fronts' entries are not used below)
   static_for<0, NT>([&](auto t_c) {
     constexpr int t = decltype(t_c)::value;
     nu[FP<R>::v.tg[t]] = nut[t];
@@ -1445,7 +1521,7 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
   }
   if (X.t == 0) {
     if constexpr (R::floating) {
-      float bq[4];
+      Sc bq[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) bq[i] = X.l[G::O_BS + 3 + i];
 #pragma unroll
@@ -1454,7 +1530,7 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
         X.l[G::O_BS + 10 + i] = nu[NJ + 3 + i];
         X.l[G::O_BS + i] += dt * nu[NJ + i];
       }
-      free_body_quat(bq, mk3(nu[NJ + 3], nu[NJ + 4], nu[NJ + 5]), X.P);
+      free_body_quat(bq, mk3<Sc>(nu[NJ + 3], nu[NJ + 4], nu[NJ + 5]), X.P);
 #pragma unroll
       for (int i = 0; i < 4; i++) X.l[G::O_BS + 3 + i] = bq[i];
     }
@@ -1464,7 +1540,7 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
       for (int i = 0; i < 3; i++) cs.cube.p[i] = X.l[G::O_CS + i];
 #pragma unroll
       for (int i = 0; i < 4; i++) cs.cube.q[i] = X.l[G::O_CS + 3 + i];
-      float uc[6];
+      Sc uc[6];
 #pragma unroll
       for (int i = 0; i < 6; i++) uc[i] = X.l[G::O_U + N + i];
       cube_integrate<R>(cs, uc, X.P);
@@ -1478,7 +1554,9 @@ PBG_DEV void gang_front_integrate(State<R>& s, const GangCtx& X) {
 }
 // the env's state record between registers and its LDS copy (front path)
 template <class R, int T>
-PBG_DEV void gang_put_state(const State<R>& s, const GangCtx& X) {
+PBG_DEV void gang_put_state(const State<R>& s, const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
   if (X.t == 0) {
 #pragma unroll
@@ -1496,7 +1574,9 @@ PBG_DEV void gang_put_state(const State<R>& s, const GangCtx& X) {
   }
 }
 template <class R, int T>
-PBG_DEV void gang_get_state(State<R>& s, const GangCtx& X) {
+PBG_DEV void gang_get_state(State<R>& s, const GangCtx<R>& X) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using G = Gang<R, T>;
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) { s.q[d] = X.l[G::O_Q + d]; s.qd[d] = X.l[G::O_QD + d]; }
@@ -1514,16 +1594,18 @@ PBG_DEV void gang_get_state(State<R>& s, const GangCtx& X) {
 
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int T, bool DIST>
-PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64_t& slot_bits, uint32_t sub,
+PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X, uint64_t& slot_bits, uint32_t sub,
                          uint32_t& csig SUB_STAMP_ARGS) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   using D = Dims<R>;
   using G = Gang<R, T>;
   auto& TB = GangTabs<R>::tab(X.tabs);
   constexpr int N = R::NDOF, NB = D::NB, NLIM = D::NLIM, NSL = G::NSL, YS = G::YS;
-  const SimP& P = X.P;
+  const SimPT<Sc>& P = X.P;
   const bool w0 = X.t == 0;  // the gang's writer for replicated values
   // L (Dims<R>::lidx order) into the factor's LDS word order (pbg_fronts.h)
-  auto stage_solution = [&](const float* L, const float* Ld, const float* u) {
+  auto stage_solution = [&](const Sc* L, const Sc* Ld, const Sc* u) {
     if (w0) {
       static_for<0, N>([&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
@@ -1539,14 +1621,14 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       static_for<0, NLIM>([&](auto li_c) {
         constexpr int li = decltype(li_c)::value;
         constexpr int d = D::LIM.v[li][0];
-        X.l[G::O_LP + 2 * li] = s.q[d] - (float)R::dof_lower[d];
-        X.l[G::O_LP + 2 * li + 1] = (float)R::dof_upper[d] - s.q[d];
+        X.l[G::O_LP + 2 * li] = s.q[d] - (Sc)R::dof_lower[d];
+        X.l[G::O_LP + 2 * li + 1] = (Sc)R::dof_upper[d] - s.q[d];
       });
     }
   };
   // the replicated path keeps its factor in registers from the factorisation through the rows pass
   // (the distributed path loads it from its LDS staging before the rows pass)
-  float Lr[G::NNZ4], Ldr[G::N4];
+  Sc Lr[G::NNZ4], Ldr[G::N4];
   if constexpr (DIST) {
     // --- distributed dynamics (M, rhs, frames, motion vectors in LDS) ----------------------
 #ifndef PBG_DEV_NODYN
@@ -1556,13 +1638,13 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   } else {
     // --- replicated dynamics (compile-time folded; short trees), staged into LDS ---------
     {
-      float nu[N], u[N];
+      Sc nu[N], u[N];
       dynamics<R>(s, tau, Lr, Ldr, nu, u, P SUB_STAMP_PASS);
       STAMP(3)
       stage_solution(Lr, Ldr, u);
     }
     Kin<R> k;
-    f3 sw[N], sv[N], O0;
+    V3<Sc> sw[N], sv[N], O0;
     kin_motion<R>(s, k, sw, sv, O0);
     if (w0) {
 #pragma unroll
@@ -1572,32 +1654,32 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       }
 #pragma unroll
       for (int b = 0; b < D::NB; b++) {
-        lds_float* p = body_word<R, T>(X.l, b, 0);
+        LW* p = body_word<R, T>(X.l, b, 0);
 #pragma unroll
         for (int i = 0; i < 9; i++) p[i] = k.Rm[b].m[i];
         p[9] = k.x[b].x; p[10] = k.x[b].y; p[11] = k.x[b].z;
-        lds_float* pk = body_word<R, T>(X.l, b, G::FW);
+        LW* pk = body_word<R, T>(X.l, b, G::FW);
         pk[0] = k.c[b].x; pk[1] = k.c[b].y; pk[2] = k.c[b].z;
       }
     }
   }
   PBG_GANG_SYNC
-  const f3 O = gang_O<R, T>(X);
+  const V3<Sc> O = gang_O<R, T>(X);
   PBG_GANG_SYNC
   STAMP(10)
-  auto frame = [&](int b, m3& Rm, f3& x) {
-    const lds_float* p = body_word<R, T>(X.l, b, 0);
+  auto frame = [&](int b, M3<Sc>& Rm, V3<Sc>& x) {
+    const LW* p = body_word<R, T>(X.l, b, 0);
 #pragma unroll
     for (int i = 0; i < 9; i++) Rm.m[i] = p[i];
-    x = mk3(p[9], p[10], p[11]);
+    x = mk3<Sc>(p[9], p[10], p[11]);
   };
   // descriptor: rA | rB | n | dist | fA (body A carries the base dofs) | fB (body B does) | chain masks of
   // A and B | floor | cube (+1: A is HumanoidFlagrunHarder's cube, -1: B is, 0: no cube; its lever
   // arm from the cube's centre is then rA, resp. rB)
-  auto put_desc = [&](int c, f3 rA, f3 rB, f3 n, float dist, float fB, uint32_t mA, uint32_t mB, float floor_, float mu,
-                      float fA = 1.f, float cube = 0.f) {
-    const float v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, fA, fB,
-                            __builtin_bit_cast(float, mA), __builtin_bit_cast(float, mB), floor_, cube};
+  auto put_desc = [&](int c, V3<Sc> rA, V3<Sc> rB, V3<Sc> n, Sc dist, Sc fB, uint32_t mA, uint32_t mB, Sc floor_, Sc mu,
+                      Sc fA = 1.f, Sc cube = 0.f) {
+    const Sc v[G::DW] = {rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, n.x, n.y, n.z, dist, fA, fB,
+                            mask_word<Sc>(mA), mask_word<Sc>(mB), floor_, cube};
     contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
       for (int w = 0; w < G::DW; w++) p[w] = v[w];
@@ -1615,11 +1697,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     static_for<0, (R::NG + T - 1) / T>([&](auto r_c) {
       const int g = decltype(r_c)::value * T + X.t;
       if (g < R::NG) {
-        m3 Rm; f3 x;
+        M3<Sc> Rm; V3<Sc> x;
         frame(TB.geom_body[g], Rm, x);
-        const f3 e0 = x + mul(Rm, mk3(TB.gp0[g][0], TB.gp0[g][1], TB.gp0[g][2]));
-        const f3 e1 = x + mul(Rm, mk3(TB.gp1[g][0], TB.gp1[g][1], TB.gp1[g][2]));
-        lds_float* e = X.l + O_GE + 6 * g;
+        const V3<Sc> e0 = x + mul(Rm, mk3<Sc>(TB.gp0[g][0], TB.gp0[g][1], TB.gp0[g][2]));
+        const V3<Sc> e1 = x + mul(Rm, mk3<Sc>(TB.gp1[g][0], TB.gp1[g][1], TB.gp1[g][2]));
+        LW* e = X.l + O_GE + 6 * g;
         e[0] = e0.x; e[1] = e0.y; e[2] = e0.z; e[3] = e1.x; e[4] = e1.y; e[5] = e1.z;
       }
     });
@@ -1632,14 +1714,14 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     constexpr int r = decltype(r_c)::value;
     const int sl = r * T + X.t;
     bool act = false;
-    f3 cc;
-    float rad = 0.f;
+    V3<Sc> cc;
+    Sc rad = 0.f;
     if (sl < R::NS) {
-      m3 Rm; f3 x;
+      M3<Sc> Rm; V3<Sc> x;
       frame(ST.slot_body[sl], Rm, x);
-      cc = x + mul(Rm, mk3(ST.slot[sl][0], ST.slot[sl][1], ST.slot[sl][2]));
+      cc = x + mul(Rm, mk3<Sc>(ST.slot[sl][0], ST.slot[sl][1], ST.slot[sl][2]));
       rad = ST.slot[sl][3];
-      act = cc.z - rad < (float)PBG_CONTACT_THRESHOLD;
+      act = cc.z - rad < (Sc)PBG_CONTACT_THRESHOLD;
     }
     const uint64_t bal = __ballot(act);
     const uint64_t mine = bal & gang_mask;
@@ -1647,8 +1729,8 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     if (act) {
       csig += pbg_contact_hash(sub, (uint32_t)sl);  // this lane's share of the signature
       const int c = nc + __popcll(bal & gang_mask & below);
-      const f3 cp = mk3(cc.x, cc.y, cc.z - rad);
-      put_desc(c, cp - O, mk3(0, 0, 0), mk3(0, 0, 1), cc.z - rad, 0.f, TB.chain[ST.slot_body[sl]], 0u, 1.f, ST.slot_mu[sl]);
+      const V3<Sc> cp = mk3<Sc>(cc.x, cc.y, cc.z - rad);
+      put_desc(c, cp - O, mk3<Sc>(0, 0, 0), mk3<Sc>(0, 0, 1), cc.z - rad, 0.f, TB.chain[ST.slot_body[sl]], 0u, 1.f, ST.slot_mu[sl]);
     }
     nc += __popcll(mine);
   });
@@ -1663,42 +1745,42 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     for (int r = 0; r < (R::NPAIR + T - 1) / T; r++) {  // rounds unrolled: their loads overlap
       const int pp = r * T + X.t;
       bool act = false;
-      f3 PA, PB, nrm;
-      float dist = 0.f;
+      V3<Sc> PA, PB, nrm;
+      Sc dist = 0.f;
       int ga = 0, gb = 0;
       if (pp < R::NPAIR) {
         ga = TB.pga[pp]; gb = TB.pgb[pp];
-        const lds_float* ea = X.l + O_GE + 6 * ga;
-        const lds_float* eb = X.l + O_GE + 6 * gb;
-        const f3 a0 = mk3(ea[0], ea[1], ea[2]), a1 = mk3(ea[3], ea[4], ea[5]);
-        const f3 b0 = mk3(eb[0], eb[1], eb[2]), b1 = mk3(eb[3], eb[4], eb[5]);
-        const f3 dc = (a0 + a1) - (b0 + b1);
+        const LW* ea = X.l + O_GE + 6 * ga;
+        const LW* eb = X.l + O_GE + 6 * gb;
+        const V3<Sc> a0 = mk3<Sc>(ea[0], ea[1], ea[2]), a1 = mk3<Sc>(ea[3], ea[4], ea[5]);
+        const V3<Sc> b0 = mk3<Sc>(eb[0], eb[1], eb[2]), b1 = mk3<Sc>(eb[3], eb[4], eb[5]);
+        const V3<Sc> dc = (a0 + a1) - (b0 + b1);
         if (dot3(dc, dc) <= TB.pbound2[pp]) {
           // closest points of two segments (same branch structure as the lane kernel)
-          const f3 d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
-          const float aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
-          float ss, tt;
-          const float eps = 1e-12f;
+          const V3<Sc> d1 = a1 - a0, d2 = b1 - b0, r0 = a0 - b0;
+          const Sc aa = dot3(d1, d1), ee = dot3(d2, d2), ff = dot3(d2, r0);
+          Sc ss, tt;
+          const Sc eps = Sc(1e-12);
           if (aa <= eps && ee <= eps) { ss = tt = 0.f; }
-          else if (aa <= eps) { ss = 0.f; tt = fminf(fmaxf(ff / ee, 0.f), 1.f); }
+          else if (aa <= eps) { ss = 0.f; tt = tmin(tmax(ff / ee, 0.f), 1.f); }
           else {
-            const float cc2 = dot3(d1, r0);
-            if (ee <= eps) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
+            const Sc cc2 = dot3(d1, r0);
+            if (ee <= eps) { tt = 0.f; ss = tmin(tmax(-cc2 / aa, 0.f), 1.f); }
             else {
-              const float bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
-              ss = den > eps ? fminf(fmaxf((bb2 * ff - cc2 * ee) / den, 0.f), 1.f) : 0.f;
+              const Sc bb2 = dot3(d1, d2), den = aa * ee - bb2 * bb2;
+              ss = den > eps ? tmin(tmax((bb2 * ff - cc2 * ee) / den, 0.f), 1.f) : 0.f;
               tt = (bb2 * ss + ff) / ee;
-              if (tt < 0.f) { tt = 0.f; ss = fminf(fmaxf(-cc2 / aa, 0.f), 1.f); }
-              else if (tt > 1.f) { tt = 1.f; ss = fminf(fmaxf((bb2 - cc2) / aa, 0.f), 1.f); }
+              if (tt < 0.f) { tt = 0.f; ss = tmin(tmax(-cc2 / aa, 0.f), 1.f); }
+              else if (tt > 1.f) { tt = 1.f; ss = tmin(tmax((bb2 - cc2) / aa, 0.f), 1.f); }
             }
           }
-          const f3 ca = a0 + ss * d1, cb = b0 + tt * d2;
-          const f3 dv = ca - cb;
-          const float dd = norm3(dv);
-          const float ra = TB.gp0[ga][3], rb = TB.gp0[gb][3];
+          const V3<Sc> ca = a0 + ss * d1, cb = b0 + tt * d2;
+          const V3<Sc> dv = ca - cb;
+          const Sc dd = norm3(dv);
+          const Sc ra = TB.gp0[ga][3], rb = TB.gp0[gb][3];
           dist = dd - ra - rb;
-          act = dist < (float)PBG_CONTACT_THRESHOLD;
-          nrm = dd > 1e-9f ? fast_rcp(dd) * dv : mk3(0, 0, 1);
+          act = dist < (Sc)PBG_CONTACT_THRESHOLD;
+          nrm = dd > Sc(1e-9) ? fast_rcp(dd) * dv : mk3<Sc>(0, 0, 1);
           PA = ca - ra * nrm;
           PB = cb + rb * nrm;
         }
@@ -1717,55 +1799,55 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   // candidate per lane, compacted in candidate order ------------------------------------------
   if constexpr (R::harder) {
     constexpr int NCC = 8 + R::NCG;
-    const float h = (float)PBG_CUBE_HALF, thr = (float)PBG_CONTACT_THRESHOLD;
-    const m3 Rc = quat_to_m3(X.l[G::O_CS + 3], X.l[G::O_CS + 4], X.l[G::O_CS + 5], X.l[G::O_CS + 6]);
-    const f3 xc = mk3(X.l[G::O_CS], X.l[G::O_CS + 1], X.l[G::O_CS + 2]);
+    const Sc h = (Sc)PBG_CUBE_HALF, thr = (Sc)PBG_CONTACT_THRESHOLD;
+    const M3<Sc> Rc = quat_to_m3(X.l[G::O_CS + 3], X.l[G::O_CS + 4], X.l[G::O_CS + 5], X.l[G::O_CS + 6]);
+    const V3<Sc> xc = mk3<Sc>(X.l[G::O_CS], X.l[G::O_CS + 1], X.l[G::O_CS + 2]);
 #pragma unroll
     for (int r = 0; r < (NCC + T - 1) / T; r++) {
       const int k = r * T + X.t;
       bool act = false;
-      f3 rA, rB, nrm;
-      float dist = 0.f, mu = 0.f, fA = 1.f, cube = 0.f, flo = 0.f;
+      V3<Sc> rA, rB, nrm;
+      Sc dist = 0.f, mu = 0.f, fA = 1.f, cube = 0.f, flo = 0.f;
       uint32_t mA = 0u;
       if (k < 8) {  // corner k vs the floor: A = the cube, normal +z
-        const f3 lc = mk3((k & 1) ? h : -h, (k & 2) ? h : -h, (k & 4) ? h : -h);
-        const f3 pp = xc + mul(Rc, lc);
+        const V3<Sc> lc = mk3<Sc>((k & 1) ? h : -h, (k & 2) ? h : -h, (k & 4) ? h : -h);
+        const V3<Sc> pp = xc + mul(Rc, lc);
         act = pp.z < thr;
-        rA = pp - xc; rB = mk3(0, 0, 0); nrm = mk3(0, 0, 1);
-        dist = pp.z; mu = (float)R::cube_floor_mu; fA = 0.f; cube = 1.f; flo = 1.f;
+        rA = pp - xc; rB = mk3<Sc>(0, 0, 0); nrm = mk3<Sc>(0, 0, 1);
+        dist = pp.z; mu = (Sc)R::cube_floor_mu; fA = 0.f; cube = 1.f; flo = 1.f;
       } else if (k < NCC) {  // robot geom g vs the box: A = the robot link, B = the cube
         const int g = k - 8;
         int lnk = 0;
-        float gp0[3], gp1[3], rr = 0.f, gmu = 0.f;
+        Sc gp0[3], gp1[3], rr = 0.f, gmu = 0.f;
         static_for<0, R::NCG>([&](auto g_c) {  // the geom's constants by selects (no table loads)
           constexpr int gg = decltype(g_c)::value;
           if (g == gg) {
             lnk = R::cgeom_link[gg];
 #pragma unroll
-            for (int i = 0; i < 3; i++) { gp0[i] = (float)R::cgeom_p0[gg][i]; gp1[i] = (float)R::cgeom_p1[gg][i]; }
-            rr = (float)R::cgeom_r[gg];
-            gmu = (float)R::cgeom_mu[gg];
+            for (int i = 0; i < 3; i++) { gp0[i] = (Sc)R::cgeom_p0[gg][i]; gp1[i] = (Sc)R::cgeom_p1[gg][i]; }
+            rr = (Sc)R::cgeom_r[gg];
+            gmu = (Sc)R::cgeom_mu[gg];
           }
         });
-        m3 Rm; f3 x;
+        M3<Sc> Rm; V3<Sc> x;
         frame(lnk + 1, Rm, x);
-        const f3 e0 = x + mul(Rm, mk3(gp0[0], gp0[1], gp0[2])), e1 = x + mul(Rm, mk3(gp1[0], gp1[1], gp1[2]));
-        m3 Rt;
+        const V3<Sc> e0 = x + mul(Rm, mk3<Sc>(gp0[0], gp0[1], gp0[2])), e1 = x + mul(Rm, mk3<Sc>(gp1[0], gp1[1], gp1[2]));
+        M3<Sc> Rt;
 #pragma unroll
         for (int i = 0; i < 3; i++)
 #pragma unroll
           for (int j = 0; j < 3; j++) Rt.m[3 * i + j] = Rc.m[3 * j + i];
-        const f3 p0 = mul(Rt, e0 - xc), p1 = mul(Rt, e1 - xc), d = p1 - p0;
-        const float dd = dot3(d, d);
-        const float t0 = dd > 1e-12f ? fminf(fmaxf(-dot3(p0, d) / dd, 0.f), 1.f) : 0.f;
-        const float bound = (float)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
+        const V3<Sc> p0 = mul(Rt, e0 - xc), p1 = mul(Rt, e1 - xc), d = p1 - p0;
+        const Sc dd = dot3(d, d);
+        const Sc t0 = dd > Sc(1e-12) ? tmin(tmax(-dot3(p0, d) / dd, 0.f), 1.f) : 0.f;
+        const Sc bound = (Sc)(1.7320508075688772 * PBG_CUBE_HALF);  // circumradius
         if (norm3(p0 + t0 * d) < bound + rr + thr) {
-          float t = 0.f;
-          if (dd > 1e-12f) {  // golden-section minimisation of the box's signed distance along the segment
-            const float phi = 0.6180339887498949f;
-            float a = 0.f, bb = 1.f;
-            float x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
-            float f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
+          Sc t = 0.f;
+          if (dd > Sc(1e-12)) {  // golden-section minimisation of the box's signed distance along the segment
+            const Sc phi = Sc(0.6180339887498949);
+            Sc a = 0.f, bb = 1.f;
+            Sc x1 = bb - phi * (bb - a), x2 = a + phi * (bb - a);
+            Sc f1 = box_sd(p0 + x1 * d, h), f2 = box_sd(p0 + x2 * d, h);
 #pragma unroll 1
             for (int it = 0; it < PBG_CUBE_GS_ITERS; it++) {
               if (f1 <= f2) { bb = x2; x2 = x1; f2 = f1; x1 = bb - phi * (bb - a); f1 = box_sd(p0 + x1 * d, h); }
@@ -1773,25 +1855,25 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
             }
             t = 0.5f * (a + bb);
           }
-          const f3 ps = p0 + t * d;
+          const V3<Sc> ps = p0 + t * d;
           dist = box_sd(ps, h) - rr;
           act = dist < thr;
-          f3 nb, qb;
-          const float qx = fabsf(ps.x) - h, qy = fabsf(ps.y) - h, qz = fabsf(ps.z) - h;
-          if (fmaxf(qx, fmaxf(qy, qz)) > 0.f) {
-            qb = mk3(fminf(fmaxf(ps.x, -h), h), fminf(fmaxf(ps.y, -h), h), fminf(fmaxf(ps.z, -h), h));
-            const f3 dv = ps - qb;
-            const float l = norm3(dv);
-            nb = l > 1e-9f ? (1.f / l) * dv : mk3(0, 0, 1);
+          V3<Sc> nb, qb;
+          const Sc qx = tabs(ps.x) - h, qy = tabs(ps.y) - h, qz = tabs(ps.z) - h;
+          if (tmax(qx, tmax(qy, qz)) > 0.f) {
+            qb = mk3<Sc>(tmin(tmax(ps.x, -h), h), tmin(tmax(ps.y, -h), h), tmin(tmax(ps.z, -h), h));
+            const V3<Sc> dv = ps - qb;
+            const Sc l = norm3(dv);
+            nb = l > Sc(1e-9) ? (1.f / l) * dv : mk3<Sc>(0, 0, 1);
           } else {
             const int ax = (qx >= qy && qx >= qz) ? 0 : (qy >= qz ? 1 : 2);
-            const float cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
-            const float sg = cc < 0.f ? -1.f : 1.f;
-            nb = mk3(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
-            qb = mk3(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
+            const Sc cc = ax == 0 ? ps.x : (ax == 1 ? ps.y : ps.z);
+            const Sc sg = cc < 0.f ? -1.f : 1.f;
+            nb = mk3<Sc>(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
+            qb = mk3<Sc>(ax == 0 ? sg * h : ps.x, ax == 1 ? sg * h : ps.y, ax == 2 ? sg * h : ps.z);
           }
           nrm = mul(Rc, nb);
-          const f3 PA = xc + mul(Rc, ps) - rr * nrm, PB = xc + mul(Rc, qb);
+          const V3<Sc> PA = xc + mul(Rc, ps) - rr * nrm, PB = xc + mul(Rc, qb);
           rA = PA - O; rB = PB - xc;
           mu = gmu; cube = -1.f;
           mA = lnk >= 0 ? TB.chain[lnk + 1] : 0u;
@@ -1815,7 +1897,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     } else {
       // --- replicated: factorisation and the unconstrained velocity, staged for the PGS ----
       // (the factor stays in Lr / Ldr for the rows pass: no reload from LDS)
-      float rhs[N], nu[N], u[N];
+      Sc rhs[N], nu[N], u[N];
 #pragma unroll
       for (int i = 0; i < D::NNZ; i++) Lr[i] = X.l[G::O_L + i];
 #pragma unroll
@@ -1841,12 +1923,12 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 #pragma unroll 1
   for (int j = X.t; wave_any(j < njobs); j += T) {
     if (j >= njobs) continue;
-    float J[N];
+    Sc J[N];
     const bool is_lim = j < NLIM;
     int c = 0, dir = 0;
-    float dist = 0.f;
-    float cubef = 0.f;            // HumanoidFlagrunHarder: the contact's cube side (descriptor word 15)
-    f3 ycl = mk3(0, 0, 0), cubes = mk3(0, 0, 0);  // and the cube part of y (linear | angular)
+    Sc dist = 0.f;
+    Sc cubef = 0.f;            // HumanoidFlagrunHarder: the contact's cube side (descriptor word 15)
+    V3<Sc> ycl = mk3<Sc>(0, 0, 0), cubes = mk3<Sc>(0, 0, 0);  // and the cube part of y (linear | angular)
     if (is_lim) {
       const int g = TB.lim_g[j];
 #pragma unroll
@@ -1854,45 +1936,45 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     } else {
       c = (j - NLIM) / 3;
       dir = (j - NLIM) - 3 * c;
-      float v[G::DW];
+      Sc v[G::DW];
       contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
         for (int w = 0; w < G::DW; w++) v[w] = p[w];
       });
-      const f3 rA = mk3(v[0], v[1], v[2]), rB = mk3(v[3], v[4], v[5]), nrm = mk3(v[6], v[7], v[8]);
+      const V3<Sc> rA = mk3<Sc>(v[0], v[1], v[2]), rB = mk3<Sc>(v[3], v[4], v[5]), nrm = mk3<Sc>(v[6], v[7], v[8]);
       dist = v[9];
-      const float fB = v[11];
-      const uint32_t mA = __builtin_bit_cast(uint32_t, v[12]), mB = __builtin_bit_cast(uint32_t, v[13]);
-      f3 t1, t2;  // btPlaneSpace1(nrm); the floor's (+z) gives (0,-1,0), (1,0,0)
-      if (v[14] != 0.f) { t1 = mk3(0, -1, 0); t2 = mk3(1, 0, 0); }
-      else if (fabsf(nrm.z) > 0.7071067811865476f) {
-        const float a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
-        t1 = mk3(0, -nrm.z * kinv, nrm.y * kinv);
-        t2 = mk3(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
+      const Sc fB = v[11];
+      const uint32_t mA = word_mask(v[12]), mB = word_mask(v[13]);
+      V3<Sc> t1, t2;  // btPlaneSpace1(nrm); the floor's (+z) gives (0,-1,0), (1,0,0)
+      if (v[14] != 0.f) { t1 = mk3<Sc>(0, -1, 0); t2 = mk3<Sc>(1, 0, 0); }
+      else if (tabs(nrm.z) > Sc(0.7071067811865476)) {
+        const Sc a2 = nrm.y * nrm.y + nrm.z * nrm.z, kinv = fast_rsq(a2);
+        t1 = mk3<Sc>(0, -nrm.z * kinv, nrm.y * kinv);
+        t2 = mk3<Sc>(a2 * kinv, -nrm.x * t1.z, nrm.x * t1.y);
       } else {
-        const float a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
-        t1 = mk3(-nrm.y * kinv, nrm.x * kinv, 0);
-        t2 = mk3(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
+        const Sc a2 = nrm.x * nrm.x + nrm.y * nrm.y, kinv = fast_rsq(a2);
+        t1 = mk3<Sc>(-nrm.y * kinv, nrm.x * kinv, 0);
+        t2 = mk3<Sc>(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
       }
-      const f3 nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
-      const f3 mmA = cross3(rA, nd), mmB = cross3(rB, nd);
+      const V3<Sc> nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
+      const V3<Sc> mmA = cross3(rA, nd), mmB = cross3(rB, nd);
       cubef = v[15];
-      cubes = mk3(0, 0, 0);
+      cubes = mk3<Sc>(0, 0, 0);
       if constexpr (R::harder) {  // the cube's columns: +-(nd / sqrt m, (r x nd) / sqrt I), r its lever arm
-        const f3 rc = cubef > 0.f ? rA : rB;
-        const f3 mc = cross3(rc, nd);
-        const float rm = 1.f / CubeK<float>::sm(), rI = 1.f / CubeK<float>::sI();
+        const V3<Sc> rc = cubef > 0.f ? rA : rB;
+        const V3<Sc> mc = cross3(rc, nd);
+        const Sc rm = Sc(1) / CubeK<Sc>::sm(), rI = Sc(1) / CubeK<Sc>::sI();
         ycl = cubef * rm * nd;
         cubes = cubef * rI * mc;
       }
-      const float fA = v[10];
+      const Sc fA = v[10];
 #pragma unroll
       for (int i = 0; i < N; i++) {
         const int di = D::dof_of(i);
         const bool inA = di < 0 ? fA != 0.f : ((mA >> di) & 1u) != 0u, inB = di < 0 ? fB != 0.f : ((mB >> di) & 1u) != 0u;
-        const f3 sw = mk3(X.l[G::O_SW + G::SS * i], X.l[G::O_SW + G::SS * i + 1], X.l[G::O_SW + G::SS * i + 2]);
-        const f3 sv = mk3(X.l[G::O_SV + G::SS * i], X.l[G::O_SV + G::SS * i + 1], X.l[G::O_SV + G::SS * i + 2]);
-        float tj = 0.f;
+        const V3<Sc> sw = mk3<Sc>(X.l[G::O_SW + G::SS * i], X.l[G::O_SW + G::SS * i + 1], X.l[G::O_SW + G::SS * i + 2]);
+        const V3<Sc> sv = mk3<Sc>(X.l[G::O_SV + G::SS * i], X.l[G::O_SV + G::SS * i + 1], X.l[G::O_SV + G::SS * i + 2]);
+        Sc tj = 0.f;
         if (inA) tj += dot3(nd, sv) + dot3(mmA, sw);
         if (inB) tj -= dot3(nd, sv) + dot3(mmB, sw);
         J[i] = tj;
@@ -1900,11 +1982,11 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     }
     // y = L^-1 J (forward substitution over the compile-time pattern of L, held in registers for
     // the pass: 16-byte loads of the staged factor before the job loop)
-    float y[N];
-    float D2 = 0.f;
+    Sc y[N];
+    Sc D2 = 0.f;
 #pragma unroll
     for (int i = 0; i < N; i++) {
-      float tt = J[i];
+      Sc tt = J[i];
 #pragma unroll
       for (int kk = 0; kk < i; kk++)
         if (D::coupled(i, kk)) tt -= (LREG ? Lr[DIST ? FP<R>::idx(i, kk) : D::lidx(i, kk)] : X.l[G::O_L + FP<R>::idx(i, kk)]) * y[kk];
@@ -1912,9 +1994,9 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       D2 += y[i] * y[i];
     }
     if constexpr (R::harder) D2 += dot3(ycl, ycl) + dot3(cubes, cubes);
-    const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
+    const Sc meff = D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f;
     if (is_lim) {
-      const float plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
+      const Sc plo = X.l[G::O_LP + 2 * j], phi = X.l[G::O_LP + 2 * j + 1];
       limit_at<R, T>(X, j, [&](auto p) {
 #pragma unroll
         for (int i = 0; i < YS; i++) p[i] = i < N ? y[i] : 0.f;
@@ -1924,10 +2006,10 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
       });
     } else {
       const int w0r = G::RW0 + dir * G::CRW;
-      const float tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
+      const Sc tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
       contact_at<R, T>(X, c, [&](auto p0) {
         auto p = p0 + w0r;
-        const float yc[6] = {ycl.x, ycl.y, ycl.z, cubes.x, cubes.y, cubes.z};
+        const Sc yc[6] = {ycl.x, ycl.y, ycl.z, cubes.x, cubes.y, cubes.z};
 #pragma unroll
         for (int i = 0; i < YS; i++) p[G::yw(i)] = i < N ? y[i] : (i < G::NY ? yc[(i - N) % 6] : 0.f);
         p[YS] = meff;
@@ -1939,7 +2021,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   PBG_GANG_SYNC
   STAMP(11)
   // --- PGS: 5 sweeps, Bullet order (scene_bases.py:65 numSolverIterations=5) -------------
-  float us[NSL];
+  Sc us[NSL];
 #pragma unroll
   for (int m = 0; m < NSL; m++) us[m] = X.l[G::O_U + X.t + m * T];
   {
@@ -1948,7 +2030,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     constexpr int NLIM = 0;
 #endif
     constexpr int NL1 = NLIM > 0 ? NLIM : 1;
-    float ly[NL1][NSL], lm[NL1], lrm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
+    Sc ly[NL1][NSL], lm[NL1], lrm[NL1], ltl[NL1], lth[NL1], llo[NL1], lhi[NL1];
 #pragma unroll
     for (int li = 0; li < NLIM; li++) {
       limit_at<R, T>(X, li, [&](auto p) {
@@ -1965,22 +2047,22 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
     for (int it = 0; it < P.iterations; it++) {
 #pragma unroll
       for (int li = 0; li < NLIM; li++) {
-        float part = 0.f;
+        Sc part = 0.f;
 #pragma unroll
         for (int m = 0; m < NSL; m++) part += ly[li][m] * us[m];
-        const float yu = gang_sum<T>(part);
-        const float meff = lm[li];
-        const float nlo = clampf(llo[li] + meff * (ltl[li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-        const float dlo = nlo - llo[li];
+        const Sc yu = gang_sum<T>(part);
+        const Sc meff = lm[li];
+        const Sc nlo = clampf(llo[li] + meff * (ltl[li] - yu), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+        const Sc dlo = nlo - llo[li];
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
         // lrm = 0 when meff = 0: no select on the chain (Atlas keeps it: without it the allocator
         // spilled 48 bytes of its 512 registers)
-        const float yu2 = G::NSL > 2 && !(meff > 0.f) ? yu : yu + dlo * lrm[li];
-        const float nhi = clampf(lhi[li] + meff * (lth[li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-        const float dhi = nhi - lhi[li];
+        const Sc yu2 = G::NSL > 2 && !(meff > 0.f) ? yu : yu + dlo * lrm[li];
+        const Sc nhi = clampf(lhi[li] + meff * (lth[li] + yu2), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+        const Sc dhi = nhi - lhi[li];
         llo[li] = nlo;
         lhi[li] = nhi;
-        const float dl = dlo - dhi;
+        const Sc dl = dlo - dhi;
 #pragma unroll
         for (int m = 0; m < NSL; m++) us[m] += ly[li][m] * dl;
       }
@@ -2001,7 +2083,7 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
   if constexpr (DIST && G::LST) {
     gang_front_integrate<R, T>(s, X);
   } else {
-    float L[D::NNZ], Ld[N], u[N], nu[N];
+    Sc L[D::NNZ], Ld[N], u[N], nu[N];
     // the staged factor in Dims<R>::lidx order (a compile-time permutation of its LDS words)
     static_for<0, N>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
@@ -2024,10 +2106,12 @@ PBG_DEV int gang_substep(State<R>& s, const float* tau, const GangCtx& X, uint64
 // t+T, ... ([env][D]) -- a few full-wave stores instead of one partial store per word from
 // lane 0, whose queue of ~100 outstanding stores stalled the wave.
 template <class R, int T>
-PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __restrict__ st, int n,
+PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], real_t<R>* __restrict__ st, int n,
                         float* __restrict__ obs_out, int e, int t) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   constexpr int SW = PBG_STATE_WORDS(R::NJ, R::harder);
-  float w[SW];  // store_state's word order
+  Sc w[SW];  // store_state's word order
 #pragma unroll
   for (int i = 0; i < 3; i++) { w[i] = s.bp[i]; w[7 + i] = s.bv[i]; w[10 + i] = s.bw[i]; }
 #pragma unroll
@@ -2043,7 +2127,7 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
   }
   static_for<0, (SW + T - 1) / T>([&](auto m_c) {
     constexpr int m = decltype(m_c)::value;
-    const float v = lanes_pick<T, m, SW>(w, t);
+    const Sc v = lanes_pick<T, m, SW>(w, t);
     if (m * T + t < SW) st[(size_t)(m * T + t) * n + e] = v;
   });
   lanes_store_row<R, T>(obs, obs_out, e, t);
@@ -2052,12 +2136,14 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], float* __
 template <class R, int T, bool DIST>
 __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   using G = Gang<R, T>;
   using TT = GangTabs<R>;
   constexpr int BLK = gang_block<R>();
   constexpr int EPB = BLK / T;  // envs per workgroup
-  lds_float* lds = (lds_float*)lds_dyn;
+  lds_float* lds = (lds_float*)lds_dyn;  // the model tables (4-byte words), then the env regions
   {
     const uint32_t* src0 = (const uint32_t*)&g_gang_tab<R>;
     const uint32_t* src1 = (const uint32_t*)&g_gang_dyn<R>;
@@ -2066,7 +2152,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     for (int i = threadIdx.x; i < (int)(sizeof(GangDynTab<R>) / 4); i += BLK) dst[TT::TAB_WORDS + i] = src1[i];
   }
   __syncthreads();
-  GangCtx X;
+  GangCtx<R> X;
   X.tabs = lds;
   X.t = threadIdx.x % T;
   X.le = threadIdx.x / T;
@@ -2076,13 +2162,13 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   // (env_words is a multiple of REGION_ALIGN: saying so lets the compiler prove the 8 / 16-byte
   // alignment of the region's fixed words and use b64 / b128 LDS accesses with offsets instead
   // of ds_read2_b32 pairs, whose 8-bit offsets needed a v_add_u32 for every address)
-  X.l = lds + TT::WORDS + (threadIdx.x / T) * (env_words & ~(G::REGION_ALIGN - 1));
-  X.g = scratch + (size_t)e * G::GWORDS;
+  X.l = (LW*)(lds + TT::WORDS) + (threadIdx.x / T) * (env_words & ~(G::REGION_ALIGN - 1));
+  X.g = (Sc*)scratch + (size_t)e * G::GWORDS;
   X.cap = cap;
 #ifdef PBG_DEV_CHECKS
   X.env_words = env_words;
 #endif
-  X.P = B.sp;
+  X.P = sp_of<R>(B);
   const bool w0 = X.t == 0;
   STAMP_DECL
   State<R> s;
@@ -2093,13 +2179,13 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   constexpr bool LST = DIST && G::LST;  // the front path: the state in LDS through the sub-steps
   if constexpr (LST) gang_put_state<R, T>(s, X);
   // apply_action: tau = power * power_coef * clip(a, -1, 1)   (robot_locomotors.py:26-29)
-  float tau[R::NJ];
+  Sc tau[R::NJ];
 #pragma unroll
   for (int d = 0; d < R::NJ; d++) tau[d] = 0.f;
 #pragma unroll
   for (int i = 0; i < R::NA; i++) {
     const float c = fminf(fmaxf(act[i], -1.f), 1.f);
-    tau[R::act_dof[i]] += (float)(R::act_gain[i] * (double)c);
+    tau[R::act_dof[i]] += (Sc)(R::act_gain[i] * (double)c);
   }
   if (w0) {
 #pragma unroll
@@ -2109,7 +2195,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   int nc = 0;
   uint32_t csig = 0;  // per-lane share; gang-summed below
   STAMP(7)
-  for (int sub = 0; sub < B.sp.substeps; sub++)
+  for (int sub = 0; sub < X.P.substeps; sub++)
     nc = gang_substep<R, T, DIST>(s, tau, X, slot_bits, (uint32_t)sub, csig SUB_STAMP_PASS);
   if constexpr (LST) {
     gang_get_state<R, T>(s, X);  // (the sub-step ends with a gang sync)
@@ -2127,7 +2213,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   const double pot_old = B.pot[e];
-  const float z0_old = z0_of<R>(B)[e];
+  const Sc z0_old = z0_of<R>(B)[e];
   float obs[R::OBS];
   PackOut po;
   double pot_new = 0.0;
@@ -2174,7 +2260,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
       double pos[3], vel[3];
       if (harder_step<R>(B, e, in, obs, po, hb, pos, vel, nullptr)) {  // resetBasePosition / Velocity
 #pragma unroll
-        for (int i = 0; i < 3; i++) { s.cube.p[i] = (float)pos[i]; s.cube.v[i] = (float)vel[i]; s.cube.w[i] = 0.f; }
+        for (int i = 0; i < 3; i++) { s.cube.p[i] = (Sc)pos[i]; s.cube.v[i] = (Sc)vel[i]; s.cube.w[i] = 0.f; }
       }
     }
     pot_new = po.potential;
@@ -2197,7 +2283,7 @@ __global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gan
     if (io.term_obs) lanes_store_row<R, T>(obs, io.term_obs, e, X.t);
     bool has_floor = flags & 1u;
     double pot;
-    float z0;
+    Sc z0;
     // every lane reads the episode counter (one load instruction) before the writer bumps it
     const uint32_t epi = B.episode[e];
     if (w0) B.episode[e] = epi + 1;

@@ -71,8 +71,11 @@ template <class S>
 PBG_DEV S norm3(V3<S> a) { return fast_sqrt(dot3(a, a)); }
 // clamp(x, lo, hi) for lo <= hi in one v_med3_f32 (fminf(fmaxf()) costs two instructions
 // plus the IEEE canonicalisations of its operands); same result for non-NaN x
-PBG_DEV float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
-PBG_DEV double clampf(double x, double lo, double hi) { return __builtin_fmin(__builtin_fmax(x, lo), hi); }
+template <class S>
+PBG_DEV S clampf(S x, nd<S> lo, nd<S> hi) {
+  if constexpr (std::is_same<S, float>::value) return __builtin_amdgcn_fmed3f(x, lo, hi);
+  else return __builtin_fmin(__builtin_fmax(x, lo), hi);
+}
 
 
 // sin/cos for the moderate arguments of the physics (joint angles, exp-map half angles):

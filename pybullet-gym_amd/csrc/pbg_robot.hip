@@ -76,23 +76,32 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
   }
 }
 
+// robots and widths with a gang kernel: walkers (the cube robot on the front path); 32-lane gangs for
+// the Humanoid family in float32; float64 (F64<R>): 16 lanes, Atlas-sized models excluded
+template <class RR, int T>
+constexpr bool gang_ok() {
+  constexpr bool f64 = sizeof(real_t<RR>) == 8;
+  return (RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) &&
+         (T == 16 || (gang32_ok<RR>() && !f64)) && !(f64 && gang_big<RR>());
+}
 // Gang geometry (pbg_gang.hip): T = 16 or 32 lanes per env, 256 / T envs per 4-wave workgroup;
 // the per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
 // + 3 rows), contacts past the capacity spill to the device workspace.
 template <class RR, int T>
 static int plan_gang_t(int n_envs, int cus, Geometry* g) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>())) {
+  if constexpr (gang_ok<RR, T>()) {
     using G = Gang<RR, T>;
+    constexpr long WB = (long)sizeof(real_t<RR>);  // env-region word: 4 bytes, or 8 on the float64 path
     constexpr int EPB = gang_block<RR>() / T;  // envs per workgroup
     // the layout's floor (fixed words + the kinematic area, no LDS contact) must fit one CU's LDS
-    static_assert(4L * (GangTabs<RR>::WORDS + EPB * ((G::FIXED + G::MIN_CONTACT_WORDS + 3L) & ~3L)) <= 163840L,
+    static_assert(4L * GangTabs<RR>::WORDS + WB * EPB * ((G::FIXED + G::MIN_CONTACT_WORDS + 3L) & ~3L) <= 163840L,
                   "gang env regions exceed the CU's LDS");
     const int wgs = (n_envs + EPB - 1) / EPB;
     const int wpc = (wgs + cus - 1) / cus;
     // signed: with many workgroups per CU the share can be smaller than the model tables
-    long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - (long)sizeof(float) * (long)GangTabs<RR>::WORDS;
+    long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - 4L * (long)GangTabs<RR>::WORDS;
     if (budget < 0) budget = 0;
-    long words = budget / (long)(EPB * sizeof(float)) - G::FIXED;
+    long words = budget / (long)(EPB * WB) - G::FIXED;
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
@@ -102,23 +111,26 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
       const int w = G::FIXED + (c * G::PERC > G::MIN_CONTACT_WORDS ? c * G::PERC : G::MIN_CONTACT_WORDS);
       return (w + G::REGION_ALIGN - 1) & ~(G::REGION_ALIGN - 1);
     };
-    while (cap > 0 && (long)region(cap) * EPB * (long)sizeof(float) > budget) cap--;
+    while (cap > 0 && (long)region(cap) * EPB * WB > budget) cap--;
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
-    g->gang_dist = RR::NDOF >= 8 || T >= 32 || (size_t)n_envs * T > (size_t)64 * 4 * cus;
-    // pbg_create_debug (32-lane gangs and the cube robot have no replicated-dynamics variant)
-    if ((g->force_dist == 0 || g->force_dist == 1) && T == 16 && !RR::harder) g->gang_dist = g->force_dist;
+    // (float64: distributed always -- the replicated dynamics() of a whole robot per lane spills in float64)
+    constexpr bool REPL = T == 16 && !RR::harder && sizeof(real_t<RR>) == 4;  // has a replicated variant
+    g->gang_dist = !REPL || RR::NDOF >= 8 || (size_t)n_envs * T > (size_t)64 * 4 * cus;
+    // pbg_create_debug (32-lane gangs, the cube robot and float64 have no replicated-dynamics variant)
+    if ((g->force_dist == 0 || g->force_dist == 1) && REPL) g->gang_dist = g->force_dist;
     g->team = T;
     g->block = gang_block<RR>();
     g->lds_rows = cap;
     g->env_words = region(cap);
-    g->lds_bytes = sizeof(float) * ((size_t)GangTabs<RR>::WORDS + (size_t)EPB * (size_t)g->env_words);
+    g->lds_bytes = 4 * (size_t)GangTabs<RR>::WORDS + (size_t)WB * (size_t)EPB * (size_t)g->env_words;
     // the workgroup's regions must fit the CU's LDS (the contact floor MIN_CONTACT_WORDS is the only
     // term the budget does not bound: a model whose tables + floor exceed it is not launchable)
     if (g->lds_bytes > (size_t)163840) return (int)hipErrorInvalidConfiguration;
     g->scratch_words_per_env = G::GWORDS;
+    g->word_bytes = (int)WB;
     const void* fn;
-    if constexpr (T == 16 && !RR::harder)
+    if constexpr (REPL)
       fn = g->gang_dist ? (const void*)gang_step_kernel<RR, T, true> : (const void*)gang_step_kernel<RR, T, false>;
     else
       fn = (const void*)gang_step_kernel<RR, T, true>;
@@ -138,9 +150,9 @@ static int plan_gang(int n_envs, int cus, Geometry* g, int lanes) {
 }
 template <class RR, int T>
 static bool launch_gang_t(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
-  if constexpr ((RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>())) {
+  if constexpr (gang_ok<RR, T>()) {
     const dim3 grid(blocks(B.n, gang_block<RR>() / T)), blk(gang_block<RR>());
-    if constexpr (T == 16 && !RR::harder) {
+    if constexpr (T == 16 && !RR::harder && sizeof(real_t<RR>) == 4) {
       if (!g.gang_dist) {
         hipLaunchKernelGGL((gang_step_kernel<RR, T, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows,
                            g.env_words);
@@ -252,14 +264,20 @@ int PBG_FN(launch_pack_)(int n, const double* in, double* out, hipStream_t s) {
 }
 
 // ---- the reference-precision path (pbg_create_v2 precision 64): float64 physics state and
-// arithmetic (pybullet's btScalar, scene_bases.py:75-76), the lane-per-env kernel of every robot
-// with at most 128 floor-contact slots (Atlas: PBG_E_HIP at create)
+// arithmetic (pybullet's btScalar, scene_bases.py:75-76) for every robot with at most 128
+// floor-contact slots (Atlas: PBG_E_HIP at create).  mode 0: the lane-per-env
+// kernel (the float64 gang kernel's parity cross-check); otherwise the 16-lane gang kernel for the
+// walkers (Ant included: the quad kernel has no float64 variant) and the lane kernel for the
+// pendulums.
 using R64 = F64<R>;
 int PBG_FN(plan64_)(int n_envs, int cus, int mode, Geometry* g) {
-  (void)mode;
+  if constexpr (gang_ok<R64, 16>()) {
+    if (mode != 0) return plan_gang_t<R64, 16>(n_envs, cus, g);
+  }
   return plan_lane<R64>(n_envs, cus, g);
 }
 int PBG_FN(launch_step64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if (g.team == 16 && launch_gang_t<R64, 16>(B, io, scratch, g, s)) return (int)hipGetLastError();
   return launch_lane<R64>(B, io, scratch, g, s);
 }
 int PBG_FN(launch_reset64_)(const Buffers& B, const ResetIO& io, hipStream_t s) {

@@ -263,10 +263,16 @@ PBG_DEV const SimPT<real_t<R>>& sp_of(const Buffers& B) {
 // precision-generic libm pieces (float: the f-suffixed calls the float32 kernels always made)
 PBG_DEV float tabs(float x) { return fabsf(x); }
 PBG_DEV double tabs(double x) { return fabs(x); }
-PBG_DEV float tmin(float a, float b) { return fminf(a, b); }
-PBG_DEV double tmin(double a, double b) { return fmin(a, b); }
-PBG_DEV float tmax(float a, float b) { return fmaxf(a, b); }
-PBG_DEV double tmax(double a, double b) { return fmax(a, b); }
+template <class S>
+PBG_DEV S tmin(S a, nd<S> b) {
+  if constexpr (std::is_same<S, float>::value) return fminf(a, b);
+  else return fmin(a, b);
+}
+template <class S>
+PBG_DEV S tmax(S a, nd<S> b) {
+  if constexpr (std::is_same<S, float>::value) return fmaxf(a, b);
+  else return fmax(a, b);
+}
 PBG_DEV float tsqrt(float x) { return sqrtf(x); }
 PBG_DEV double tsqrt(double x) { return sqrt(x); }
 
@@ -337,9 +343,9 @@ PBG_DEV void store_state(const State<R>& s, real_t<R>* __restrict__ st, int n, i
 // Stores of a value replicated over T cooperating lanes (gang / quad kernels), dealt over
 // them: lane t stores elements t, t+T, ... -- each element picked by selects, so the
 // register arrays are never indexed at run time.
-template <int T, int M, int W>
-PBG_DEV float lanes_pick(const float (&v)[W], int t) {  // v[M*T + t] by selects (no indexed registers)
-  float r = v[M * T];
+template <int T, int M, int W, class V>
+PBG_DEV V lanes_pick(const V (&v)[W], int t) {  // v[M*T + t] by selects (no indexed registers)
+  V r = v[M * T];
   static_for<1, T>([&](auto k_c) {
     constexpr int k = decltype(k_c)::value;
     if constexpr (M * T + k < W) r = t == k ? v[M * T + k] : r;

@@ -57,7 +57,7 @@ def _state_rel(a, b):
     return (np.abs(a - b) / np.maximum(1.0, np.abs(b))).max(axis=1)
 
 
-def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None):
+def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None, **opts):
     """The GPU float64 handle steps all n envs (auto-reset, Philox actions); before each step the
     sampled envs' float64 state records go to the oracle (and to N probes perturbed by 1e-12
     relative), which steps them; compared as in the module docstring."""
@@ -66,7 +66,7 @@ def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None
         sp.update(sim)
         oracle.set_sim_params(sp)
     try:
-        env = VecEnv(env_id, n, seed=seed, autoreset=True, precision=64, sim_params=sim)
+        env = VecEnv(env_id, n, seed=seed, autoreset=True, precision=64, sim_params=sim, **opts)
         assert env.precision == 64
         env.reset()
         idx = np.arange(n) if sample is None else np.linspace(0, n - 1, sample).astype(np.int64)
@@ -254,3 +254,83 @@ def test_f64_atlas_is_refused():
     from pybulletgym_amd._native import PbgError
     with pytest.raises(PbgError):
         VecEnv("AtlasPyBulletEnv-v0", 4, precision=64)
+
+
+# ------------------------------------------------------------------ float64 kernel variants
+# The float64 walkers run the 16-lane gang kernel (pbg_gang.hip instantiated on F64<R>; Ant
+# included -- the quad kernel has no float64 variant); kernel=0 selects the float64 lane-per-env
+# kernel, which stays the pendulums' path and the gang kernel's cross-check.
+@pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HopperPyBulletEnv-v0",
+                                    "HumanoidFlagrunHarderPyBulletEnv-v0"])
+def test_f64_lane_kernel_teacher_forced(env_id):
+    """The float64 lane kernel against the float64 oracle, same bounds."""
+    _teacher_forced64(env_id, 128, 40, name=f"f64_lane[{env_id}]", kernel=0)
+
+
+@pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
+                                    "Walker2DPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0",
+                                    "HumanoidFlagrunHarderPyBulletEnv-v0"])
+def test_f64_gang_matches_f64_lane(env_id):
+    """Float64 gang vs float64 lane kernel from the same states every step: the same contact sets
+    and the state within 1e-9 (different summation orders in float64)."""
+    n = 256
+    g = VecEnv(env_id, n, seed=3, autoreset=False, precision=64)
+    ln = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, kernel=0)
+    assert g.info.lanes_per_env == 16 and ln.info.lanes_per_env == 1
+    r = np.random.default_rng(7)
+    g.reset(init_q=torch.from_numpy(r.uniform(-0.1, 0.1, (n, g.info.reset_dofs)).astype(np.float32)))
+    errs, same_n = [], 0
+    for t in range(30):
+        phys, aux = g.get_state()
+        ln.set_state(phys, aux)
+        a = torch.from_numpy(r.uniform(-1, 1, (n, g.info.action_dim)).astype(np.float32)).cuda()
+        g.step(a, want_contacts=True)
+        ln.step(a, want_contacts=True)
+        same = (g.contact_sig == ln.contact_sig).cpu().numpy()
+        sg, sl = g.get_state()[0].cpu().numpy(), ln.get_state()[0].cpu().numpy()
+        errs.append(_state_rel(sg, sl)[same])
+        same_n += int(same.sum())
+        np.testing.assert_array_equal(g.ncontact.cpu().numpy()[same], ln.ncontact.cpu().numpy()[same])
+    e = np.concatenate(errs)
+    rec = dict(test=f"f64_gang_vs_lane[{env_id}]", same_frac=same_n / (30 * n), max_rel=float(e.max()),
+               share_within_1e_9=float((e <= STATE_REL64).mean()))
+    _report(rec)
+    assert rec["same_frac"] >= 1 - LOOSE_FRAC64 and rec["share_within_1e_9"] >= SHARE64 and rec["max_rel"] <= HARD_MAX64, rec
+
+
+def test_f64_gang_workspace_contacts_bitwise_equal_lds_contacts():
+    """Float64 gang contacts past the LDS capacity (lds_rows=0: all in the device workspace) change
+    no bit (Humanoid: floor + self contacts)."""
+    def run(**kw):
+        e = VecEnv("HumanoidPyBulletEnv-v0", 128, seed=11, autoreset=True, precision=64, **kw)
+        e.reset()
+        gen = torch.Generator(device="cuda").manual_seed(5)
+        out, nc = [], []
+        for _ in range(40):
+            e.step(torch.rand((128, 17), device="cuda", generator=gen) * 2 - 1, want_contacts=True)
+            out.append(e.get_state()[0].clone())
+            nc.append(e.ncontact.clone())
+        return torch.stack(out).cpu().numpy(), torch.stack(nc).cpu().numpy()
+    a, ca = run()
+    b, cb = run(lds_rows=0)
+    assert ca.max() > 0
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def test_f64_gang_determinism_and_offset_invariance():
+    def run(n, off):
+        env = VecEnv("HumanoidPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True, precision=64)
+        assert env.info.lanes_per_env == 16
+        env.reset()
+        g = torch.Generator(device="cuda").manual_seed(0)
+        acts = torch.rand((30, 97, 17), device="cuda", generator=g) * 2 - 1
+        out = [env.step(acts[t][off:off + n].contiguous()).obs.clone() for t in range(30)]
+        return torch.stack(out).cpu().numpy(), env.get_state()[0].cpu().numpy()
+    a, sa = run(97, 0)
+    b, sb = run(97, 0)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(sa, sb)
+    c, sc = run(56, 41)
+    np.testing.assert_array_equal(a[:, 41:], c)
+    np.testing.assert_array_equal(sa[41:], sc)
