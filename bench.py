@@ -138,10 +138,11 @@ def cpu_baseline(seconds=12.0, single_core_seconds=3.0):
 PERF = os.path.join(REPO, "pybullet-gym_amd", "perf")
 
 
-def load_pmc(env_id, n):
-    """PMC summary of the step kernel (pybullet-gym_amd/perf/pmc_step_<robot>.json), if it was
-    taken at this env count."""
-    path = os.path.join(PERF, f"pmc_step_{SHORT.get(env_id, env_id)}.json")
+def load_pmc(env_id, n, precision=32):
+    """PMC summary of the step kernel (pybullet-gym_amd/perf/pmc_step_<robot>[_f64].json), if it
+    was taken at this env count."""
+    f64 = "_f64" if precision == 64 else ""
+    path = os.path.join(PERF, f"pmc_step_{SHORT.get(env_id, env_id)}{f64}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -305,7 +306,7 @@ def leg_summary(env, world, n, steps, elapsed, kernel_ms, flops):
     prec = getattr(env, "precision", 32)
     alg = alg_bytes_per_env_step(env.info, prec)
     achieved = alg * n / (kernel_ms * 1e-3) / 1e9
-    pmc = load_pmc(env.env_id, n) if prec == 32 else None
+    pmc = load_pmc(env.env_id, n, prec)
     d = {"env": env.env_id, "envs_per_gpu": n, "global_envs": world * n, "steps": steps,
          "dtype": "f64" if prec == 64 else "f32",
          "value": world * n * steps / elapsed, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,

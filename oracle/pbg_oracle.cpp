@@ -61,7 +61,7 @@ int g_flags = 0;
 enum { OPT_CONTACT_ERP, OPT_DEEP_ERP, OPT_DEEP_THR, OPT_DEEP_MODE, OPT_LIMIT_MODE, OPT_DAMP_MODE, OPT_FRIC_MODE,
        OPT_WARM, OPT_WARM_FRIC, OPT_LIMIT_ERP, OPT_ITERS, OPT_SEP_MODE, OPT_SLOP, OPT_SEP_ABS, OPT_LIM_SEP_ABS,
        OPT_SPRINGS, OPT_ROLL_MU, OPT_SPIN_MU, OPT_LIM_DEEP_MODE, OPT_LIMIT_CFM, OPT_CONTACT_CFM, OPT_CONTACT_THR,
-       OPT_MARGIN, OPT_SELF_COLLISION, OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_TORQUE_SUBSTEPS, OPT_COUNT };
+       OPT_MARGIN, OPT_SELF_COLLISION, OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_TORQUE_SUBSTEPS, OPT_MAX_COORD_VEL, OPT_COUNT };
 double g_opt[OPT_COUNT];
 const double g_opt_default[OPT_COUNT] = {
     -1.0,             // contact ERP of penetrating contact normal rows (-1: the model's, models_gen.h)
@@ -96,6 +96,7 @@ const double g_opt_default[OPT_COUNT] = {
     -1.0,             // sub-steps that carry apply_action's joint torques (-1: all of them; 1: the first
                       //   only -- Bullet clears a multibody's joint torques after each internal step
                       //   [EXT, rule study, SURVEY.md Appendix B1])
+    PBG_MAX_COORD_VELOCITY,  // btMultiBody m_maxCoordinateVelocity (rule study, round 5: the pendulums)
 };
 struct OptInit { OptInit() { for (int i = 0; i < OPT_COUNT; i++) g_opt[i] = g_opt_default[i]; } } g_opt_init;
 // persistent contact impulses per env and collision candidate (warm starting):
@@ -186,6 +187,13 @@ struct LinkDynOverride {
   MV orig;
 };
 LinkDynOverride g_dyn_ov[17];
+// joint damping replaced at run time (importer-rule study: MJCF <default> damping inheritance)
+struct DampOverride {
+  bool on = false;
+  double damping[MAXD];
+  const double* orig = nullptr;
+};
+DampOverride g_damp_ov[17];
 
 // ------------------------------------------------------------------ physics (pbg_physics.h)
 #include "pbg_physics.h"
@@ -381,6 +389,24 @@ int pbg_oracle_set_sim_params(const double* v) {
   const int ids[6] = {OPT_GRAVITY, OPT_DT, OPT_SUBSTEPS, OPT_ITERS, OPT_CONTACT_ERP, OPT_LIMIT_ERP};
   for (int i = 0; i < 6; i++) g_opt[ids[i]] = v ? v[i] : g_opt_default[ids[i]];
   return 0;
+}
+
+// Importer-rule study: joint dof damping [NJ] of robot (NULL restores the compiled table).  Never
+// used by a product-parity comparison.
+int pbg_oracle_set_dof_damping(int robot, const double* damping) {
+  if (robot < 0 || robot > 16) return -1;
+  MV& v = model_views()[robot];
+  DampOverride& o = g_damp_ov[robot];
+  if (!o.on) o.orig = v.damping;
+  if (!damping) {
+    v.damping = o.orig;
+    o.on = false;
+    return v.NJ;
+  }
+  for (int d = 0; d < v.NJ; d++) o.damping[d] = damping[d];
+  o.on = true;
+  v.damping = o.damping;
+  return v.NJ;
 }
 
 // Physics-rule variants (see OPT_*): v[i] for i < n replaces option i; n = 0 restores the defaults.

@@ -625,7 +625,7 @@ template <class T> inline uint32_t solve_row(int n, RowT<T>& r, T* nu) {
 }
 
 template <class T> inline T clampv(T v) {
-  const T mx(PBG_MAX_COORD_VELOCITY);
+  const T mx(g_opt[OPT_MAX_COORD_VEL]);  // PBG_MAX_COORD_VELOCITY unless the rule study changes it
   return v > mx ? mx : (v < T(0) - mx ? T(0) - mx : v);
 }
 

@@ -297,6 +297,11 @@ def _floats(s: Optional[str], n: Optional[int] = None) -> Optional[np.ndarray]:
     return v
 
 
+# Rule-study switch (tools/physics_rules.py, round 5): joint damping inherited from <default>.  The
+# product tables (codegen.py) are compiled with it off (B6).
+INHERIT_DEFAULT_DAMPING = False
+
+
 class _Ctx:
     def __init__(self, root: ET.Element):
         comp = root.find("compiler")
@@ -429,7 +434,9 @@ def compile_mjcf(path: str, robot_name: str) -> RobotModel:
             limited = False
         return dict(jtype=jtype, axis=axis, anchor=anchor, lower=lo if limited else 0.0,
                     upper=hi if limited else -1.0, limited=limited,
-                    damping=float(j.get("damping", "0")),  # B6: the joint's own attribute only
+                    # B6: the joint's own attribute only (INHERIT_DEFAULT_DAMPING: the rule study's
+                    # alternative, <default> inherited; tools/physics_rules.py, never the product tables)
+                    damping=float((ctx.jattr(j, "damping", "0") if INHERIT_DEFAULT_DAMPING else j.get("damping", "0"))),
                     stiffness=float(j.get("stiffness", "0")),  # B7: likewise
                     armature=0.0,  # B3: btMultiBody has no armature
                     joint_name=j.get("name"))

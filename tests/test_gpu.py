@@ -620,7 +620,8 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
             print(f"  free_running[{env_id}]: step {t}/{steps} {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
         res = env.step(acts[t], want_contacts=True)
         og = res.obs.index_select(0, tidx).cpu().numpy()
-        dg = res.done.index_select(0, tidx).cpu().numpy().astype(bool)
+        # termination (the oracle has no TimeLimit: the GPU's truncation at step 1,000 is not a done)
+        dg = (res.done.bool() & ~res.truncated.bool()).index_select(0, tidx).cpu().numpy()
         cg = env.ncontact.index_select(0, tidx).cpu().numpy()
         a = acts[t].index_select(0, tidx).cpu().numpy()
         o64, _, d64, c64 = orcs["f64"].step(a)

@@ -29,11 +29,12 @@ import policies  # noqa: E402
 KEYS = ["contact_erp", "deep_erp", "deep_thr", "deep_mode", "limit_mode", "damp_mode", "fric_mode", "warm",
         "warm_fric", "limit_erp", "iters", "sep_mode", "slop", "sep_abs", "lim_sep_abs",
         "springs", "roll_mu", "spin_mu", "lim_deep_mode", "limit_cfm", "contact_cfm", "contact_thr", "margin",
-        "self_collision", "gravity", "dt", "substeps", "torque_substeps"]
+        "self_collision", "gravity", "dt", "substeps", "torque_substeps", "max_coord_vel"]
 DEFAULT = [-1.0, -1.0, -0.04, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.2, 5.0, 0.0, 0.0, 1.0, 1.0,
-           1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.02, 0.0, 1.0, 9.8, -1.0, -1.0, -1.0]
-# importer switches (not oracle options): recompiled link dynamics
-IMPORTER_KEYS = ("inertia_margin", "mass_first", "capsule_margin")
+           1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.02, 0.0, 1.0, 9.8, -1.0, -1.0, -1.0, 100.0]
+# importer switches (not oracle options): recompiled link dynamics; joint damping with the MJCF
+# <default> inherited (round 5)
+IMPORTER_KEYS = ("inertia_margin", "mass_first", "capsule_margin", "default_damping")
 VARIANTS = {
     "current": {},
     "erp0.9": {"contact_erp": 0.9},
@@ -83,7 +84,14 @@ VARIANTS = {
     "torque_first+mass_first": {"torque_substeps": 1.0, "mass_first": 1.0},
     "margin0.04+mass_first": {"inertia_margin": 0.04, "mass_first": 1.0},
     "torque_first+margin0.04+mass_first": {"torque_substeps": 1.0, "inertia_margin": 0.04, "mass_first": 1.0},
+    # round 5: contact-free rules scored on the pendulum family first
+    "default_damping": {"default_damping": 1.0},
+    "max_coord_vel1000": {"max_coord_vel": 1000.0},
+    "max_coord_vel10": {"max_coord_vel": 10.0},
+    "margin0.04+default_damping": {"inertia_margin": 0.04, "default_damping": 1.0},
 }
+PENDULUMS = ["InvertedPendulumPyBulletEnv-v0", "InvertedPendulumSwingupPyBulletEnv-v0",
+             "InvertedDoublePendulumPyBulletEnv-v0"]
 ENVS = ["HopperPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "AntPyBulletEnv-v0",
         "HumanoidPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "InvertedDoublePendulumPyBulletEnv-v0",
         "HumanoidFlagrunHarderPyBulletEnv-v0", "AtlasPyBulletEnv-v0"]
@@ -91,6 +99,7 @@ SHORT = {"HopperPyBulletEnv-v0": "Hopper", "Walker2DPyBulletEnv-v0": "Walker", "
          "AntPyBulletEnv-v0": "Ant", "HumanoidPyBulletEnv-v0": "Humanoid", "HumanoidFlagrunPyBulletEnv-v0": "Flagrun",
          "InvertedDoublePendulumPyBulletEnv-v0": "DblPend", "HumanoidFlagrunHarderPyBulletEnv-v0": "Harder",
          "AtlasPyBulletEnv-v0": "Atlas"}
+SHORT.update({"InvertedPendulumPyBulletEnv-v0": "Pendulum", "InvertedPendulumSwingupPyBulletEnv-v0": "Swingup"})
 
 
 def set_physics(over):
@@ -105,14 +114,14 @@ def set_physics(over):
     L.pbg_oracle_set_physics(arr.ctypes.data_as(ctypes.c_void_p), len(v))
 
 
-def importer_tables(env_id, margin=0.0, mass_first=False, capsule_margin=0.0):
+def importer_tables(env_id, margin=0.0, mass_first=False, capsule_margin=0.0, default_damping=False):
     """The robot's compiled tables under the importer variant (mjcf.py B2/B3, urdf.py U3).
     margin: the compound AABB grown by `margin` per side; capsule_margin: each capsule's AABB grown
     by capsule_margin x its radius per side before the union (a btCapsuleShape's collision margin is
     its radius; whether its getAabb adds the margin on top of the radius is the question)."""
     from pybulletgym_amd import codegen, mjcf, robots, urdf
     spec = next(s for s in robots.SPECS.values() if s.env_id == env_id)
-    saved = (mjcf.bullet_compound_inertia, urdf.aabb_inertia, mjcf.collision_aabb)
+    saved = (mjcf.bullet_compound_inertia, urdf.aabb_inertia, mjcf.collision_aabb, mjcf.INHERIT_DEFAULT_DAMPING)
     orig_aabb = mjcf.collision_aabb
 
     def capsule_aabb(geoms):
@@ -134,6 +143,7 @@ def importer_tables(env_id, margin=0.0, mass_first=False, capsule_margin=0.0):
                             mass / 12.0 * (l[0] ** 2 + l[1] ** 2)])
         return inertia
     try:
+        mjcf.INHERIT_DEFAULT_DAMPING = bool(default_damping)
         if capsule_margin:
             mjcf.collision_aabb = capsule_aabb
         if margin or capsule_margin:
@@ -141,7 +151,7 @@ def importer_tables(env_id, margin=0.0, mass_first=False, capsule_margin=0.0):
             urdf.aabb_inertia = grown(urdf.geom_aabb)
         model = robots.compile_model(spec)
     finally:
-        mjcf.bullet_compound_inertia, urdf.aabb_inertia, mjcf.collision_aabb = saved
+        mjcf.bullet_compound_inertia, urdf.aabb_inertia, mjcf.collision_aabb, mjcf.INHERIT_DEFAULT_DAMPING = saved
     if mass_first:
         # links of one MJCF body: its dummies then the real link (mjcf.py add_body), same frame
         by_body = {}
@@ -163,10 +173,15 @@ def set_importer(env_id, over):
     rid = oracle.robot_id(env_id)
     margin, mass_first = float(over.get("inertia_margin", 0.0)), bool(over.get("mass_first", 0.0))
     cmargin = float(over.get("capsule_margin", 0.0))
-    if not margin and not mass_first and not cmargin:
+    ddamp = bool(over.get("default_damping", 0.0))
+    L.pbg_oracle_set_dof_damping.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    if not margin and not mass_first and not cmargin and not ddamp:
         L.pbg_oracle_set_link_dynamics(rid, None, None, None, 0.0, None)
+        L.pbg_oracle_set_dof_damping(rid, None)
         return
-    t = importer_tables(env_id, margin, mass_first, cmargin)
+    t = importer_tables(env_id, margin, mass_first, cmargin, ddamp)
+    damp = np.ascontiguousarray(t["dof_damping"], dtype=np.float64)
+    L.pbg_oracle_set_dof_damping(rid, damp.ctypes.data)
     p = lambda a: np.ascontiguousarray(a, dtype=np.float64)
     mass, com, inertia, bi = p(t["link_mass"]), p(t["link_com"]), p(t["link_inertia"]), p(t["base_inertia"])
     _keep = (mass, com, inertia, bi)
@@ -203,6 +218,8 @@ def parse(spec):
 if __name__ == "__main__":
     specs = sys.argv[1:] or list(VARIANTS)
     envs = os.environ.get("PBG_RULE_ENVS", "").split(",") if os.environ.get("PBG_RULE_ENVS") else ENVS
+    if envs == ["pendulums"]:
+        envs = PENDULUMS
     print(f"{'variant':38s}" + "".join(f"{SHORT[e]:>16s}" for e in envs), flush=True)
     for sp in specs:
         name, over = parse(sp)

@@ -19,13 +19,16 @@ src, rnd, robot, envs = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(REPO, "profiles")
 tag = f"{robot}{envs // 1024}k"
+F64 = robot.endswith("_f64")  # the float64 (reference-precision) handle's kernel, F64<R>
 STRUCT = {"ant": "Ant", "humanoid": "Humanoid", "hopper": "Hopper", "halfcheetah": "HalfCheetah",
-          "walker2d": "Walker2D", "pendulum": "Pendulum"}[robot]
-KEY = f"pbg_models::{STRUCT}"
+          "walker2d": "Walker2D", "pendulum": "Pendulum"}[robot[:-4] if F64 else robot]
+KEY = f"pbg::F64<pbg_models::{STRUCT}>" if F64 else f"pbg_models::{STRUCT}"
 
 
 def is_step(name):
-    return "step_kernel" in name and KEY in name
+    if "step_kernel" not in name or KEY not in name:
+        return False
+    return F64 or "F64<" not in name
 
 
 def counter_csv(d):
@@ -45,7 +48,7 @@ def medians(path):
 
 
 out = {"kernel": "pbg::*step_kernel<" + KEY + ">", "robot": robot, "envs": envs, "round": rnd}
-for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops"):
+for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops", "pmc_flops64"):
     p = counter_csv(os.path.join(robot, d))
     if not p:
         continue
@@ -73,6 +76,10 @@ if "SQ_INSTS_VALU_FMA_F32_median" in out:
     out["fp32_flops_per_launch_from_insts"] = 64 * (
         2 * out["SQ_INSTS_VALU_FMA_F32_median"] + out.get("SQ_INSTS_VALU_ADD_F32_median", 0)
         + out.get("SQ_INSTS_VALU_MUL_F32_median", 0) + out.get("SQ_INSTS_VALU_TRANS_F32_median", 0))
+if "SQ_INSTS_VALU_FMA_F64_median" in out:
+    out["fp64_flops_per_launch_from_insts"] = 64 * (
+        2 * out["SQ_INSTS_VALU_FMA_F64_median"] + out.get("SQ_INSTS_VALU_ADD_F64_median", 0)
+        + out.get("SQ_INSTS_VALU_MUL_F64_median", 0) + out.get("SQ_INSTS_VALU_TRANS_F64_median", 0))
 out["source"] = ("rocprofv3 --kernel-trace --stats; separate --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_* | "
                  "SQ_INSTS_VALU_* (tools/gpu_bench_prof.sh), python bench.py --steps 20 --warmup 2")
 # the round-named record under profiles/ (judged) and the copy bench.py ships and reads
