@@ -27,6 +27,8 @@ for W in ${PROF_ROBOTS:-ant humanoid hopper halfcheetah ant_f64 humanoid_f64}; d
   timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$W/pmc_write -o run -- $B > $OUT/$W.pmc_write.log 2>&1
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/$W/pmc_sq -o run -- $B > $OUT/$W.pmc_sq.log 2>&1
   timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 --output-format csv -d $OUT/$W/pmc_flops -o run -- $B > $OUT/$W.pmc_flops.log 2>&1
+  # L2 hit / miss and L1->L2 reads (is the gang kernels' read excess the tables?)
+  timeout -k 10 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum --output-format csv -d $OUT/$W/pmc_l2 -o run -- $B > $OUT/$W.pmc_l2.log 2>&1
   case $W in *_f64) timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP64 --output-format csv -d $OUT/$W/pmc_flops64 -o run -- $B > $OUT/$W.pmc_flops64.log 2>&1;; esac
 done
 echo done

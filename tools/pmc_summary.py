@@ -48,7 +48,7 @@ def medians(path):
 
 
 out = {"kernel": "pbg::*step_kernel<" + KEY + ">", "robot": robot, "envs": envs, "round": rnd}
-for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops", "pmc_flops64"):
+for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_flops", "pmc_flops64", "pmc_l2"):
     p = counter_csv(os.path.join(robot, d))
     if not p:
         continue
@@ -70,6 +70,8 @@ if "FETCH_SIZE_median" in out and "WRITE_SIZE_median" in out:
     out["correction"] = (f"FETCH_SIZE x{cal['fetch_factor']}, WRITE_SIZE x{cal['write_dword_factor']}, measured for "
                          "4 B/lane SoA dword loads/stores by tools/fetch_calib.hip (profiles/fetch_calibration.json); "
                          "kB = 1024 B")
+if "TCC_HIT_sum_median" in out and "TCC_MISS_sum_median" in out:
+    out["l2_hit_rate"] = out["TCC_HIT_sum_median"] / max(1.0, out["TCC_HIT_sum_median"] + out["TCC_MISS_sum_median"])
 if "SQ_INSTS_VALU_median" in out:
     out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_median"]
 if "SQ_INSTS_VALU_FMA_F32_median" in out:
@@ -81,7 +83,7 @@ if "SQ_INSTS_VALU_FMA_F64_median" in out:
         2 * out["SQ_INSTS_VALU_FMA_F64_median"] + out.get("SQ_INSTS_VALU_ADD_F64_median", 0)
         + out.get("SQ_INSTS_VALU_MUL_F64_median", 0) + out.get("SQ_INSTS_VALU_TRANS_F64_median", 0))
 out["source"] = ("rocprofv3 --kernel-trace --stats; separate --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_* | "
-                 "SQ_INSTS_VALU_* (tools/gpu_bench_prof.sh), python bench.py --steps 20 --warmup 2")
+                 "SQ_INSTS_VALU_* | TCC_HIT/MISS (tools/gpu_bench_prof.sh), python bench.py --steps 20 --warmup 2")
 # the round-named record under profiles/ (judged) and the copy bench.py ships and reads
 for path in (os.path.join(prof, f"{rnd}_pmc_step_{robot}.json"),
              os.path.join(REPO, "pybullet-gym_amd", "perf", f"pmc_step_{robot}.json")):
