@@ -16,6 +16,7 @@
 
 namespace pbg {
 using R = pbg_models::PBG_ROBOT;
+using R64 = F64<R>;
 
 static inline unsigned blocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
 
@@ -40,10 +41,11 @@ static int plan_team(int n_envs, int cus, Geometry* g) {
   if constexpr (Team<RR>::ok) {
     using RW = TRows<RR, 16>;
     constexpr int ES = 16;
+    constexpr size_t WB = sizeof(real_t<RR>);  // row word: float, or double on the float64 path
     const int wgs = (n_envs + ES - 1) / ES;
     const int wpc = (wgs + cus - 1) / cus;
     const size_t budget = (size_t)163840 / (size_t)(wpc > 0 ? wpc : 1);
-    long words = (long)(budget / ((size_t)ES * sizeof(float))) - RW::HEAD;
+    long words = (long)(budget / ((size_t)ES * WB)) - RW::HEAD;
     int cap = (int)(words / RW::W);
     if (cap > RW::MR) cap = RW::MR;
     if (cap < 0) cap = 0;
@@ -53,8 +55,9 @@ static int plan_team(int n_envs, int cus, Geometry* g) {
     g->env_words = 0;
     g->block = 64;
     g->lds_rows = cap;
-    g->lds_bytes = (size_t)ES * sizeof(float) * per_env;
+    g->lds_bytes = (size_t)ES * WB * per_env;
     g->scratch_words_per_env = RW::WORDS;
+    g->word_bytes = (int)WB;
     const void* fn = (const void*)team_step_kernel<RR, 16>;
     const int e = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes);
     return e ? e : kernel_attrs(fn, g);
@@ -228,6 +231,29 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
   }
 }
 
+// ---- the float64 quad kernel (Team<R64>::ok: Ant, AntMuJoCo) is its own translation unit, compiled
+// with -DPBG_TEAM64_TU and the AMDGPU register-pressure trackers in the machine scheduler
+// (Makefile): with the default scheduler this ROCm's backend miscompiles it -- NaN velocities
+// from the first sub-step in every env, while the LLVM IR is free of undef / poison, the same
+// source with printf calls or the trackers schedule is bit-exact against the float64 lane kernel,
+// and moving the double quad permutes from DPP to ds_bpermute does not change it (DESIGN.md
+// section 4).  The float32 kernels keep the default scheduler (their ISA is unchanged).  AntMuJoCo's
+// instance is wrong under both schedules and is not built: its float64 handle runs the gang kernel.
+template <class RR>
+constexpr bool team64_ok() { return Team<RR>::ok && RR::kind == 0; }
+int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g);
+bool PBG_FN(launch_team64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s);
+#ifdef PBG_TEAM64_TU
+int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g) {
+  if constexpr (team64_ok<R64>()) return plan_team<R64>(n_envs, cus, g);
+  else { (void)n_envs; (void)cus; (void)g; return (int)hipErrorInvalidValue; }
+}
+bool PBG_FN(launch_team64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if constexpr (team64_ok<R64>()) return launch_team<R64>(B, io, scratch, g, s);
+  else { (void)B; (void)io; (void)scratch; (void)g; (void)s; return false; }
+}
+#else
+
 // mode: 0 = lane kernel; 1 = default (quad for Ant, gang for the other walkers -- HumanoidFlagrunHarder
 // and Atlas included: the cube robot runs the gang kernel's front path, distributed dynamics only);
 // 2 = gang for every walker (parity tests of the gang kernel on Ant).
@@ -266,17 +292,18 @@ int PBG_FN(launch_pack_)(int n, const double* in, double* out, hipStream_t s) {
 // ---- the reference-precision path (pbg_create_v2 precision 64): float64 physics state and
 // arithmetic (pybullet's btScalar, scene_bases.py:75-76) for every robot with at most 128
 // floor-contact slots (Atlas: PBG_E_HIP at create).  mode 0: the lane-per-env
-// kernel (the float64 gang kernel's parity cross-check); otherwise the 16-lane gang kernel for the
-// walkers (Ant included: the quad kernel has no float64 variant) and the lane kernel for the
-// pendulums.
-using R64 = F64<R>;
+// kernel (the float64 gang and quad kernels' parity cross-check); 1 (default): the quad kernel for Ant
+// (team64_ok), the 16-lane gang kernel for the other walkers and the lane kernel for the pendulums;
+// 2: the gang kernel for every walker (Ant included).
 int PBG_FN(plan64_)(int n_envs, int cus, int mode, Geometry* g) {
+  if (team64_ok<R64>() && mode == 1) return PBG_FN(plan_team64_)(n_envs, cus, g);
   if constexpr (gang_ok<R64, 16>()) {
     if (mode != 0) return plan_gang_t<R64, 16>(n_envs, cus, g);
   }
   return plan_lane<R64>(n_envs, cus, g);
 }
 int PBG_FN(launch_step64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
+  if (PBG_FN(launch_team64_)(B, io, scratch, g, s)) return (int)hipGetLastError();
   if (g.team == 16 && launch_gang_t<R64, 16>(B, io, scratch, g, s)) return (int)hipGetLastError();
   return launch_lane<R64>(B, io, scratch, g, s);
 }
@@ -304,4 +331,5 @@ int PBG_FN(debug_stamps_)(unsigned long long* host_out) {
   return -1;
 #endif
 }
+#endif  // PBG_TEAM64_TU
 }  // namespace pbg

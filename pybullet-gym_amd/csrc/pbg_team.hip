@@ -46,6 +46,20 @@ template <int K>
 PBG_DEV float quad_bcast(float x) { return qperm<K | (K << 2) | (K << 4) | (K << 6)>(x); }
 template <int K>
 PBG_DEV int quad_bcast_i(int x) { return qperm_i<K | (K << 2) | (K << 4) | (K << 6)>(x); }
+// float64 (F64<R>: the reference-precision path): a double moves as its two dwords
+template <int CTRL>
+PBG_DEV double qperm(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+PBG_DEV double quad_sum(double x) {
+  x = x + qperm<0xB1>(x);
+  return x + qperm<0x4E>(x);
+}
+template <int K>
+PBG_DEV double quad_bcast(double x) { return qperm<K | (K << 2) | (K << 4) | (K << 6)>(x); }
 // LDS written by one lane and read by another lane of the same wave: a compiler fence
 // (the wave's LDS operations execute in order).
 #define PBG_QUAD_SYNC                                    \
@@ -56,9 +70,9 @@ PBG_DEV int quad_bcast_i(int x) { return qperm_i<K | (K << 2) | (K << 4) | (K <<
   }
 
 // ------------------------------------------------------------------ branch decomposition
-template <int N>
+template <int N, class S = float>
 struct BTab {  // per-branch constant: v[entry][branch]
-  float v[N > 0 ? N : 1][4];
+  S v[N > 0 ? N : 1][4];
 };
 template <int N>
 struct BTabI {
@@ -67,6 +81,7 @@ struct BTabI {
 
 template <class R>
 struct Team {
+  using Sc = real_t<R>;
   static constexpr int NL = R::NL, NJ = R::NJ;
   static constexpr int roots() {
     int c = 0;
@@ -137,15 +152,15 @@ struct Team {
   }
 
   // per-branch constants
-  static constexpr BTab<NLB * 3> vec3(const double (*t)[3]) {
-    BTab<NLB * 3> r{};
+  static constexpr BTab<NLB * 3, Sc> vec3(const double (*t)[3]) {
+    BTab<NLB * 3, Sc> r{};
     for (int i = 0; i < NLB; i++)
       for (int c = 0; c < 3; c++)
-        for (int k = 0; k < B; k++) r.v[i * 3 + c][k] = (float)t[k * NLB + i][c];
+        for (int k = 0; k < B; k++) r.v[i * 3 + c][k] = (Sc)t[k * NLB + i][c];
     return r;
   }
-  static constexpr BTab<NLB * 9> make_rot() {
-    BTab<NLB * 9> r{};
+  static constexpr BTab<NLB * 9, Sc> make_rot() {
+    BTab<NLB * 9, Sc> r{};
     for (int i = 0; i < NLB; i++)
       for (int k = 0; k < B; k++) {
         const double* q = R::link_offset_quat[k * NLB + i];
@@ -153,32 +168,32 @@ struct Team {
         const double m[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
                              2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
                              2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
-        for (int c = 0; c < 9; c++) r.v[i * 9 + c][k] = (float)m[c];
+        for (int c = 0; c < 9; c++) r.v[i * 9 + c][k] = (Sc)m[c];
       }
     return r;
   }
-  static constexpr BTab<NLB> make_mass() {
-    BTab<NLB> r{};
+  static constexpr BTab<NLB, Sc> make_mass() {
+    BTab<NLB, Sc> r{};
     for (int i = 0; i < NLB; i++)
-      for (int k = 0; k < B; k++) r.v[i][k] = (float)R::link_mass[k * NLB + i];
+      for (int k = 0; k < B; k++) r.v[i][k] = (Sc)R::link_mass[k * NLB + i];
     return r;
   }
-  static constexpr BTab<NLB * 6> make_iner() {
-    BTab<NLB * 6> r{};
+  static constexpr BTab<NLB * 6, Sc> make_iner() {
+    BTab<NLB * 6, Sc> r{};
     for (int i = 0; i < NLB; i++)
       for (int c = 0; c < 6; c++)
-        for (int k = 0; k < B; k++) r.v[i * 6 + c][k] = (float)R::link_inertia[k * NLB + i][c];
+        for (int k = 0; k < B; k++) r.v[i * 6 + c][k] = (Sc)R::link_inertia[k * NLB + i][c];
     return r;
   }
-  static constexpr BTab<NDB> dofs(const double* t) {
-    BTab<NDB> r{};
+  static constexpr BTab<NDB, Sc> dofs(const double* t) {
+    BTab<NDB, Sc> r{};
     for (int j = 0; j < NDB; j++)
-      for (int k = 0; k < B; k++) r.v[j][k] = (float)t[k * NDB + j];
+      for (int k = 0; k < B; k++) r.v[j][k] = (Sc)t[k * NDB + j];
     return r;
   }
-  static constexpr BTab<NDB> make_gain() {  // tau = gain * clip(a) of the actuator driving the dof
-    BTab<NDB> r{};
-    for (int i = 0; i < R::NA; i++) r.v[R::act_dof[i] % NDB][R::act_dof[i] / NDB] = (float)R::act_gain[i];
+  static constexpr BTab<NDB, Sc> make_gain() {  // tau = gain * clip(a) of the actuator driving the dof
+    BTab<NDB, Sc> r{};
+    for (int i = 0; i < R::NA; i++) r.v[R::act_dof[i] % NDB][R::act_dof[i] / NDB] = (Sc)R::act_gain[i];
     return r;
   }
   static constexpr BTabI<NDB> make_acti() {
@@ -202,38 +217,38 @@ struct Team {
     for (int f = 0; f < R::NF; f++) r.v[R::foot_link[f] % NLB][R::foot_link[f] / NLB] = f;
     return r;
   }
-  static constexpr BTab<NSB * 3> make_spt() {
-    BTab<NSB * 3> r{};
+  static constexpr BTab<NSB * 3, Sc> make_spt() {
+    BTab<NSB * 3, Sc> r{};
     for (int s = 0; s < NSB; s++)
       for (int c = 0; c < 3; c++)
-        for (int k = 0; k < B; k++) r.v[s * 3 + c][k] = (float)R::slot_point[NS0 + k * NSB + s][c];
+        for (int k = 0; k < B; k++) r.v[s * 3 + c][k] = (Sc)R::slot_point[NS0 + k * NSB + s][c];
     return r;
   }
-  static constexpr BTab<NSB> slots(const double* t) {
-    BTab<NSB> r{};
+  static constexpr BTab<NSB, Sc> slots(const double* t) {
+    BTab<NSB, Sc> r{};
     for (int s = 0; s < NSB; s++)
-      for (int k = 0; k < B; k++) r.v[s][k] = (float)t[NS0 + k * NSB + s];
+      for (int k = 0; k < B; k++) r.v[s][k] = (Sc)t[NS0 + k * NSB + s];
     return r;
   }
-  static constexpr BTab<NLB * 3> OFFP = vec3(R::link_offset_pos);
-  static constexpr BTab<NLB * 3> AXIS = vec3(R::link_axis);
-  static constexpr BTab<NLB * 3> ANCH = vec3(R::link_anchor);
-  static constexpr BTab<NLB * 3> COM = vec3(R::link_com);
-  static constexpr BTab<NLB * 9> ROT = make_rot();
-  static constexpr BTab<NLB> MASS = make_mass();
-  static constexpr BTab<NLB * 6> INER = make_iner();
-  static constexpr BTab<NDB> DLO = dofs(R::dof_lower);
-  static constexpr BTab<NDB> DHI = dofs(R::dof_upper);
-  static constexpr BTab<NDB> DAMP = dofs(R::dof_damping);
-  static constexpr BTab<NDB> STIFF = dofs(R::dof_stiffness);
-  static constexpr BTab<NDB> ARM = dofs(R::dof_armature);
-  static constexpr BTab<NDB> GAIN = make_gain();
+  static constexpr BTab<NLB * 3, Sc> OFFP = vec3(R::link_offset_pos);
+  static constexpr BTab<NLB * 3, Sc> AXIS = vec3(R::link_axis);
+  static constexpr BTab<NLB * 3, Sc> ANCH = vec3(R::link_anchor);
+  static constexpr BTab<NLB * 3, Sc> COM = vec3(R::link_com);
+  static constexpr BTab<NLB * 9, Sc> ROT = make_rot();
+  static constexpr BTab<NLB, Sc> MASS = make_mass();
+  static constexpr BTab<NLB * 6, Sc> INER = make_iner();
+  static constexpr BTab<NDB, Sc> DLO = dofs(R::dof_lower);
+  static constexpr BTab<NDB, Sc> DHI = dofs(R::dof_upper);
+  static constexpr BTab<NDB, Sc> DAMP = dofs(R::dof_damping);
+  static constexpr BTab<NDB, Sc> STIFF = dofs(R::dof_stiffness);
+  static constexpr BTab<NDB, Sc> ARM = dofs(R::dof_armature);
+  static constexpr BTab<NDB, Sc> GAIN = make_gain();
   static constexpr BTabI<NDB> ACTI = make_acti();
   static constexpr BTabI<NDB> RST = make_rst();
   static constexpr BTabI<NLB> FOOT = make_foot();
-  static constexpr BTab<NSB * 3> SPT = make_spt();
-  static constexpr BTab<NSB> SRAD = slots(R::slot_radius);
-  static constexpr BTab<NSB> SMU = slots(R::slot_mu);
+  static constexpr BTab<NSB * 3, Sc> SPT = make_spt();
+  static constexpr BTab<NSB, Sc> SRAD = slots(R::slot_radius);
+  static constexpr BTab<NSB, Sc> SMU = slots(R::slot_mu);
 };
 
 // The lane's branch and its one-hot weights, for picking per-branch constants.
@@ -253,13 +268,14 @@ PBG_DEV Lane make_lane(int k) {
 }
 // per-branch constant of entry I of table T for this lane (a constant when all branches agree)
 template <const auto& T, int I>
-PBG_DEV float pk(const Lane& L) {
-  constexpr float a0 = T.v[I][0], a1 = T.v[I][1], a2 = T.v[I][2], a3 = T.v[I][3];
+PBG_DEV auto pk(const Lane& L) {
+  using S = std::remove_cv_t<std::remove_reference_t<decltype(T.v[0][0])>>;
+  constexpr S a0 = T.v[I][0], a1 = T.v[I][1], a2 = T.v[I][2], a3 = T.v[I][3];
   if constexpr (a0 == a1 && a0 == a2 && a0 == a3) return a0;
   else if constexpr (a0 == a2 && a1 == a3) return L.odd ? a1 : a0;
   else if constexpr (a0 == a1 && a2 == a3) return L.hi ? a2 : a0;
   else if constexpr (a0 == a3 && a1 == a2) return L.mid ? a1 : a0;
-  else return a0 * L.e0 + a1 * L.e1 + a2 * L.e2 + a3 * L.e3;
+  else return a0 * (S)L.e0 + a1 * (S)L.e1 + a2 * (S)L.e2 + a3 * (S)L.e3;
 }
 template <const auto& T, int I>
 PBG_DEV int pki(const Lane& L) {
@@ -268,20 +284,24 @@ PBG_DEV int pki(const Lane& L) {
   else return L.k == 0 ? a0 : (L.k == 1 ? a1 : (L.k == 2 ? a2 : a3));
 }
 template <const auto& T, int I>
-PBG_DEV f3 pk3(const Lane& L) {
-  return mk3(pk<T, 3 * I>(L), pk<T, 3 * I + 1>(L), pk<T, 3 * I + 2>(L));
+PBG_DEV auto pk3(const Lane& L) {
+  return mk3<decltype(pk<T, 3 * I>(L))>(pk<T, 3 * I>(L), pk<T, 3 * I + 1>(L), pk<T, 3 * I + 2>(L));
 }
 
 // ------------------------------------------------------------------ per-lane state
 template <class R>
 struct TState {
+  using Sc = real_t<R>;
   static constexpr int NDB = Team<R>::NDB;
-  float bp[3], bq[4], bv[3], bw[3];  // replicated
-  float q[NDB], qd[NDB];             // this lane's branch dofs (local order)
+  Sc bp[3], bq[4], bv[3], bw[3];  // replicated
+  Sc q[NDB], qd[NDB];             // this lane's branch dofs (local order)
 };
 
 template <class R>
 struct TKin {  // this lane's branch links
+  using Sc = real_t<R>;
+  using f3 = V3<Sc>;
+  using m3 = M3<Sc>;
   static constexpr int NLB = Team<R>::NLB;
   m3 Rm[NLB];
   f3 x[NLB], c[NLB];
@@ -289,9 +309,13 @@ struct TKin {  // this lane's branch links
 
 // branch forward kinematics (positions); joint axes / anchors of the branch dofs on request
 template <class R, bool AXES = false>
-PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k, f3* ja = nullptr, f3* jo = nullptr) {
+PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const M3<real_t<R>>& Rb, TKin<R>& k, V3<real_t<R>>* ja = nullptr,
+                     V3<real_t<R>>* jo = nullptr) {
+  using Sc = real_t<R>;
+  using f3 = V3<Sc>;
+  using m3 = M3<Sc>;
   using T = Team<R>;
-  const f3 xb = mk3(s.bp[0], s.bp[1], s.bp[2]);
+  const f3 xb = mk3<Sc>(s.bp[0], s.bp[1], s.bp[2]);
   static_for<0, T::NLB>([&](auto i_c) {
     constexpr int i = decltype(i_c)::value;
     constexpr int p = R::link_parent[i], jt = R::link_jtype[i], d = R::link_dof[i];
@@ -339,6 +363,8 @@ PBG_DEV void team_fk(const TState<R>& s, const Lane& L, const m3& Rb, TKin<R>& k
 template <class R, int ES>
 struct TRows {
   using T = Team<R>;
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   static constexpr int NDB = T::NDB, NC = T::NC, MR = 3 * T::NC, ES_ = ES;
   static constexpr int PW = NDB + 2;    // per-lane words of a row
   static constexpr int W = 4 * PW + 4;  // words per env per row (P of its 4 lanes + S)
@@ -346,76 +372,76 @@ struct TRows {
   static constexpr int HEAD = 0;        // per-env words before the rows (pack staging overlaps the rows)
   static_assert(NC <= 32, "contact_sweep keeps one bit per contact in a 32-bit mask");
   static constexpr int WORDS = MR * W;  // device workspace words per env
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  typedef float v2f __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(3))) v4f lds_float4;
-  typedef __attribute__((address_space(3))) v2f lds_float2;
-  lds_float* lds;   // LDS base + env slot (pack staging, [word][env])
-  lds_float* rows;  // LDS base of the wave's row regions
-  float* gbl;       // workspace base + env
+  typedef Sc v4f __attribute__((ext_vector_type(4)));
+  typedef Sc v2f __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v4f LW4;
+  typedef __attribute__((address_space(3))) v2f LW2;
+  LW* lds;   // LDS base + env slot (pack staging, [word][env])
+  LW* rows;  // LDS base of the wave's row regions
+  Sc* gbl;       // workspace base + env
   int n;
   int cap;          // rows resident in LDS
   int lane;         // lane in the wave (4 e + k)
-  PBG_DEV lds_float& stage(int w) const { return lds[(size_t)w * ES]; }
+  PBG_DEV LW& stage(int w) const { return lds[(size_t)w * ES]; }
   // row offsets by a 24-bit multiply (rows < 2^24): the 32-bit v_mul_lo_u32 the compiler chose for
   // an unbounded row index is a quarter-rate instruction, two of them per normal row of the sweep
   PBG_DEV int roff(int r) const { return (int)__umul24((unsigned)r, (unsigned)(ES * W)); }
-  PBG_DEV lds_float* P(int r) const { return rows + roff(r) + PW * lane; }
-  PBG_DEV lds_float* S(int r) const { return rows + roff(r) + SOFF + 4 * (lane >> 2); }
+  PBG_DEV LW* P(int r) const { return rows + roff(r) + PW * lane; }
+  PBG_DEV LW* S(int r) const { return rows + roff(r) + SOFF + 4 * (lane >> 2); }
   // row words of lane k in the workspace ([word][env], stride n)
-  PBG_DEV float* gP(int r, int k) const { return gbl + ((size_t)r * W + (size_t)k * PW) * n; }
-  PBG_DEV float* gS(int r) const { return gbl + ((size_t)r * W + 4 * PW) * n; }
+  PBG_DEV Sc* gP(int r, int k) const { return gbl + ((size_t)r * W + (size_t)k * PW) * n; }
+  PBG_DEV Sc* gS(int r) const { return gbl + ((size_t)r * W + 4 * PW) * n; }
   // slot: the writing lane's branch for a branch contact (the owner writes all four lanes'
   // P), -1 for a base contact (every lane of the quad writes, each its own P)
-  PBG_DEV void put(int r, int slot, const float* yb, const float* yB, float meff, float target, float mu) const {
+  PBG_DEV void put(int r, int slot, const Sc* yb, const Sc* yB, Sc meff, Sc target, Sc mu) const {
     const int k0 = lane & 3;
-    auto pw = [&](int k, int i) -> float {  // word i of lane k's P
+    auto pw = [&](int k, int i) -> Sc {  // word i of lane k's P
       if (i < NDB) return k == slot ? yb[i] : 0.f;
       if (i == NDB) return yB[k];
       return k < 2 ? yB[k + 4] : 0.f;
     };
     if (r < cap) {
-      lds_float* p0 = rows + roff(r) + PW * (lane & ~3);
+      LW* p0 = rows + roff(r) + PW * (lane & ~3);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (slot < 0 && k != k0) continue;
-        float v[PW];
+        Sc v[PW];
 #pragma unroll
         for (int i = 0; i < PW; i++) v[i] = pw(k, i);
         if constexpr (PW == 4) {
-          *(lds_float4*)(p0 + PW * k) = v4f{v[0], v[1], v[2], v[3]};
+          *(LW4*)(p0 + PW * k) = v4f{v[0], v[1], v[2], v[3]};
         } else {
 #pragma unroll
           for (int i = 0; i < PW; i++) p0[PW * k + i] = v[i];
         }
       }
-      *(lds_float4*)S(r) = v4f{meff, target, 0.f, mu};
+      *(LW4*)S(r) = v4f{meff, target, 0.f, mu};
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (slot < 0 && k != k0) continue;
-        float* q = gP(r, k);
+        Sc* q = gP(r, k);
 #pragma unroll
         for (int i = 0; i < PW; i++) q[(size_t)i * n] = pw(k, i);
       }
-      float* q = gS(r);
+      Sc* q = gS(r);
       q[0] = meff; q[n] = target; q[2 * (size_t)n] = 0.f; q[3 * (size_t)n] = mu;
     }
   }
   // One row in registers (loaded ahead of its update: PGS software pipelining): this
   // lane's branch slot and base slice.
   struct Row {
-    float yb[NDB], yB[2], meff, tgt, lam;
+    Sc yb[NDB], yB[2], meff, tgt, lam;
   };
   // LDS: every row of the wave is resident (the common case, no workspace branches)
   template <bool LDS>
   PBG_DEV void load(int r, int kb, Row& row) const {
     if (LDS || r < cap) {
       if constexpr (PW == 4) {
-        const v4f a = *(const lds_float4*)P(r);
+        const v4f a = *(const LW4*)P(r);
         row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
       } else {
-        const lds_float* p = P(r);
+        const LW* p = P(r);
 #pragma unroll
         for (int i = 0; i < NDB; i++) row.yb[i] = p[i];
         row.yB[0] = p[NDB]; row.yB[1] = p[NDB + 1];
@@ -423,14 +449,14 @@ struct TRows {
       // m_eff and target as one b64, lambda as a b32: a b128 whose fourth register (mu) is
       // dead lets the allocator reuse it at once, and the write-after-write on the pending
       // load forces an lgkmcnt(0) wait right behind the look-ahead load (no pipelining)
-      const v2f b = *(const lds_float2*)S(r);
+      const v2f b = *(const LW2*)S(r);
       row.meff = b.x; row.tgt = b.y; row.lam = S(r)[2];
     } else {
-      const float* p = gP(r, kb);
+      const Sc* p = gP(r, kb);
 #pragma unroll
       for (int i = 0; i < NDB; i++) row.yb[i] = p[(size_t)i * n];
       row.yB[0] = p[(size_t)NDB * n]; row.yB[1] = p[(size_t)(NDB + 1) * n];
-      const float* q = gS(r);
+      const Sc* q = gS(r);
       row.meff = q[0]; row.tgt = q[n]; row.lam = q[2 * (size_t)n];
     }
   }
@@ -439,36 +465,36 @@ struct TRows {
   // instead of recomputing the row address from the row index
   PBG_DEV int poff(int r) const { return roff(r) + PW * lane; }
   PBG_DEV int sdelta() const { return SOFF + 4 * (lane >> 2) - PW * lane; }
-  static PBG_DEV void load_at(const lds_float* p, const lds_float* q, Row& row) {
-    const v4f a = *(const lds_float4*)p;
+  static PBG_DEV void load_at(const LW* p, const LW* q, Row& row) {
+    const v4f a = *(const LW4*)p;
     row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
-    const v2f b = *(const lds_float2*)q;
+    const v2f b = *(const LW2*)q;
     row.meff = b.x; row.tgt = b.y; row.lam = q[2];
   }
   template <bool LDS>
-  PBG_DEV void set_lam(int r, float v) const {
+  PBG_DEV void set_lam(int r, Sc v) const {
     if (LDS || r < cap) S(r)[2] = v;
     else gS(r)[2 * (size_t)n] = v;
   }
   // friction bound of contact c: mu * lambda of its normal row (one ds_read_b64)
   template <bool LDS>
-  PBG_DEV float fric_limit(int c) const {
+  PBG_DEV Sc fric_limit(int c) const {
     if (LDS || 3 * c < cap) {
-      const v2f v = *(const lds_float2*)(S(3 * c) + 2);
+      const v2f v = *(const LW2*)(S(3 * c) + 2);
       return v.y * v.x;
     }
-    const float* q = gS(3 * c);
+    const Sc* q = gS(3 * c);
     return q[3 * (size_t)n] * q[2 * (size_t)n];
   }
   // projected Gauss-Seidel update of a loaded row (u: the branch part ub, the base slice
   // uBs); returns the new impulse, bitwise identical in the four lanes
-  static PBG_DEV float update(const Row& r, float* ub, float* uBs, float lo, float hi) {
-    float part = r.yB[0] * uBs[0] + r.yB[1] * uBs[1];
+  static PBG_DEV Sc update(const Row& r, Sc* ub, Sc* uBs, Sc lo, Sc hi) {
+    Sc part = r.yB[0] * uBs[0] + r.yB[1] * uBs[1];
 #pragma unroll
     for (int i = 0; i < NDB; i++) part += r.yb[i] * ub[i];
-    const float yu = quad_sum(part);
-    const float nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
-    const float dl = nl - r.lam;
+    const Sc yu = quad_sum(part);
+    const Sc nl = clampf(r.lam + r.meff * (r.tgt - yu), lo, hi);
+    const Sc dl = nl - r.lam;
     uBs[0] += r.yB[0] * dl;
     uBs[1] += r.yB[1] * dl;
 #pragma unroll
@@ -478,10 +504,11 @@ struct TRows {
 };
 
 // y_base = Lbb^-1 t (6x6 lower, reciprocal diagonal)
-PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
+template <class Sc>
+PBG_DEV void fwd6(const Sc (&Lbb)[6][6], const Sc* Ldb, Sc* t) {
   static_for<0, 6>([&](auto g_c) {
     constexpr int g = decltype(g_c)::value;
-    float v = t[g];
+    Sc v = t[g];
     static_for<0, g>([&](auto h_c) { v -= Lbb[g][decltype(h_c)::value] * t[decltype(h_c)::value]; });
     t[g] = v * Ldb[g];
   });
@@ -493,7 +520,9 @@ PBG_DEV void fwd6(const float (&Lbb)[6][6], const float* Ldb, float* t) {
 // latency overlaps the previous update); the normal pass records which impulses came out
 // positive, so the friction pass walks those contacts without a load-then-test round trip.
 template <bool LDS, class RW>
-PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SUB_STAMP_ARGS) {
+PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, typename RW::Sc* ub, typename RW::Sc* uB SUB_STAMP_ARGS) {
+  using Sc = typename RW::Sc;
+  using LW = typename RW::LW;
   using Row = typename RW::Row;
   if (nc <= 0) return;
   // The look-ahead loads are unconditional (the last row re-reads itself): a prefetch under a
@@ -505,22 +534,22 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
     // clamped at the last normal row (an add and a min per row instead of the index arithmetic)
     constexpr int NS = 3 * RW::ES_ * RW::W;
     const int sd = rw.sdelta();
-    const lds_float* plast = rw.rows + rw.poff(3 * (nc - 1));
-    const lds_float *pA = rw.rows + rw.poff(0), *pB;
-    lds_float *qA = (lds_float*)pA + sd, *qB;
+    const LW* plast = rw.rows + rw.poff(3 * (nc - 1));
+    const LW *pA = rw.rows + rw.poff(0), *pB;
+    LW *qA = (LW*)pA + sd, *qB;
     Row A, B;
     RW::load_at(pA, qA, A);
     int c = 0;
     while (true) {
       pB = pA + NS < plast ? pA + NS : plast;
-      qB = (lds_float*)pB + sd;
+      qB = (LW*)pB + sd;
       RW::load_at(pB, qB, B);
-      float nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
+      Sc nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
       qA[2] = nl;
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
       pA = pB + NS < plast ? pB + NS : plast;
-      qA = (lds_float*)pA + sd;
+      qA = (LW*)pA + sd;
       RW::load_at(pA, qA, A);
       nl = RW::update(B, ub, uB, 0.f, 3.0e38f);
       qB[2] = nl;
@@ -533,7 +562,7 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
     int c = 0;
     while (true) {
       rw.template load<LDS>(3 * min(c + 1, nc - 1), kb, B);
-      float nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
+      Sc nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
       rw.template set_lam<LDS>(3 * c, nl);
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
@@ -553,7 +582,7 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
   Row A1, A2, B1, B2;
   rw.template load<LDS>(3 * c + 1, kb, A1);
   rw.template load<LDS>(3 * c + 2, kb, A2);
-  float limA = rw.template fric_limit<LDS>(c), limB;
+  Sc limA = rw.template fric_limit<LDS>(c), limB;
   while (true) {
     bool more = pos != 0u;
     int c2 = more ? __builtin_ctz(pos) : c;
@@ -580,33 +609,37 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, float* ub, float* uB SU
 
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int ES>
-PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t& slot_bits, uint32_t& base_bits,
-                         const TRows<R, ES>& rw, const SimP& P SUB_STAMP_ARGS) {
+PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint32_t& slot_bits, uint32_t& base_bits,
+                         const TRows<R, ES>& rw, const SimPT<real_t<R>>& P SUB_STAMP_ARGS) {
+  using Sc = real_t<R>;
+  using f3 = V3<Sc>;
+  using m3 = M3<Sc>;
+  using s6 = S6<Sc>;
   using T = Team<R>;
   constexpr int NDB = T::NDB, NLB = T::NLB;
-  const float dt = P.dt;
-  const float g = P.gravity;
+  const Sc dt = P.dt;
+  const Sc g = P.gravity;
   const int kb = L.k;
 
   // --- phase A: branch kinematics, velocities, bias accelerations; composites of the
   // branch's dof-owning links and the branch total (all about O = base COM)
   const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
-  const f3 O = mk3(s.bp[0], s.bp[1], s.bp[2]);
-  const f3 w0 = mk3(s.bw[0], s.bw[1], s.bw[2]), v0 = mk3(s.bv[0], s.bv[1], s.bv[2]);
+  const f3 O = mk3<Sc>(s.bp[0], s.bp[1], s.bp[2]);
+  const f3 w0 = mk3<Sc>(s.bw[0], s.bw[1], s.bw[2]), v0 = mk3<Sc>(s.bv[0], s.bv[1], s.bv[2]);
   TKin<R> k;
   f3 ja[NDB], jo[NDB];
-  float cmass[NLB];
+  Sc cmass[NLB];
   f3 cp1[NLB], cF[NLB], cN[NLB];
   s6 cJ[NLB];
-  float tm = 0.f;
-  f3 tp1 = mk3(0, 0, 0), tF = mk3(0, 0, 0), tN = mk3(0, 0, 0);
+  Sc tm = 0.f;
+  f3 tp1 = mk3<Sc>(0, 0, 0), tF = mk3<Sc>(0, 0, 0), tN = mk3<Sc>(0, 0, 0);
   s6 tJ;
 #pragma unroll
   for (int i = 0; i < 6; i++) tJ.a[i] = 0.f;
   static_for<0, NLB>([&](auto i_c) {
     constexpr int i = decltype(i_c)::value;
     if constexpr (T::owner(i)) {
-      cmass[i] = 0.f; cp1[i] = mk3(0, 0, 0); cF[i] = mk3(0, 0, 0); cN[i] = mk3(0, 0, 0);
+      cmass[i] = 0.f; cp1[i] = mk3<Sc>(0, 0, 0); cF[i] = mk3<Sc>(0, 0, 0); cN[i] = mk3<Sc>(0, 0, 0);
 #pragma unroll
       for (int c = 0; c < 6; c++) cJ[i].a[c] = 0.f;
     }
@@ -620,7 +653,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       const f3 xp = p < 0 ? O : k.x[p < 0 ? 0 : p];
       const f3 cp = p < 0 ? O : k.c[p < 0 ? 0 : p];
       const f3 wp = p < 0 ? w0 : w[p < 0 ? 0 : p], vp = p < 0 ? v0 : v[p < 0 ? 0 : p];
-      const f3 alp = p < 0 ? mk3(0, 0, 0) : al[p < 0 ? 0 : p], acp = p < 0 ? mk3(0, 0, 0) : ac[p < 0 ? 0 : p];
+      const f3 alp = p < 0 ? mk3<Sc>(0, 0, 0) : al[p < 0 ? 0 : p], acp = p < 0 ? mk3<Sc>(0, 0, 0) : ac[p < 0 ? 0 : p];
       m3 Ro;
       static_for<0, 9>([&](auto c_c) { Ro.m[decltype(c_c)::value] = pk<T::ROT, 9 * i + decltype(c_c)::value>(L); });
       const m3 R0 = mulc(Rp, Ro);
@@ -669,12 +702,12 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         ac[i] = acp + cross3(alp, r) + cross3(wp, cross3(wp, r));
       }
       if constexpr (R::link_mass[i] > 0.0) {
-        const float m = pk<T::MASS, i>(L);
-        float I6[6];
+        const Sc m = pk<T::MASS, i>(L);
+        Sc I6[6];
         static_for<0, 6>([&](auto c_c) { I6[decltype(c_c)::value] = pk<T::INER, 6 * i + decltype(c_c)::value>(L); });
         const s6 Iw = rotate_inertia(k.Rm[i], I6);
         const f3 r = k.c[i] - O;
-        const float rr = dot3(r, r);
+        const Sc rr = dot3(r, r);
         s6 J;
         J.a[0] = Iw.a[0] + m * (rr - r.x * r.x);
         J.a[1] = Iw.a[1] + m * (rr - r.y * r.y);
@@ -683,10 +716,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         J.a[4] = Iw.a[4] - m * r.x * r.z;
         J.a[5] = Iw.a[5] - m * r.y * r.z;
         const f3 Iww = mul(Iw, w[i]);
-        const f3 f = m * (ac[i] - mk3(0, 0, -g)) +
-                     (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v[i]))) * v[i];
+        const f3 f = m * (ac[i] - mk3<Sc>(0, 0, -g)) +
+                     (m * ((Sc)PBG_LINEAR_DAMPING + (Sc)PBG_LINEAR_DAMPING * norm3(v[i]))) * v[i];
         const f3 n = mul(Iw, al[i]) + cross3(w[i], Iww) +
-                     ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w[i])) * Iww;
+                     ((Sc)PBG_ANGULAR_DAMPING + (Sc)PBG_ANGULAR_DAMPING * norm3(w[i])) * Iww;
         const f3 pr = m * r, Nn = n + cross3(r, f);
         static_for<0, NLB>([&](auto a_c) {
           constexpr int a = decltype(a_c)::value;
@@ -706,16 +739,16 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   // whole-robot composite = sum of the branch totals + the base body (at O: r = 0)
   {
     tm = quad_sum(tm);
-    tp1 = mk3(quad_sum(tp1.x), quad_sum(tp1.y), quad_sum(tp1.z));
-    tF = mk3(quad_sum(tF.x), quad_sum(tF.y), quad_sum(tF.z));
-    tN = mk3(quad_sum(tN.x), quad_sum(tN.y), quad_sum(tN.z));
+    tp1 = mk3<Sc>(quad_sum(tp1.x), quad_sum(tp1.y), quad_sum(tp1.z));
+    tF = mk3<Sc>(quad_sum(tF.x), quad_sum(tF.y), quad_sum(tF.z));
+    tN = mk3<Sc>(quad_sum(tN.x), quad_sum(tN.y), quad_sum(tN.z));
 #pragma unroll
     for (int c = 0; c < 6; c++) tJ.a[c] = quad_sum(tJ.a[c]);
-    const float m = (float)R::base_mass;
+    const Sc m = (Sc)R::base_mass;
     const s6 Iw = rotate_inertia(Rb, R::base_inertia);
     const f3 Iww = mul(Iw, w0);
-    const f3 f = m * (mk3(0, 0, g)) + (m * ((float)PBG_LINEAR_DAMPING + (float)PBG_LINEAR_DAMPING * norm3(v0))) * v0;
-    const f3 n = cross3(w0, Iww) + ((float)PBG_ANGULAR_DAMPING + (float)PBG_ANGULAR_DAMPING * norm3(w0)) * Iww;
+    const f3 f = m * (mk3<Sc>(0, 0, g)) + (m * ((Sc)PBG_LINEAR_DAMPING + (Sc)PBG_LINEAR_DAMPING * norm3(v0))) * v0;
+    const f3 n = cross3(w0, Iww) + ((Sc)PBG_ANGULAR_DAMPING + (Sc)PBG_ANGULAR_DAMPING * norm3(w0)) * Iww;
     tm += m; tF += f; tN += n;
 #pragma unroll
     for (int c = 0; c < 6; c++) tJ.a[c] += Iw.a[c];
@@ -723,14 +756,14 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 
   STAMP(0)
   // --- mass matrix: branch block Lbr, base-branch block Lgb, base block Mbb; bias -------
-  float Lbr[NDB][NDB], Lgb[6][NDB], Mbb[6][6];
-  float rb[NDB], rB[6];
+  Sc Lbr[NDB][NDB], Lgb[6][NDB], Mbb[6][6];
+  Sc rb[NDB], rB[6];
   f3 sw[NDB], sv[NDB];
   static_for<0, NDB>([&](auto a_c) {
     constexpr int a = decltype(a_c)::value;
     constexpr int d = T::dof_of(a);
     if constexpr (R::dof_jtype[d] == 0) { sw[a] = ja[d]; sv[a] = cross3(jo[d] - O, ja[d]); }
-    else { sw[a] = mk3(0, 0, 0); sv[a] = ja[d]; }
+    else { sw[a] = mk3<Sc>(0, 0, 0); sv[a] = ja[d]; }
   });
   static_for<0, NDB>([&](auto a_c) {
     constexpr int a = decltype(a_c)::value;
@@ -771,22 +804,22 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 
   STAMP(1)
   // --- Cholesky: branch columns (lane), Schur complement of the base (quad sum), 6x6 ----
-  float Ld[NDB];
+  Sc Ld[NDB];
   static_for<0, NDB>([&](auto b_c) {
     constexpr int b = decltype(b_c)::value;
-    float sbb = Lbr[b][b];
+    Sc sbb = Lbr[b][b];
     static_for<0, b>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       if constexpr (T::coupled(b, kk)) sbb -= Lbr[b][kk] * Lbr[b][kk];
     });
-    const float lbb = fast_sqrt(sbb);
-    const float inv = fast_rcp(lbb);
+    const Sc lbb = fast_sqrt(sbb);
+    const Sc inv = fast_rcp(lbb);
     Ld[b] = inv;
     Lbr[b][b] = lbb;
     static_for<b + 1, NDB>([&](auto a_c) {
       constexpr int a = decltype(a_c)::value;
       if constexpr (T::coupled(a, b)) {
-        float t = Lbr[a][b];
+        Sc t = Lbr[a][b];
         static_for<0, b>([&](auto k_c) {
           constexpr int kk = decltype(k_c)::value;
           if constexpr (T::coupled(a, kk) && T::coupled(b, kk)) t -= Lbr[a][kk] * Lbr[b][kk];
@@ -796,7 +829,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     });
 #pragma unroll
     for (int gg = 0; gg < 6; gg++) {
-      float t = Lgb[gg][b];
+      Sc t = Lgb[gg][b];
       static_for<0, b>([&](auto k_c) {
         constexpr int kk = decltype(k_c)::value;
         if constexpr (T::coupled(b, kk)) t -= Lgb[gg][kk] * Lbr[b][kk];
@@ -804,12 +837,12 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
       Lgb[gg][b] = t * inv;
     }
   });
-  float Lbb[6][6], Ldb[6];
+  Sc Lbb[6][6], Ldb[6];
   static_for<0, 6>([&](auto g_c) {
     constexpr int gg = decltype(g_c)::value;
     static_for<0, gg + 1>([&](auto h_c) {
       constexpr int h = decltype(h_c)::value;
-      float c = 0.f;
+      Sc c = 0.f;
 #pragma unroll
       for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * Lgb[h][b];
       Lbb[gg][h] = Mbb[gg][h] - quad_sum(c);
@@ -817,25 +850,25 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
   static_for<0, 6>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
-    float sjj = Lbb[j][j];
+    Sc sjj = Lbb[j][j];
     static_for<0, j>([&](auto k_c) { sjj -= Lbb[j][decltype(k_c)::value] * Lbb[j][decltype(k_c)::value]; });
-    const float ljj = fast_sqrt(sjj);
-    const float inv = fast_rcp(ljj);
+    const Sc ljj = fast_sqrt(sjj);
+    const Sc inv = fast_rcp(ljj);
     Ldb[j] = inv;
     Lbb[j][j] = ljj;
     static_for<j + 1, 6>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
-      float t = Lbb[i][j];
+      Sc t = Lbb[i][j];
       static_for<0, j>([&](auto k_c) { t -= Lbb[i][decltype(k_c)::value] * Lbb[j][decltype(k_c)::value]; });
       Lbb[i][j] = t * inv;
     });
   });
 
   // --- unconstrained velocity nu_pred = nu + dt M^-1 (tau - C); u = L^T nu_pred --------
-  float yb[NDB], yB[6];
+  Sc yb[NDB], yB[6];
   static_for<0, NDB>([&](auto a_c) {
     constexpr int a = decltype(a_c)::value;
-    float t = rb[a];
+    Sc t = rb[a];
     static_for<0, a>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       if constexpr (T::coupled(a, kk)) t -= Lbr[a][kk] * yb[kk];
@@ -844,22 +877,22 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
 #pragma unroll
   for (int gg = 0; gg < 6; gg++) {
-    float c = 0.f;
+    Sc c = 0.f;
 #pragma unroll
     for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * yb[b];
     yB[gg] = rB[gg] - quad_sum(c);
   }
   fwd6(Lbb, Ldb, yB);
-  float xB[6], xb[NDB];
+  Sc xB[6], xb[NDB];
   static_for<0, 6>([&](auto r_c) {
     constexpr int gg = 5 - decltype(r_c)::value;
-    float t = yB[gg];
+    Sc t = yB[gg];
     static_for<gg + 1, 6>([&](auto h_c) { t -= Lbb[decltype(h_c)::value][gg] * xB[decltype(h_c)::value]; });
     xB[gg] = t * Ldb[gg];
   });
   static_for<0, NDB>([&](auto r_c) {
     constexpr int a = NDB - 1 - decltype(r_c)::value;
-    float t = yb[a];
+    Sc t = yb[a];
     static_for<a + 1, NDB>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       if constexpr (T::coupled(kk, a)) t -= Lbr[kk][a] * xb[kk];
@@ -868,21 +901,21 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     for (int gg = 0; gg < 6; gg++) t -= Lgb[gg][a] * xB[gg];
     xb[a] = t * Ld[a];
   });
-  float nb[NDB], nB[6];
+  Sc nb[NDB], nB[6];
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
     constexpr int a = T::lg(j);
-    nb[a] = clampf(s.qd[j] + dt * xb[a], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    nb[a] = clampf(s.qd[j] + dt * xb[a], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
   });
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    nB[i] = clampf(s.bv[i] + dt * xB[i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
-    nB[3 + i] = clampf(s.bw[i] + dt * xB[3 + i], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    nB[i] = clampf(s.bv[i] + dt * xB[i], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
+    nB[3 + i] = clampf(s.bw[i] + dt * xB[3 + i], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
   }
-  float ub[NDB], uB[6];
+  Sc ub[NDB], uB[6];
   static_for<0, NDB>([&](auto a_c) {
     constexpr int a = decltype(a_c)::value;
-    float t = 0.f;
+    Sc t = 0.f;
     static_for<a, NDB>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       if constexpr (T::coupled(kk, a)) t += Lbr[kk][a] * nb[kk];
@@ -893,7 +926,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
   static_for<0, 6>([&](auto g_c) {
     constexpr int gg = decltype(g_c)::value;
-    float t = 0.f;
+    Sc t = 0.f;
     static_for<gg, 6>([&](auto h_c) { t += Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
     uB[gg] = t;
   });
@@ -906,7 +939,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     return c;
   }();
   constexpr int NLB_ = NLIMB > 0 ? NLIMB : 1;
-  float Lyb[NLB_][NDB], Lm[NLB_], Ltl[NLB_], Lth[NLB_], LyB[NLB_][6];
+  Sc Lyb[NLB_][NDB], Lm[NLB_], Ltl[NLB_], Lth[NLB_], LyB[NLB_][6];
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
     if constexpr (R::dof_limited[j]) {
@@ -916,13 +949,13 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
         return c;
       }();
       constexpr int gd = T::lg(j);
-      float y[NDB];
+      Sc y[NDB];
       static_for<0, NDB>([&](auto a_c) {
         constexpr int a = decltype(a_c)::value;
         if constexpr (a < gd || !T::coupled(a, gd)) {
           y[a] = 0.f;
         } else {
-          float t = a == gd ? 1.f : 0.f;
+          Sc t = a == gd ? 1.f : 0.f;
           static_for<gd, a>([&](auto k_c) {
             constexpr int kk = decltype(k_c)::value;
             if constexpr (T::coupled(a, kk) && T::coupled(kk, gd)) t -= Lbr[a][kk] * y[kk];
@@ -930,22 +963,22 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
           y[a] = t * Ld[a];
         }
       });
-      float t6[6];
+      Sc t6[6];
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) {
-        float c = 0.f;
+        Sc c = 0.f;
 #pragma unroll
         for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * y[b];
         t6[gg] = -c;
       }
       fwd6(Lbb, Ldb, t6);
-      float D2 = 0.f;
+      Sc D2 = 0.f;
 #pragma unroll
       for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; }
-      const float meff = D2 > 1e-12f ? fast_rcp(D2) : 0.f;
-      const float plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
+      const Sc meff = D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f;
+      const Sc plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
       Ltl[li] = pos_target(plo, P.k_limit, P.k_sep);
       Lth[li] = pos_target(phi, P.k_limit, P.k_sep);
       Lm[li] = meff;
@@ -959,15 +992,15 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   // kb + 4) of each branch's base part (the sweeps' base dot products are sliced)
   // (and its own branch part, zero in the lanes of the other branches: no owner test in
   // the sweeps)
-  float BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
-  float Byb[4][NLB_][NDB];
+  Sc BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
+  Sc Byb[4][NLB_][NDB];
   static_for<0, 4>([&](auto k_c) {
     constexpr int kk = decltype(k_c)::value;
     static_for<0, NLIMB>([&](auto l_c) {
       constexpr int li = decltype(l_c)::value;
 #pragma unroll
       for (int a = 0; a < NDB; a++) Byb[kk][li][a] = kb == kk ? Lyb[li][a] : 0.f;
-      float b6[6];
+      Sc b6[6];
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
       BY[kk][li][0] = kb == 0 ? b6[0] : (kb == 1 ? b6[1] : (kb == 2 ? b6[2] : b6[3]));
@@ -987,41 +1020,41 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   base_bits = 0;
   static_for<0, T::NS0>([&](auto sl_c) {
     constexpr int sl = decltype(sl_c)::value;
-    const f3 cc = O + mulc(Rb, (float)R::slot_point[sl][0], (float)R::slot_point[sl][1], (float)R::slot_point[sl][2]);
-    const float rad = (float)R::slot_radius[sl];
-    const float dist = cc.z - rad;
-    if (!(dist < (float)PBG_CONTACT_THRESHOLD)) return;
+    const f3 cc = O + mulc(Rb, (Sc)R::slot_point[sl][0], (Sc)R::slot_point[sl][1], (Sc)R::slot_point[sl][2]);
+    const Sc rad = (Sc)R::slot_radius[sl];
+    const Sc dist = cc.z - rad;
+    if (!(dist < (Sc)PBG_CONTACT_THRESHOLD)) return;
     base_bits |= 1u << sl;
-    const f3 rP = mk3(cc.x, cc.y, cc.z - rad) - O;
+    const f3 rP = mk3<Sc>(cc.x, cc.y, cc.z - rad) - O;
 #pragma unroll
     for (int dir = 0; dir < 3; dir++) {
-      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
       const f3 mm = cross3(rP, nd);
-      float y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+      Sc y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
       fwd6(Lbb, Ldb, y6);
-      float D2 = 0.f;
+      Sc D2 = 0.f;
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
-      float z[NDB];
+      Sc z[NDB];
 #pragma unroll
       for (int a = 0; a < NDB; a++) z[a] = 0.f;
-      rw.put(3 * n0 + dir, -1, z, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (float)R::slot_mu[sl]);
+      rw.put(3 * n0 + dir, -1, z, y6, D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f,
+             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (Sc)R::slot_mu[sl]);
     }
     n0++;
   });
   // this branch's active slots, then their contact indices (exclusive quad prefix)
   uint32_t act = 0;
-  float sdist[T::NSB > 0 ? T::NSB : 1];
+  Sc sdist[T::NSB > 0 ? T::NSB : 1];
   f3 sP[T::NSB > 0 ? T::NSB : 1];
   static_for<0, T::NSB>([&](auto sl_c) {
     constexpr int sl = decltype(sl_c)::value;
     constexpr int li = R::slot_link[T::NS0 + sl];
     const f3 cc = k.x[li] + mulc(k.Rm[li], pk3<T::SPT, sl>(L));
-    const float rad = pk<T::SRAD, sl>(L);
+    const Sc rad = pk<T::SRAD, sl>(L);
     sdist[sl] = cc.z - rad;
-    sP[sl] = mk3(cc.x, cc.y, cc.z - rad);
-    act |= (sdist[sl] < (float)PBG_CONTACT_THRESHOLD ? 1u : 0u) << sl;
+    sP[sl] = mk3<Sc>(cc.x, cc.y, cc.z - rad);
+    act |= (sdist[sl] < (Sc)PBG_CONTACT_THRESHOLD ? 1u : 0u) << sl;
   });
   const int cnt = __builtin_popcount(act);
   const int c0 = quad_bcast_i<0>(cnt), c1 = quad_bcast_i<1>(cnt), c2 = quad_bcast_i<2>(cnt), c3 = quad_bcast_i<3>(cnt);
@@ -1032,19 +1065,19 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     constexpr int sl = decltype(sl_c)::value;
     if (!((act >> sl) & 1u)) return;
     constexpr int li = R::slot_link[T::NS0 + sl];
-    const float dist = sdist[sl];
+    const Sc dist = sdist[sl];
     const f3 rP = sP[sl] - O;
 #pragma unroll
     for (int dir = 0; dir < 3; dir++) {
-      const f3 nd = dir == 0 ? mk3(0, 0, 1) : (dir == 1 ? mk3(0, -1, 0) : mk3(1, 0, 0));
+      const f3 nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
       const f3 mm = cross3(rP, nd);
-      float y[NDB];
+      Sc y[NDB];
       static_for<0, NDB>([&](auto a_c) {
         constexpr int a = decltype(a_c)::value;
         if constexpr (!T::in_chain(a, li)) {
           y[a] = 0.f;
         } else {
-          float t = dot3(nd, sv[a]) + dot3(mm, sw[a]);
+          Sc t = dot3(nd, sv[a]) + dot3(mm, sw[a]);
           static_for<0, a>([&](auto k_c) {
             constexpr int kk = decltype(k_c)::value;
             if constexpr (T::coupled(a, kk) && T::in_chain(kk, li)) t -= Lbr[a][kk] * y[kk];
@@ -1052,19 +1085,19 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
           y[a] = t * Ld[a];
         }
       });
-      float y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+      Sc y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) {
 #pragma unroll
         for (int b = 0; b < NDB; b++) y6[gg] -= Lgb[gg][b] * y[b];
       }
       fwd6(Lbb, Ldb, y6);
-      float D2 = 0.f;
+      Sc D2 = 0.f;
 #pragma unroll
       for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
 #pragma unroll
       for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
-      rw.put(3 * ci + dir, kb, y, y6, D2 > 1e-12f ? fast_rcp(D2) : 0.f,
+      rw.put(3 * ci + dir, kb, y, y6, D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f,
              dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, pk<T::SMU, sl>(L));
     }
     ci++;
@@ -1080,29 +1113,29 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   STAMP(4)
   // --- PGS, 5 sweeps, Bullet order: joint limits (dof order), normals, frictions ------
   // u's base part sliced over the quad: lane kb owns components kb and kb + 4 (kb < 2)
-  float uBs[2] = {kb == 0 ? uB[0] : (kb == 1 ? uB[1] : (kb == 2 ? uB[2] : uB[3])),
+  Sc uBs[2] = {kb == 0 ? uB[0] : (kb == 1 ? uB[1] : (kb == 2 ? uB[2] : uB[3])),
                   kb == 0 ? uB[4] : (kb == 1 ? uB[5] : 0.f)};
   for (int it = 0; it < P.iterations; it++) {
     static_for<0, 4>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       static_for<0, NLIMB>([&](auto l_c) {
         constexpr int li = decltype(l_c)::value;
-        float part = BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1];
+        Sc part = BY[kk][li][0] * uBs[0] + BY[kk][li][1] * uBs[1];
         static_for<0, NDB>([&](auto a_c) {  // structural zeros of the row skipped
           constexpr int a = decltype(a_c)::value;
           if constexpr (T::lim_nz(li, a)) part += Byb[kk][li][a] * ub[a];
         });
-        const float yu = quad_sum(part);
-        const float meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
-        const float nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-        const float dlo = nlo - llo;
+        const Sc yu = quad_sum(part);
+        const Sc meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
+        const Sc nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+        const Sc dlo = nlo - llo;
         // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const float yu2 = yu + dlo * Brm[kk][li];  // Brm = 0 when meff = 0
-        const float nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (float)PBG_LIMIT_MAX_IMPULSE);
-        const float dhi = nhi - lhi;
+        const Sc yu2 = yu + dlo * Brm[kk][li];  // Brm = 0 when meff = 0
+        const Sc nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+        const Sc dhi = nhi - lhi;
         Blo[kk][li] = nlo;
         Bhi[kk][li] = nhi;
-        const float dl = dlo - dhi;
+        const Sc dl = dlo - dhi;
         uBs[0] += BY[kk][li][0] * dl;
         uBs[1] += BY[kk][li][1] * dl;
         static_for<0, NDB>([&](auto a_c) {
@@ -1118,7 +1151,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   }
   // gather the base part back (replicated for the back-substitution)
   {
-    const float s0 = uBs[0], s1 = uBs[1];
+    const Sc s0 = uBs[0], s1 = uBs[1];
     uB[0] = quad_bcast<0>(s0); uB[1] = quad_bcast<1>(s0); uB[2] = quad_bcast<2>(s0); uB[3] = quad_bcast<3>(s0);
     uB[4] = quad_bcast<0>(s1); uB[5] = quad_bcast<1>(s1);
   }
@@ -1127,13 +1160,13 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   // --- nu = L^-T u (base first, replicated; then the branch); clamp; integrate ---------
   static_for<0, 6>([&](auto r_c) {
     constexpr int gg = 5 - decltype(r_c)::value;
-    float t = uB[gg];
+    Sc t = uB[gg];
     static_for<gg + 1, 6>([&](auto h_c) { t -= Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
-    nB[gg] = clampf(t * Ldb[gg], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    nB[gg] = clampf(t * Ldb[gg], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
   });
   static_for<0, NDB>([&](auto r_c) {
     constexpr int a = NDB - 1 - decltype(r_c)::value;
-    float t = ub[a];
+    Sc t = ub[a];
     static_for<a + 1, NDB>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       if constexpr (T::coupled(kk, a)) t -= Lbr[kk][a] * nb[kk];
@@ -1144,7 +1177,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
   });
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
-    s.qd[j] = clampf(nb[T::lg(j)], -(float)PBG_MAX_COORD_VELOCITY, (float)PBG_MAX_COORD_VELOCITY);
+    s.qd[j] = clampf(nb[T::lg(j)], -(Sc)PBG_MAX_COORD_VELOCITY, (Sc)PBG_MAX_COORD_VELOCITY);
     s.q[j] += dt * s.qd[j];
   });
 #pragma unroll
@@ -1154,20 +1187,20 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
     s.bp[i] += dt * s.bv[i];
   }
   {
-    const f3 wv = mk3(s.bw[0], s.bw[1], s.bw[2]);
-    float ang = norm3(wv);
-    if (ang * dt > (float)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
-    float sh, dw;
-    sincos_fast(0.5f * ang * dt, &sh, &dw);
+    const f3 wv = mk3<Sc>(s.bw[0], s.bw[1], s.bw[2]);
+    Sc ang = norm3(wv);
+    if (ang * dt > (Sc)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
+    Sc sh, dw;
+    sincos_fast(Sc(0.5f) * ang * dt, &sh, &dw);
     f3 ax;
-    if (ang < 0.001f) ax = (0.5f * dt - P.dt3c * ang * ang) * wv;
+    if (ang < Sc(0.001)) ax = (Sc(0.5f) * dt - P.dt3c * ang * ang) * wv;
     else ax = (sh / ang) * wv;
-    const float x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
-    const float nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
-    const float ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
-    const float nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
-    const float nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
-    const float inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+    const Sc x = s.bq[0], y = s.bq[1], z = s.bq[2], ww = s.bq[3];
+    const Sc nx = dw * x + ax.x * ww + ax.y * z - ax.z * y;
+    const Sc ny = dw * y - ax.x * z + ax.y * ww + ax.z * x;
+    const Sc nz = dw * z + ax.x * y - ax.y * x + ax.z * ww;
+    const Sc nw = dw * ww - ax.x * x - ax.y * y - ax.z * z;
+    const Sc inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
     s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
   }
   STAMP(6)
@@ -1180,6 +1213,9 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const float* tau, uint32_t
 template <class R, int ES>
 PBG_DEV void team_gather(const TState<R>& s, const Lane& L, const TRows<R, ES>& rw, bool has_floor, PackIn<R>& in) {
   using T = Team<R>;
+  using Sc = real_t<R>;
+  using f3 = V3<Sc>;
+  using m3 = M3<Sc>;
   constexpr int NL = R::NL, NJ = R::NJ, NDB = T::NDB, NLB = T::NLB;
   const m3 Rb = quat_to_m3(s.bq[0], s.bq[1], s.bq[2], s.bq[3]);
   TKin<R> k;
@@ -1220,12 +1256,13 @@ PBG_DEV void team_gather(const TState<R>& s, const Lane& L, const TRows<R, ES>& 
 // snapshot + Philox reset noise (pbg_step.hip reset_env); returns the reset pack
 template <class R, int ES>
 PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, const TRows<R, ES>& rw, float* obs,
-                        bool& has_floor, double& pot, float& z0) {
+                        bool& has_floor, double& pot, real_t<R>& z0) {
   using T = Team<R>;
+  using Sc = real_t<R>;
 #pragma unroll
-  for (int i = 0; i < 3; i++) s.bp[i] = (float)R::base_pos[i];
+  for (int i = 0; i < 3; i++) s.bp[i] = (Sc)R::base_pos[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) s.bq[i] = (float)R::base_quat[i];
+  for (int i = 0; i < 4; i++) s.bq[i] = (Sc)R::base_quat[i];
 #pragma unroll
   for (int i = 0; i < 3; i++) { s.bv[i] = 0.f; s.bw[i] = 0.f; }
   const uint32_t epi = B.episode[e];
@@ -1243,14 +1280,14 @@ PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, co
   static_for<0, T::NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
     const int r = pki<T::RST, j>(L);
-    float q = 0.f;
+    Sc q = 0.f;
 #pragma unroll
     for (int t = 0; t < R::NR; t++) q = r == t ? noise[t] : q;
     s.q[j] = q;
     s.qd[j] = 0.f;
   });
   PackIn<R> in;
-  in.env_dt = B.sp.env_dt;
+  in.env_dt = sp_of<R>(B).env_dt;
   team_gather<R, ES>(s, L, rw, has_floor, in);
 #pragma unroll
   for (int f = 0; f < R::NF; f++) in.feet_prev[f] = 0.f;
@@ -1261,7 +1298,7 @@ PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, co
   if constexpr (R::kind == 3) mujoco3d_pack<R>(in, nullptr, obs, po);
   else walker_pack<R>(in, nullptr, obs, po);
   pot = po.potential;
-  z0 = (float)po.initial_z;
+  z0 = (Sc)po.initial_z;
   has_floor = true;
   if (L.k == 0) B.episode[e] = epi + 1;
 }
@@ -1269,6 +1306,8 @@ PBG_DEV void team_reset(const Buffers& B, int e, const Lane& L, TState<R>& s, co
 template <class R, int ES>
 __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int lds_rows) {
   using T = Team<R>;
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
   constexpr int NDB = T::NDB, SB = PBG_BASE_WORDS;
   extern __shared__ float lds_dyn[];
   const int tid = xcd_block() * blockDim.x + threadIdx.x;
@@ -1295,33 +1334,33 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   const int el = B.elapsed[e] + 1;
   uint32_t flags = B.flags[e];
   const double pot_old = B.pot[e];
-  const float z0_old = z0_of<R>(B)[e];
+  const Sc z0_old = z0_of<R>(B)[e];
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
   // apply_action (robot_locomotors.py:26-29): this branch's motors
-  float tau[NDB];
+  Sc tau[NDB];
   static_for<0, NDB>([&](auto j_c) {
     constexpr int j = decltype(j_c)::value;
     const int ai = pki<T::ACTI, j>(L);
     float a = 0.f;
 #pragma unroll
     for (int i = 0; i < R::NA; i++) a = ai == i ? act[i] : a;
-    tau[j] = ai < 0 ? 0.f : (float)((double)pk<T::GAIN, j>(L) * (double)fminf(fmaxf(a, -1.f), 1.f));
+    tau[j] = ai < 0 ? 0.f : (Sc)((double)pk<T::GAIN, j>(L) * (double)fminf(fmaxf(a, -1.f), 1.f));
   });
   TRows<R, ES> rw;
-  rw.lds = (lds_float*)lds_dyn + (threadIdx.x >> 2);
-  rw.rows = (lds_float*)lds_dyn + TRows<R, ES>::HEAD * ES;
+  rw.lds = (LW*)lds_dyn + (threadIdx.x >> 2);
+  rw.rows = (LW*)lds_dyn + TRows<R, ES>::HEAD * ES;
   rw.lane = threadIdx.x;
-  rw.gbl = scratch + e;
+  rw.gbl = (Sc*)scratch + e;
   rw.n = B.n;
   rw.cap = lds_rows;
   uint32_t slot_bits = 0, base_bits = 0;
   int nc = 0;
   STAMP(7)
   uint32_t csig = 0;  // this lane's share of the contact-set signature
-  for (int sub = 0; sub < B.sp.substeps; sub++) {
-    nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw, B.sp SUB_STAMP_PASS);
+  for (int sub = 0; sub < sp_of<R>(B).substeps; sub++) {
+    nc = team_substep<R, ES>(s, L, tau, slot_bits, base_bits, rw, sp_of<R>(B) SUB_STAMP_PASS);
     if (io.csig) {  // base slots counted by lane 0, branch k's slots (global NS0 + k NSB + sl) by lane k
       if (kb == 0)
         for (int sl = 0; sl < T::NS0; sl++)
@@ -1350,7 +1389,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   PackOut po;
   {
     PackIn<R> in;
-    in.env_dt = B.sp.env_dt;
+    in.env_dt = sp_of<R>(B).env_dt;
     team_gather<R, ES>(s, L, rw, flags & 1u, in);
 #pragma unroll
     for (int f = 0; f < R::NF; f++) in.feet_prev[f] = ((flags >> (8 + f)) & 1u) ? 1.f : 0.f;
@@ -1378,7 +1417,7 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     if (io.term_obs) lanes_store_row<R, 4>(obs, io.term_obs, e, kb);
     bool has_floor = flags & 1u;
     double pot;
-    float z0;
+    Sc z0;
     team_reset<R, ES>(B, e, L, s, rw, obs, has_floor, pot, z0);
     if (kb == 0) {
       B.pot[e] = pot;
@@ -1393,11 +1432,11 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
   }
   {
     // replicated base words and obs dealt over the quad (lane kb: elements kb, kb+4, ...)
-    const float bw[PBG_BASE_WORDS] = {s.bp[0], s.bp[1], s.bp[2], s.bq[0], s.bq[1], s.bq[2], s.bq[3],
+    const Sc bw[PBG_BASE_WORDS] = {s.bp[0], s.bp[1], s.bp[2], s.bq[0], s.bq[1], s.bq[2], s.bq[3],
                                       s.bv[0], s.bv[1], s.bv[2], s.bw[0], s.bw[1], s.bw[2]};
     static_for<0, (PBG_BASE_WORDS + 3) / 4>([&](auto m_c) {
       constexpr int m = decltype(m_c)::value;
-      const float v = lanes_pick<4, m, PBG_BASE_WORDS>(bw, kb);
+      const Sc v = lanes_pick<4, m, PBG_BASE_WORDS>(bw, kb);
       if (4 * m + kb < PBG_BASE_WORDS) st_of<R>(B)[(size_t)(4 * m + kb) * B.n + e] = v;
     });
     lanes_store_row<R, 4>(obs, io.obs, e, kb);

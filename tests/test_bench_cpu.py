@@ -22,7 +22,7 @@ def test_bench_two_rank_dry_run_cpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["global_envs"] == 10
     assert d["scaling"] == "weak" and "dry_run" in d and d["allgather_step_bytes"] == 10 * (28 + 2) * 4
-    assert d["hopper"]["global_envs"] == 6
+    assert d["hopper_f32"]["global_envs"] == 6
 
 
 def test_cpu_baseline_leg_with_autoreset():

@@ -257,9 +257,11 @@ def test_f64_atlas_is_refused():
 
 
 # ------------------------------------------------------------------ float64 kernel variants
-# The float64 walkers run the 16-lane gang kernel (pbg_gang.hip instantiated on F64<R>; Ant
-# included -- the quad kernel has no float64 variant); kernel=0 selects the float64 lane-per-env
-# kernel, which stays the pendulums' path and the gang kernel's cross-check.
+# The float64 walkers run the kernels of the float32 path instantiated on F64<R>: Ant the quad
+# kernel (pbg_team.hip, 4 lanes per env), the other walkers (AntMuJoCo included: its float64 quad
+# instance is miscompiled, pbg_robot.hip) the 16-lane gang kernel (pbg_gang.hip; kernel=2 puts Ant
+# on it too); kernel=0 selects the float64 lane-per-env kernel, which stays the
+# pendulums' path and the quad / gang kernels' cross-check.
 @pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HopperPyBulletEnv-v0",
                                     "HumanoidFlagrunHarderPyBulletEnv-v0"])
 def test_f64_lane_kernel_teacher_forced(env_id):
@@ -267,16 +269,19 @@ def test_f64_lane_kernel_teacher_forced(env_id):
     _teacher_forced64(env_id, 128, 40, name=f"f64_lane[{env_id}]", kernel=0)
 
 
-@pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0",
-                                    "Walker2DPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0",
-                                    "HumanoidFlagrunHarderPyBulletEnv-v0"])
-def test_f64_gang_matches_f64_lane(env_id):
-    """Float64 gang vs float64 lane kernel from the same states every step: the same contact sets
-    and the state within 1e-9 (different summation orders in float64)."""
+@pytest.mark.parametrize("env_id,kernel,lanes", [
+    ("AntPyBulletEnv-v0", None, 4), ("AntMuJoCoEnv-v0", None, 16), ("AntPyBulletEnv-v0", 2, 16),
+    ("HumanoidPyBulletEnv-v0", None, 16), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
+    ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 16),
+    ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 16)])
+def test_f64_quad_and_gang_match_f64_lane(env_id, kernel, lanes):
+    """Float64 quad / gang vs float64 lane kernel from the same states every step: the same contact
+    sets and the state within 1e-9 (different summation orders in float64)."""
     n = 256
-    g = VecEnv(env_id, n, seed=3, autoreset=False, precision=64)
+    kw = {} if kernel is None else {"kernel": kernel}
+    g = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, **kw)
     ln = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, kernel=0)
-    assert g.info.lanes_per_env == 16 and ln.info.lanes_per_env == 1
+    assert g.info.lanes_per_env == lanes and ln.info.lanes_per_env == 1
     r = np.random.default_rng(7)
     g.reset(init_q=torch.from_numpy(r.uniform(-0.1, 0.1, (n, g.info.reset_dofs)).astype(np.float32)))
     errs, same_n = [], 0
@@ -292,10 +297,31 @@ def test_f64_gang_matches_f64_lane(env_id):
         same_n += int(same.sum())
         np.testing.assert_array_equal(g.ncontact.cpu().numpy()[same], ln.ncontact.cpu().numpy()[same])
     e = np.concatenate(errs)
-    rec = dict(test=f"f64_gang_vs_lane[{env_id}]", same_frac=same_n / (30 * n), max_rel=float(e.max()),
+    rec = dict(test=f"f64_{'quad' if lanes == 4 else 'gang'}_vs_lane[{env_id}]", same_frac=same_n / (30 * n), max_rel=float(e.max()),
                share_within_1e_9=float((e <= STATE_REL64).mean()))
     _report(rec)
     assert rec["same_frac"] >= 1 - LOOSE_FRAC64 and rec["share_within_1e_9"] >= SHARE64 and rec["max_rel"] <= HARD_MAX64, rec
+
+
+def test_f64_quad_workspace_rows_bitwise_equal_lds_rows():
+    """Float64 quad (Ant): contact rows past the LDS capacity (lds_rows=0: every row in the device
+    workspace) change no bit; the default plan keeps rows in LDS."""
+    def run(**kw):
+        e = VecEnv("AntPyBulletEnv-v0", 256, seed=13, autoreset=True, precision=64, **kw)
+        assert e.info.lanes_per_env == 4
+        e.reset()
+        gen = torch.Generator(device="cuda").manual_seed(6)
+        out, nc = [], []
+        for _ in range(40):
+            e.step(torch.rand((256, 8), device="cuda", generator=gen) * 2 - 1, want_contacts=True)
+            out.append(e.get_state()[0].clone())
+            nc.append(e.ncontact.clone())
+        return torch.stack(out).cpu().numpy(), torch.stack(nc).cpu().numpy(), e.info.lds_rows
+    a, ca, cap = run()
+    b, cb, cap0 = run(lds_rows=0)
+    assert ca.max() > 0 and cap > 0 and cap0 == 0
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
 
 
 def test_f64_gang_workspace_contacts_bitwise_equal_lds_contacts():

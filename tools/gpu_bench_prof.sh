@@ -13,14 +13,16 @@ export TMPDIR=/tmp
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 # the bench command itself (same steps / warmup), without the CPU leg
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
-for W in ${PROF_ROBOTS:-ant humanoid hopper halfcheetah ant_f64 humanoid_f64}; do
+for W in ${PROF_ROBOTS:-ant humanoid hopper halfcheetah ant_f64 humanoid_f64 hopper_f64 halfcheetah_f64}; do
   case $W in
-    ant) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384";;
-    humanoid) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096";;
-    hopper) A="--env HopperPyBulletEnv-v0 --envs-per-gpu 4096";;
-    halfcheetah) A="--env HalfCheetahPyBulletEnv-v0 --envs-per-gpu 8192";;
+    ant) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384 --precision 32";;
+    humanoid) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096 --precision 32";;
+    hopper) A="--env HopperPyBulletEnv-v0 --envs-per-gpu 4096 --precision 32";;
+    halfcheetah) A="--env HalfCheetahPyBulletEnv-v0 --envs-per-gpu 8192 --precision 32";;
     ant_f64) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384 --precision 64";;
     humanoid_f64) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096 --precision 64";;
+    hopper_f64) A="--env HopperPyBulletEnv-v0 --envs-per-gpu 4096 --precision 64";;
+    halfcheetah_f64) A="--env HalfCheetahPyBulletEnv-v0 --envs-per-gpu 8192 --precision 64";;
   esac
   B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline --second-env none $A"
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$W/pmc_fetch -o run -- $B > $OUT/$W.pmc_fetch.log 2>&1

@@ -15,7 +15,10 @@ import sys
 src, rnd = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 res = {}
-for w, key in (("ant", "pbg_models::Ant"), ("humanoid", "pbg_models::Humanoid")):
+WORK = (("ant", "pbg_models::Ant", False), ("humanoid", "pbg_models::Humanoid", False), ("ant_f64", "pbg_models::Ant", True))
+for w, key, f64 in WORK:
+    if not glob.glob(os.path.join(src, w, "pmc_wait", "**", "*counter_collection.csv"), recursive=True):
+        continue
     r = {}
     for d in ("pmc_wait", "pmc_lds"):
         f = glob.glob(os.path.join(src, w, d, "**", "*counter_collection.csv"), recursive=True)[0]
@@ -23,7 +26,8 @@ for w, key in (("ant", "pbg_models::Ant"), ("humanoid", "pbg_models::Humanoid"))
         per = {}
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "step_kernel" in row["Kernel_Name"] and key in row["Kernel_Name"]:
+                name = row["Kernel_Name"]
+                if "step_kernel" in name and key in name and (("F64<" in name) == f64):
                     per.setdefault(row["Counter_Name"], {}).setdefault(row["Dispatch_Id"], 0.0)
                     per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
         r.update({k: statistics.median(v.values()) for k, v in per.items()})
@@ -36,5 +40,5 @@ res["source"] = ("tools/gpu_stalls.sh (python bench.py --steps 20 --warmup 2, on
                  "each); per-dispatch medians of the step kernel")
 with open(os.path.join(REPO, "profiles", f"{rnd}_stalls_summary.json"), "w") as f:
     json.dump(res, f, indent=1)
-for w in ("ant", "humanoid"):
+for w in (w for w, _, _ in WORK if w in res):
     print(w, {k: round(v, 3) for k, v in res[w].items() if k.startswith(("frac", "lds"))})
