@@ -992,8 +992,24 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
   // kb + 4) of each branch's base part (the sweeps' base dot products are sliced)
   // (and its own branch part, zero in the lanes of the other branches: no owner test in
   // the sweeps)
+  // Float64 (OWN): 48 replicated doubles (96 registers) would live through the sweeps; there each
+  // lane keeps only its own branch's m_eff / targets / impulses and the owner's impulse change
+  // reaches the quad by a DPP broadcast (the same arithmetic on the same values: same results)
+  constexpr bool OWN = sizeof(Sc) == 8;
   Sc BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
   Sc Byb[4][NLB_][NDB];
+  Sc Om[NLB_], Orm[NLB_], Otl[NLB_], Oth[NLB_], Olo[NLB_], Ohi[NLB_];
+  if constexpr (OWN) {
+    static_for<0, NLIMB>([&](auto l_c) {
+      constexpr int li = decltype(l_c)::value;
+      Om[li] = Lm[li];
+      Orm[li] = Lm[li] > 0.f ? fast_rcp(Lm[li]) : 0.f;
+      Otl[li] = Ltl[li];
+      Oth[li] = Lth[li];
+      Olo[li] = 0.f;
+      Ohi[li] = 0.f;
+    });
+  }
   static_for<0, 4>([&](auto k_c) {
     constexpr int kk = decltype(k_c)::value;
     static_for<0, NLIMB>([&](auto l_c) {
@@ -1005,6 +1021,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
       for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
       BY[kk][li][0] = kb == 0 ? b6[0] : (kb == 1 ? b6[1] : (kb == 2 ? b6[2] : b6[3]));
       BY[kk][li][1] = kb == 0 ? b6[4] : (kb == 1 ? b6[5] : 0.f);
+      if constexpr (OWN) return;
       Bm[kk][li] = quad_bcast<kk>(Lm[li]);
       Brm[kk][li] = Bm[kk][li] > 0.f ? fast_rcp(Bm[kk][li]) : 0.f;  // off the sweeps' dependency chain
       Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
@@ -1126,16 +1143,28 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
           if constexpr (T::lim_nz(li, a)) part += Byb[kk][li][a] * ub[a];
         });
         const Sc yu = quad_sum(part);
-        const Sc meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
-        const Sc nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
-        const Sc dlo = nlo - llo;
-        // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
-        const Sc yu2 = yu + dlo * Brm[kk][li];  // Brm = 0 when meff = 0
-        const Sc nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
-        const Sc dhi = nhi - lhi;
-        Blo[kk][li] = nlo;
-        Bhi[kk][li] = nhi;
-        const Sc dl = dlo - dhi;
+        Sc dl;
+        if constexpr (OWN) {  // every lane runs its own row li; lane kk's result is the one kept
+          const Sc meff = Om[li], llo = Olo[li], lhi = Ohi[li];
+          const Sc nlo = clampf(llo + meff * (Otl[li] - yu), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+          const Sc dlo = nlo - llo;
+          const Sc yu2 = yu + dlo * Orm[li];
+          const Sc nhi = clampf(lhi + meff * (Oth[li] + yu2), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+          const Sc dhi = nhi - lhi;
+          if (kb == kk) { Olo[li] = nlo; Ohi[li] = nhi; }
+          dl = quad_bcast<kk>(dlo - dhi);
+        } else {
+          const Sc meff = Bm[kk][li], llo = Blo[kk][li], lhi = Bhi[kk][li];
+          const Sc nlo = clampf(llo + meff * (Btl[kk][li] - yu), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+          const Sc dlo = nlo - llo;
+          // upper row sees u after the lower update: (-y).u' = -(yu + dlo / meff)
+          const Sc yu2 = yu + dlo * Brm[kk][li];  // Brm = 0 when meff = 0
+          const Sc nhi = clampf(lhi + meff * (Bth[kk][li] + yu2), 0.f, (Sc)PBG_LIMIT_MAX_IMPULSE);
+          const Sc dhi = nhi - lhi;
+          Blo[kk][li] = nlo;
+          Bhi[kk][li] = nhi;
+          dl = dlo - dhi;
+        }
         uBs[0] += BY[kk][li][0] * dl;
         uBs[1] += BY[kk][li][1] * dl;
         static_for<0, NDB>([&](auto a_c) {
