@@ -391,7 +391,7 @@ def main():
 
         def make_env(env_id, n, dev, seed, env_offset, autoreset, precision=None):
             precision = precision or args.precision
-            lanes = args.gang_lanes if env_id.startswith("Humanoid") and precision == 32 else -1
+            lanes = args.gang_lanes if env_id.startswith("Humanoid") else -1
             return VecEnv(env_id, n, device=dev, seed=seed, env_offset=env_offset, autoreset=autoreset,
                           gang_lanes=lanes, precision=precision)
 

@@ -51,7 +51,7 @@ namespace pbg {
 // tables (32 KB) and 8 env regions (13.8 KB each) fill 142 KB of the CU's 160 KB; 16 envs would
 // not fit, and one-wave workgroups (87 KB: one per CU) left three SIMDs of each CU idle
 // (4.72 -> 3.05 ms per step at 4,096 envs, A/B)
-template <class R>
+template <class R, int T = 16>
 constexpr int gang_block();  // (after the layout: the float64 regions decide it)
 
 // bound_ctrl set: every permutation used here reads a valid lane, and with it the
@@ -139,10 +139,11 @@ PBG_DEV uint32_t gang_sum_u32(uint32_t x) {
 // stays for the others, and for these under pbg_create_debug(gang_lanes = 16).
 template <class R>
 constexpr bool gang32_ok() { return FP<R>::NF > 0 && R::NDOF >= 20 && R::NS <= 128; }
-// waves per SIMD the kernel's register budget is compiled for (__launch_bounds__): 32-lane gangs
-// exist to put two waves on a SIMD
-template <int T>
-constexpr int gang_waves_per_simd() { return T >= 32 ? 2 : 1; }
+// waves per SIMD the kernel's register budget is compiled for (__launch_bounds__): float32 32-lane
+// gangs exist to put two waves on a SIMD; float64 ones (the Humanoid family) to put a wave on each
+// of the four SIMDs of a CU whose LDS holds only 8 float64 envs
+template <class R, int T>
+constexpr int gang_waves_per_simd() { return T >= 32 && sizeof(real_t<R>) == 4 ? 2 : 1; }
 
 // ------------------------------------------------------------------ constant tables
 template <class R>
@@ -525,13 +526,15 @@ struct GangTabs {
   static PBG_DEV Tab& tab(const lds_float* p) { return *(Tab*)p; }
   static PBG_DEV Dyn& dyn(const lds_float* p) { return *(Dyn*)(p + TAB_WORDS); }
 };
-// Lanes per workgroup: 4 waves of 16-lane gangs; the float64 path (F64<R>: every region word 8
-// bytes) takes 2 waves when 16 envs' fixed words and four contacts each would not fit one CU's LDS
-template <class R>
+// Lanes per workgroup: 4 waves of T-lane gangs; the float64 path (F64<R>: every region word 8
+// bytes) takes 2 waves of 16-lane gangs when 16 envs' fixed words and four contacts each would not
+// fit one CU's LDS (its 32-lane gangs keep 4 waves: 8 envs)
+template <class R, int T>
 constexpr int gang_block() {
-  using G = Gang<R, 16>;
-  constexpr long need = 4L * GangTabs<R>::WORDS + 16L * (long)sizeof(real_t<R>) * (G::FIXED + 4L * G::PERC);
-  return sizeof(real_t<R>) == 8 && need > 163840L ? PBG_GANG_BLOCK / 2 : PBG_GANG_BLOCK;
+  using G = Gang<R, T>;
+  constexpr long need =
+      4L * GangTabs<R>::WORDS + (long)(PBG_GANG_BLOCK / T) * (long)sizeof(real_t<R>) * (G::FIXED + 4L * G::PERC);
+  return sizeof(real_t<R>) == 8 && T == 16 && need > 163840L ? PBG_GANG_BLOCK / 2 : PBG_GANG_BLOCK;
 }
 #define PBG_GANG_SYNC                                    \
   {                                                      \
@@ -2134,14 +2137,14 @@ PBG_DEV void gang_store(const State<R>& s, const float (&obs)[R::OBS], real_t<R>
 }
 
 template <class R, int T, bool DIST>
-__global__ __launch_bounds__(gang_block<R>(), gang_waves_per_simd<T>()) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
+__global__ __launch_bounds__((gang_block<R, T>()), (gang_waves_per_simd<R, T>())) void gang_step_kernel(Buffers B, StepIO io, float* __restrict__ scratch, int cap,
                                                        int env_words) {
   using Sc = real_t<R>;
   using LW = lds_t<Sc>;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   using G = Gang<R, T>;
   using TT = GangTabs<R>;
-  constexpr int BLK = gang_block<R>();
+  constexpr int BLK = gang_block<R, T>();
   constexpr int EPB = BLK / T;  // envs per workgroup
   lds_float* lds = (lds_float*)lds_dyn;  // the model tables (4-byte words), then the env regions
   {

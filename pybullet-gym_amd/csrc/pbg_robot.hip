@@ -80,12 +80,13 @@ static bool launch_team(const Buffers& B, const StepIO& io, float* scratch, cons
 }
 
 // robots and widths with a gang kernel: walkers (the cube robot on the front path); 32-lane gangs for
-// the Humanoid family in float32; float64 (F64<R>): 16 lanes, Atlas-sized models excluded
+// the Humanoid family (float64: its default width, a wave on every SIMD of a CU whose LDS holds 8
+// float64 envs); float64 (F64<R>): Atlas-sized models excluded
 template <class RR, int T>
 constexpr bool gang_ok() {
   constexpr bool f64 = sizeof(real_t<RR>) == 8;
-  return (RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) &&
-         (T == 16 || (gang32_ok<RR>() && !f64)) && !(f64 && gang_big<RR>());
+  return (RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>()) &&
+         !(f64 && gang_big<RR>());
 }
 // Gang geometry (pbg_gang.hip): T = 16 or 32 lanes per env, 256 / T envs per 4-wave workgroup;
 // the per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
@@ -95,12 +96,23 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
   if constexpr (gang_ok<RR, T>()) {
     using G = Gang<RR, T>;
     constexpr long WB = (long)sizeof(real_t<RR>);  // env-region word: 4 bytes, or 8 on the float64 path
-    constexpr int EPB = gang_block<RR>() / T;  // envs per workgroup
+    constexpr int EPB = gang_block<RR, T>() / T;  // envs per workgroup
     // the layout's floor (fixed words + the kinematic area, no LDS contact) must fit one CU's LDS
     static_assert(4L * GangTabs<RR>::WORDS + WB * EPB * ((G::FIXED + G::MIN_CONTACT_WORDS + 3L) & ~3L) <= 163840L,
                   "gang env regions exceed the CU's LDS");
+    // every env region 16-byte (front path: b128 LDS loads) or 8-byte (b64 row loads) aligned:
+    // round the region up, and give back a contact when the rounding crosses the budget
+    auto region = [&](int c) {
+      const int w = G::FIXED + (c * G::PERC > G::MIN_CONTACT_WORDS ? c * G::PERC : G::MIN_CONTACT_WORDS);
+      return (w + G::REGION_ALIGN - 1) & ~(G::REGION_ALIGN - 1);
+    };
     const int wgs = (n_envs + EPB - 1) / EPB;
-    const int wpc = (wgs + cus - 1) / cus;
+    int wpc = (wgs + cus - 1) / cus;
+    // the workgroups a CU can hold at all (no LDS contact): planning the contact capacity for more
+    // resident workgroups than fit would shrink it for nothing (round 5: float64 HalfCheetah and
+    // Humanoid, Atlas -- one workgroup per CU, planned for two, had no LDS contact)
+    const long fit0 = 163840L / (4L * (long)GangTabs<RR>::WORDS + WB * EPB * (long)region(0));
+    if (wpc > fit0) wpc = fit0 > 0 ? (int)fit0 : 1;
     // signed: with many workgroups per CU the share can be smaller than the model tables
     long budget = 163840L / (long)(wpc > 0 ? wpc : 1) - 4L * (long)GangTabs<RR>::WORDS;
     if (budget < 0) budget = 0;
@@ -108,12 +120,6 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     int cap = (int)(words / G::PERC);
     if (cap > G::MAXC) cap = G::MAXC;
     if (cap < 0) cap = 0;
-    // every env region 16-byte (front path: b128 LDS loads) or 8-byte (b64 row loads) aligned:
-    // round the region up, and give back a contact when the rounding crosses the budget
-    auto region = [&](int c) {
-      const int w = G::FIXED + (c * G::PERC > G::MIN_CONTACT_WORDS ? c * G::PERC : G::MIN_CONTACT_WORDS);
-      return (w + G::REGION_ALIGN - 1) & ~(G::REGION_ALIGN - 1);
-    };
     while (cap > 0 && (long)region(cap) * EPB * WB > budget) cap--;
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
@@ -123,7 +129,7 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     // pbg_create_debug (32-lane gangs, the cube robot and float64 have no replicated-dynamics variant)
     if ((g->force_dist == 0 || g->force_dist == 1) && REPL) g->gang_dist = g->force_dist;
     g->team = T;
-    g->block = gang_block<RR>();
+    g->block = gang_block<RR, T>();
     g->lds_rows = cap;
     g->env_words = region(cap);
     g->lds_bytes = 4 * (size_t)GangTabs<RR>::WORDS + (size_t)WB * (size_t)EPB * (size_t)g->env_words;
@@ -154,7 +160,7 @@ static int plan_gang(int n_envs, int cus, Geometry* g, int lanes) {
 template <class RR, int T>
 static bool launch_gang_t(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if constexpr (gang_ok<RR, T>()) {
-    const dim3 grid(blocks(B.n, gang_block<RR>() / T)), blk(gang_block<RR>());
+    const dim3 grid(blocks(B.n, gang_block<RR, T>() / T)), blk(gang_block<RR, T>());
     if constexpr (T == 16 && !RR::harder && sizeof(real_t<RR>) == 4) {
       if (!g.gang_dist) {
         hipLaunchKernelGGL((gang_step_kernel<RR, T, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows,
@@ -298,13 +304,21 @@ int PBG_FN(launch_pack_)(int n, const double* in, double* out, hipStream_t s) {
 int PBG_FN(plan64_)(int n_envs, int cus, int mode, Geometry* g) {
   if (team64_ok<R64>() && mode == 1) return PBG_FN(plan_team64_)(n_envs, cus, g);
   if constexpr (gang_ok<R64, 16>()) {
-    if (mode != 0) return plan_gang_t<R64, 16>(n_envs, cus, g);
+    if (mode != 0) {
+      // the Humanoid family's default is 32 lanes: its float64 regions let a CU hold 8 envs, which
+      // 32-lane gangs spread over all four SIMDs (0.493 -> 0.471 ms at 4,096 Humanoid envs)
+      if (g->gang_lanes == 32 || (g->gang_lanes < 0 && gang_ok<R64, 32>())) {
+        if constexpr (gang_ok<R64, 32>()) return plan_gang_t<R64, 32>(n_envs, cus, g);
+        else return (int)hipErrorInvalidValue;
+      }
+      return plan_gang_t<R64, 16>(n_envs, cus, g);
+    }
   }
   return plan_lane<R64>(n_envs, cus, g);
 }
 int PBG_FN(launch_step64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if (PBG_FN(launch_team64_)(B, io, scratch, g, s)) return (int)hipGetLastError();
-  if (g.team == 16 && launch_gang_t<R64, 16>(B, io, scratch, g, s)) return (int)hipGetLastError();
+  if (launch_gang<R64>(B, io, scratch, g, s)) return (int)hipGetLastError();
   return launch_lane<R64>(B, io, scratch, g, s);
 }
 int PBG_FN(launch_reset64_)(const Buffers& B, const ResetIO& io, hipStream_t s) {

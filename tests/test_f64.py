@@ -258,9 +258,9 @@ def test_f64_atlas_is_refused():
 
 # ------------------------------------------------------------------ float64 kernel variants
 # The float64 walkers run the kernels of the float32 path instantiated on F64<R>: Ant the quad
-# kernel (pbg_team.hip, 4 lanes per env), the other walkers (AntMuJoCo included: its float64 quad
-# instance is miscompiled, pbg_robot.hip) the 16-lane gang kernel (pbg_gang.hip; kernel=2 puts Ant
-# on it too); kernel=0 selects the float64 lane-per-env kernel, which stays the
+# kernel (pbg_team.hip, 4 lanes per env), the Humanoid family 32-lane gangs, the other walkers
+# (AntMuJoCo included: its float64 quad instance is miscompiled, pbg_robot.hip) the 16-lane gang
+# kernel (pbg_gang.hip; kernel=2 puts Ant on it too, gang_lanes=16 the Humanoids); kernel=0 selects the float64 lane-per-env kernel, which stays the
 # pendulums' path and the quad / gang kernels' cross-check.
 @pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HopperPyBulletEnv-v0",
                                     "HumanoidFlagrunHarderPyBulletEnv-v0"])
@@ -271,14 +271,15 @@ def test_f64_lane_kernel_teacher_forced(env_id):
 
 @pytest.mark.parametrize("env_id,kernel,lanes", [
     ("AntPyBulletEnv-v0", None, 4), ("AntMuJoCoEnv-v0", None, 16), ("AntPyBulletEnv-v0", 2, 16),
-    ("HumanoidPyBulletEnv-v0", None, 16), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
-    ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 16),
-    ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 16)])
+    ("HumanoidPyBulletEnv-v0", "g16", 16), ("HumanoidFlagrunHarderPyBulletEnv-v0", "g16", 16),
+    ("HumanoidPyBulletEnv-v0", None, 32), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
+    ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 32),
+    ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 32), ("HumanoidMuJoCoEnv-v0", None, 32)])
 def test_f64_quad_and_gang_match_f64_lane(env_id, kernel, lanes):
     """Float64 quad / gang vs float64 lane kernel from the same states every step: the same contact
     sets and the state within 1e-9 (different summation orders in float64)."""
     n = 256
-    kw = {} if kernel is None else {"kernel": kernel}
+    kw = {} if kernel is None else ({"gang_lanes": 16} if kernel == "g16" else {"kernel": kernel})
     g = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, **kw)
     ln = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, kernel=0)
     assert g.info.lanes_per_env == lanes and ln.info.lanes_per_env == 1
@@ -297,7 +298,7 @@ def test_f64_quad_and_gang_match_f64_lane(env_id, kernel, lanes):
         same_n += int(same.sum())
         np.testing.assert_array_equal(g.ncontact.cpu().numpy()[same], ln.ncontact.cpu().numpy()[same])
     e = np.concatenate(errs)
-    rec = dict(test=f"f64_{'quad' if lanes == 4 else 'gang'}_vs_lane[{env_id}]", same_frac=same_n / (30 * n), max_rel=float(e.max()),
+    rec = dict(test=f"f64_{'quad' if lanes == 4 else ('gang32' if lanes == 32 else 'gang')}_vs_lane[{env_id}]", same_frac=same_n / (30 * n), max_rel=float(e.max()),
                share_within_1e_9=float((e <= STATE_REL64).mean()))
     _report(rec)
     assert rec["same_frac"] >= 1 - LOOSE_FRAC64 and rec["share_within_1e_9"] >= SHARE64 and rec["max_rel"] <= HARD_MAX64, rec
@@ -347,7 +348,7 @@ def test_f64_gang_workspace_contacts_bitwise_equal_lds_contacts():
 def test_f64_gang_determinism_and_offset_invariance():
     def run(n, off):
         env = VecEnv("HumanoidPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True, precision=64)
-        assert env.info.lanes_per_env == 16
+        assert env.info.lanes_per_env == 32
         env.reset()
         g = torch.Generator(device="cuda").manual_seed(0)
         acts = torch.rand((30, 97, 17), device="cuda", generator=g) * 2 - 1

@@ -913,13 +913,16 @@ def test_gang_kernel_determinism_and_offset_invariance(env_id, lanes):
     np.testing.assert_array_equal(a[:, 41:], run(56, 41))
 
 
-def test_gang_plan_many_envs_spills_contacts_to_workspace():
-    """Humanoid at 131,072 envs (32 workgroups per CU): the per-workgroup LDS share is smaller
-    than the model tables plus one contact, so every contact lives in the device workspace
-    and the workgroup still fits the 160 KiB LDS (no unsigned underflow in the plan)."""
+def test_gang_plan_many_envs_plans_for_resident_workgroups():
+    """Humanoid at 131,072 envs (32 workgroups per CU): a CU holds one Humanoid workgroup at a
+    time, so the plan sizes the LDS contact capacity for one resident workgroup -- the capacity
+    of the 4,096-env plan -- instead of a 1/32 share that would hold no contact (round 5); the
+    workgroup fits the 160 KiB LDS (no unsigned underflow in the plan) and the step runs."""
+    small = VecEnv("HumanoidPyBulletEnv-v0", 4096, seed=1)
     env = VecEnv("HumanoidPyBulletEnv-v0", 131072, seed=1)
-    assert env.info.lds_rows == 0, env.info.lds_rows
+    assert env.info.lds_rows == small.info.lds_rows > 0, (env.info.lds_rows, small.info.lds_rows)
     assert 0 < env.info.lds_bytes <= 160 * 1024
+    small.close()
     env.reset()
     res = env.step(sample_actions(17, 131072, 1)[0])
     assert torch.isfinite(res.obs).all()

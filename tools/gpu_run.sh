@@ -15,6 +15,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 rc=0
+nb=0
 for S in "$@"; do
   name=${S%%:*}; arg=${S#*:}; [ "$arg" = "$S" ] && arg=""
   echo "== $S $(date +%T)"
@@ -31,8 +32,8 @@ for S in "$@"; do
     smoke)
       timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1; rc=$?; tail -2 $OUT/smoke.txt;;
     bench)
-      timeout -k 10 400 python bench.py ${arg//,/ } > $OUT/bench_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40).json \
-        2>> $OUT/bench.err; rc=$?; tail -c 400 $OUT/bench_*.json | tail -3;;
+      nb=$((nb + 1)); BF=$OUT/bench_${nb}_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40).json
+      timeout -k 10 400 python bench.py ${arg//,/ } > $BF 2>> $OUT/bench.err; rc=$?; tail -c 400 $BF;;
     prof)
       bash tools/gpu_bench_prof.sh ${TAG}_prof --steps 1000 --warmup 50; rc=$?;;
     stalls)
