@@ -620,6 +620,13 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
   const Sc dt = P.dt;
   const Sc g = P.gravity;
   const int kb = L.k;
+  // contact detection (float32: where the rows are built; float64: right after phase A, so the
+  // branch's kinematic records die before the mass matrix is built)
+  int n0 = 0, ci = 0, nc = 0;
+  uint32_t act = 0;
+  Sc sdist[T::NSB > 0 ? T::NSB : 1];
+  f3 sP[T::NSB > 0 ? T::NSB : 1];
+  constexpr bool OWN = sizeof(Sc) == 8;  // the float64 ordering and limit-row layout (below)
 
   // --- phase A: branch kinematics, velocities, bias accelerations; composites of the
   // branch's dof-owning links and the branch total (all about O = base COM)
@@ -752,6 +759,38 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     tm += m; tF += f; tN += n;
 #pragma unroll
     for (int c = 0; c < 6; c++) tJ.a[c] += Iw.a[c];
+  }
+
+  // this branch's active slots, then their contact indices (exclusive quad prefix)
+  auto detect_branch = [&]() {
+    act = 0;
+    static_for<0, T::NSB>([&](auto sl_c) {
+      constexpr int sl = decltype(sl_c)::value;
+      constexpr int li = R::slot_link[T::NS0 + sl];
+      const f3 cc = k.x[li] + mulc(k.Rm[li], pk3<T::SPT, sl>(L));
+      const Sc rad = pk<T::SRAD, sl>(L);
+      sdist[sl] = cc.z - rad;
+      sP[sl] = mk3<Sc>(cc.x, cc.y, cc.z - rad);
+      act |= (sdist[sl] < (Sc)PBG_CONTACT_THRESHOLD ? 1u : 0u) << sl;
+    });
+    const int cnt = __builtin_popcount(act);
+    const int c0 = quad_bcast_i<0>(cnt), c1 = quad_bcast_i<1>(cnt), c2 = quad_bcast_i<2>(cnt), c3 = quad_bcast_i<3>(cnt);
+    ci = n0 + (kb > 0 ? c0 : 0) + (kb > 1 ? c1 : 0) + (kb > 2 ? c2 : 0);
+    nc = n0 + c0 + c1 + c2 + c3;
+    slot_bits = act;
+  };
+  if constexpr (OWN) {
+    n0 = 0;
+    base_bits = 0;
+    static_for<0, T::NS0>([&](auto sl_c) {
+      constexpr int sl = decltype(sl_c)::value;
+      const f3 cc = O + mulc(Rb, (Sc)R::slot_point[sl][0], (Sc)R::slot_point[sl][1], (Sc)R::slot_point[sl][2]);
+      if (cc.z - (Sc)R::slot_radius[sl] < (Sc)PBG_CONTACT_THRESHOLD) {
+        base_bits |= 1u << sl;
+        n0++;
+      }
+    });
+    detect_branch();
   }
 
   STAMP(0)
@@ -939,55 +978,6 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     return c;
   }();
   constexpr int NLB_ = NLIMB > 0 ? NLIMB : 1;
-  Sc Lyb[NLB_][NDB], Lm[NLB_], Ltl[NLB_], Lth[NLB_], LyB[NLB_][6];
-  static_for<0, NDB>([&](auto j_c) {
-    constexpr int j = decltype(j_c)::value;
-    if constexpr (R::dof_limited[j]) {
-      constexpr int li = [] {
-        int c = 0;
-        for (int jj = 0; jj < j; jj++) c += R::dof_limited[jj];
-        return c;
-      }();
-      constexpr int gd = T::lg(j);
-      Sc y[NDB];
-      static_for<0, NDB>([&](auto a_c) {
-        constexpr int a = decltype(a_c)::value;
-        if constexpr (a < gd || !T::coupled(a, gd)) {
-          y[a] = 0.f;
-        } else {
-          Sc t = a == gd ? 1.f : 0.f;
-          static_for<gd, a>([&](auto k_c) {
-            constexpr int kk = decltype(k_c)::value;
-            if constexpr (T::coupled(a, kk) && T::coupled(kk, gd)) t -= Lbr[a][kk] * y[kk];
-          });
-          y[a] = t * Ld[a];
-        }
-      });
-      Sc t6[6];
-#pragma unroll
-      for (int gg = 0; gg < 6; gg++) {
-        Sc c = 0.f;
-#pragma unroll
-        for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * y[b];
-        t6[gg] = -c;
-      }
-      fwd6(Lbb, Ldb, t6);
-      Sc D2 = 0.f;
-#pragma unroll
-      for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
-#pragma unroll
-      for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; }
-      const Sc meff = D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f;
-      const Sc plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
-      Ltl[li] = pos_target(plo, P.k_limit, P.k_sep);
-      Lth[li] = pos_target(phi, P.k_limit, P.k_sep);
-      Lm[li] = meff;
-#pragma unroll
-      for (int a = 0; a < NDB; a++) Lyb[li][a] = y[a];
-#pragma unroll
-      for (int gg = 0; gg < 6; gg++) LyB[li][gg] = t6[gg];
-    }
-  });
   // every lane needs each branch's m_eff and targets, and its own slice (components kb,
   // kb + 4) of each branch's base part (the sweeps' base dot products are sliced)
   // (and its own branch part, zero in the lanes of the other branches: no owner test in
@@ -995,89 +985,151 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
   // Float64 (OWN): 48 replicated doubles (96 registers) would live through the sweeps; there each
   // lane keeps only its own branch's m_eff / targets / impulses and the owner's impulse change
   // reaches the quad by a DPP broadcast (the same arithmetic on the same values: same results)
-  constexpr bool OWN = sizeof(Sc) == 8;
   Sc BY[4][NLB_][2], Bm[4][NLB_], Brm[4][NLB_], Btl[4][NLB_], Bth[4][NLB_], Blo[4][NLB_], Bhi[4][NLB_];
   Sc Byb[4][NLB_][NDB];
   Sc Om[NLB_], Orm[NLB_], Otl[NLB_], Oth[NLB_], Olo[NLB_], Ohi[NLB_];
-  if constexpr (OWN) {
-    static_for<0, NLIMB>([&](auto l_c) {
-      constexpr int li = decltype(l_c)::value;
-      Om[li] = Lm[li];
-      Orm[li] = Lm[li] > 0.f ? fast_rcp(Lm[li]) : 0.f;
-      Otl[li] = Ltl[li];
-      Oth[li] = Lth[li];
-      Olo[li] = 0.f;
-      Ohi[li] = 0.f;
+  // the limit rows (float64: built after the contact rows -- see below)
+  auto lim_setup = [&]() {
+    Sc Lyb[NLB_][NDB], Lm[NLB_], Ltl[NLB_], Lth[NLB_], LyB[NLB_][6];
+    static_for<0, NDB>([&](auto j_c) {
+      constexpr int j = decltype(j_c)::value;
+      if constexpr (R::dof_limited[j]) {
+        constexpr int li = [] {
+          int c = 0;
+          for (int jj = 0; jj < j; jj++) c += R::dof_limited[jj];
+          return c;
+        }();
+        constexpr int gd = T::lg(j);
+        Sc y[NDB];
+        static_for<0, NDB>([&](auto a_c) {
+          constexpr int a = decltype(a_c)::value;
+          if constexpr (a < gd || !T::coupled(a, gd)) {
+            y[a] = 0.f;
+          } else {
+            Sc t = a == gd ? 1.f : 0.f;
+            static_for<gd, a>([&](auto k_c) {
+              constexpr int kk = decltype(k_c)::value;
+              if constexpr (T::coupled(a, kk) && T::coupled(kk, gd)) t -= Lbr[a][kk] * y[kk];
+            });
+            y[a] = t * Ld[a];
+          }
+        });
+        Sc t6[6];
+  #pragma unroll
+        for (int gg = 0; gg < 6; gg++) {
+          Sc c = 0.f;
+  #pragma unroll
+          for (int b = 0; b < NDB; b++) c += Lgb[gg][b] * y[b];
+          t6[gg] = -c;
+        }
+        fwd6(Lbb, Ldb, t6);
+        Sc D2 = 0.f;
+  #pragma unroll
+        for (int a = 0; a < NDB; a++) { D2 += y[a] * y[a]; }
+  #pragma unroll
+        for (int gg = 0; gg < 6; gg++) { D2 += t6[gg] * t6[gg]; }
+        const Sc meff = D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f;
+        const Sc plo = s.q[j] - pk<T::DLO, j>(L), phi = pk<T::DHI, j>(L) - s.q[j];
+        Ltl[li] = pos_target(plo, P.k_limit, P.k_sep);
+        Lth[li] = pos_target(phi, P.k_limit, P.k_sep);
+        Lm[li] = meff;
+  #pragma unroll
+        for (int a = 0; a < NDB; a++) Lyb[li][a] = y[a];
+  #pragma unroll
+        for (int gg = 0; gg < 6; gg++) LyB[li][gg] = t6[gg];
+      }
     });
-  }
-  static_for<0, 4>([&](auto k_c) {
-    constexpr int kk = decltype(k_c)::value;
-    static_for<0, NLIMB>([&](auto l_c) {
-      constexpr int li = decltype(l_c)::value;
-#pragma unroll
-      for (int a = 0; a < NDB; a++) Byb[kk][li][a] = kb == kk ? Lyb[li][a] : 0.f;
-      Sc b6[6];
-#pragma unroll
-      for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
-      BY[kk][li][0] = kb == 0 ? b6[0] : (kb == 1 ? b6[1] : (kb == 2 ? b6[2] : b6[3]));
-      BY[kk][li][1] = kb == 0 ? b6[4] : (kb == 1 ? b6[5] : 0.f);
-      if constexpr (OWN) return;
-      Bm[kk][li] = quad_bcast<kk>(Lm[li]);
-      Brm[kk][li] = Bm[kk][li] > 0.f ? fast_rcp(Bm[kk][li]) : 0.f;  // off the sweeps' dependency chain
-      Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
-      Bth[kk][li] = quad_bcast<kk>(Lth[li]);
-      Blo[kk][li] = 0.f;
-      Bhi[kk][li] = 0.f;
+    if constexpr (OWN) {
+      static_for<0, NLIMB>([&](auto l_c) {
+        constexpr int li = decltype(l_c)::value;
+        Om[li] = Lm[li];
+        Orm[li] = Lm[li] > 0.f ? fast_rcp(Lm[li]) : 0.f;
+        Otl[li] = Ltl[li];
+        Oth[li] = Lth[li];
+        Olo[li] = 0.f;
+        Ohi[li] = 0.f;
+      });
+    }
+    static_for<0, 4>([&](auto k_c) {
+      constexpr int kk = decltype(k_c)::value;
+      static_for<0, NLIMB>([&](auto l_c) {
+        constexpr int li = decltype(l_c)::value;
+  #pragma unroll
+        for (int a = 0; a < NDB; a++) Byb[kk][li][a] = kb == kk ? Lyb[li][a] : 0.f;
+        Sc b6[6];
+  #pragma unroll
+        for (int gg = 0; gg < 6; gg++) b6[gg] = quad_bcast<kk>(LyB[li][gg]);
+        BY[kk][li][0] = kb == 0 ? b6[0] : (kb == 1 ? b6[1] : (kb == 2 ? b6[2] : b6[3]));
+        BY[kk][li][1] = kb == 0 ? b6[4] : (kb == 1 ? b6[5] : 0.f);
+        if constexpr (OWN) return;
+        Bm[kk][li] = quad_bcast<kk>(Lm[li]);
+        Brm[kk][li] = Bm[kk][li] > 0.f ? fast_rcp(Bm[kk][li]) : 0.f;  // off the sweeps' dependency chain
+        Btl[kk][li] = quad_bcast<kk>(Ltl[li]);
+        Bth[kk][li] = quad_bcast<kk>(Lth[li]);
+        Blo[kk][li] = 0.f;
+        Bhi[kk][li] = 0.f;
+      });
     });
-  });
+  };
+  if constexpr (!OWN) lim_setup();
 
   STAMP(3)
   // --- contact rows: base slots (replicated), then each branch's slots (owner lane) ------
-  int n0 = 0;
-  base_bits = 0;
-  static_for<0, T::NS0>([&](auto sl_c) {
-    constexpr int sl = decltype(sl_c)::value;
-    const f3 cc = O + mulc(Rb, (Sc)R::slot_point[sl][0], (Sc)R::slot_point[sl][1], (Sc)R::slot_point[sl][2]);
-    const Sc rad = (Sc)R::slot_radius[sl];
-    const Sc dist = cc.z - rad;
-    if (!(dist < (Sc)PBG_CONTACT_THRESHOLD)) return;
-    base_bits |= 1u << sl;
-    const f3 rP = mk3<Sc>(cc.x, cc.y, cc.z - rad) - O;
+  if constexpr (!OWN) {
+    n0 = 0;
+    base_bits = 0;
+    static_for<0, T::NS0>([&](auto sl_c) {
+      constexpr int sl = decltype(sl_c)::value;
+      const f3 cc = O + mulc(Rb, (Sc)R::slot_point[sl][0], (Sc)R::slot_point[sl][1], (Sc)R::slot_point[sl][2]);
+      const Sc rad = (Sc)R::slot_radius[sl];
+      const Sc dist = cc.z - rad;
+      if (!(dist < (Sc)PBG_CONTACT_THRESHOLD)) return;
+      base_bits |= 1u << sl;
+      const f3 rP = mk3<Sc>(cc.x, cc.y, cc.z - rad) - O;
+  #pragma unroll
+      for (int dir = 0; dir < 3; dir++) {
+        const f3 nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
+        const f3 mm = cross3(rP, nd);
+        Sc y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+        fwd6(Lbb, Ldb, y6);
+        Sc D2 = 0.f;
+  #pragma unroll
+        for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
+        Sc z[NDB];
+  #pragma unroll
+        for (int a = 0; a < NDB; a++) z[a] = 0.f;
+        rw.put(3 * n0 + dir, -1, z, y6, D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f,
+               dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (Sc)R::slot_mu[sl]);
+      }
+      n0++;
+    });
+    detect_branch();
+  } else {  // float64: the detection ran after phase A; the base rows here
+    static_for<0, T::NS0>([&](auto sl_c) {
+      constexpr int sl = decltype(sl_c)::value;
+      if (!((base_bits >> sl) & 1u)) return;
+      const f3 cc = O + mulc(Rb, (Sc)R::slot_point[sl][0], (Sc)R::slot_point[sl][1], (Sc)R::slot_point[sl][2]);
+      const Sc rad = (Sc)R::slot_radius[sl];
+      const Sc dist = cc.z - rad;
+      const f3 rP = mk3<Sc>(cc.x, cc.y, cc.z - rad) - O;
+      const int r0 = __builtin_popcount(base_bits & ((1u << sl) - 1u));
 #pragma unroll
-    for (int dir = 0; dir < 3; dir++) {
-      const f3 nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
-      const f3 mm = cross3(rP, nd);
-      Sc y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
-      fwd6(Lbb, Ldb, y6);
-      Sc D2 = 0.f;
+      for (int dir = 0; dir < 3; dir++) {
+        const f3 nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
+        const f3 mm = cross3(rP, nd);
+        Sc y6[6] = {nd.x, nd.y, nd.z, mm.x, mm.y, mm.z};
+        fwd6(Lbb, Ldb, y6);
+        Sc D2 = 0.f;
 #pragma unroll
-      for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
-      Sc z[NDB];
+        for (int gg = 0; gg < 6; gg++) { D2 += y6[gg] * y6[gg]; }
+        Sc z[NDB];
 #pragma unroll
-      for (int a = 0; a < NDB; a++) z[a] = 0.f;
-      rw.put(3 * n0 + dir, -1, z, y6, D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f,
-             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (Sc)R::slot_mu[sl]);
-    }
-    n0++;
-  });
-  // this branch's active slots, then their contact indices (exclusive quad prefix)
-  uint32_t act = 0;
-  Sc sdist[T::NSB > 0 ? T::NSB : 1];
-  f3 sP[T::NSB > 0 ? T::NSB : 1];
-  static_for<0, T::NSB>([&](auto sl_c) {
-    constexpr int sl = decltype(sl_c)::value;
-    constexpr int li = R::slot_link[T::NS0 + sl];
-    const f3 cc = k.x[li] + mulc(k.Rm[li], pk3<T::SPT, sl>(L));
-    const Sc rad = pk<T::SRAD, sl>(L);
-    sdist[sl] = cc.z - rad;
-    sP[sl] = mk3<Sc>(cc.x, cc.y, cc.z - rad);
-    act |= (sdist[sl] < (Sc)PBG_CONTACT_THRESHOLD ? 1u : 0u) << sl;
-  });
-  const int cnt = __builtin_popcount(act);
-  const int c0 = quad_bcast_i<0>(cnt), c1 = quad_bcast_i<1>(cnt), c2 = quad_bcast_i<2>(cnt), c3 = quad_bcast_i<3>(cnt);
-  int ci = n0 + (kb > 0 ? c0 : 0) + (kb > 1 ? c1 : 0) + (kb > 2 ? c2 : 0);
-  const int nc = n0 + c0 + c1 + c2 + c3;
-  slot_bits = act;
+        for (int a = 0; a < NDB; a++) z[a] = 0.f;
+        rw.put(3 * r0 + dir, -1, z, y6, D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f,
+               dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f, (Sc)R::slot_mu[sl]);
+      }
+    });
+  }
   static_for<0, T::NSB>([&](auto sl_c) {
     constexpr int sl = decltype(sl_c)::value;
     if (!((act >> sl) & 1u)) return;
@@ -1119,6 +1171,7 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     }
     ci++;
   });
+  if constexpr (OWN) lim_setup();
   if (3 * nc > rw.cap) {  // rows in the device workspace: same-CU visibility
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
