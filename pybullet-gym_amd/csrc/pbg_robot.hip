@@ -243,10 +243,11 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
 // from the first sub-step in every env, while the LLVM IR is free of undef / poison, the same
 // source with printf calls or the trackers schedule is bit-exact against the float64 lane kernel,
 // and moving the double quad permutes from DPP to ds_bpermute does not change it (DESIGN.md
-// section 4).  The float32 kernels keep the default scheduler (their ISA is unchanged).  AntMuJoCo's
-// instance is wrong under both schedules and is not built: its float64 handle runs the gang kernel.
+// section 4).  The float32 kernels keep the default scheduler (their ISA is unchanged).  (AntMuJoCo's
+// instance was wrong under both schedules until the float64 sub-step was reordered; with the
+// current source both instances pass the float64 parity tests.)
 template <class RR>
-constexpr bool team64_ok() { return Team<RR>::ok && RR::kind == 0; }
+constexpr bool team64_ok() { return Team<RR>::ok; }
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g);
 bool PBG_FN(launch_team64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s);
 #ifdef PBG_TEAM64_TU

@@ -369,6 +369,13 @@ struct TRows {
   static constexpr int PW = NDB + 2;    // per-lane words of a row
   static constexpr int W = 4 * PW + 4;  // words per env per row (P of its 4 lanes + S)
   static constexpr int SOFF = 4 * ES * PW;  // S block within a row region
+  // float64 (PL): a lane's P record (4 doubles, 32 B) as two 16-B planes -- branch words, then the
+  // base slice -- and the S record as (m_eff, target) and (lambda, mu) planes, so every b128 access
+  // of 64 lanes strides 16 B (with 32-B records every access was a 2-way LDS bank conflict, 48 % of
+  // the float64 kernel's LDS-active cycles)
+  static constexpr bool PL = sizeof(Sc) == 8 && PW == 4;
+  static constexpr int P1OFF = 2 * 4 * ES;           // PL: the base-slice plane (words)
+  static constexpr int LAMO = PL ? 2 * ES : 2;       // lambda's word offset from the (m_eff, target) pair
   static constexpr int HEAD = 0;        // per-env words before the rows (pack staging overlaps the rows)
   static_assert(NC <= 32, "contact_sweep keeps one bit per contact in a 32-bit mask");
   static constexpr int WORDS = MR * W;  // device workspace words per env
@@ -386,8 +393,8 @@ struct TRows {
   // row offsets by a 24-bit multiply (rows < 2^24): the 32-bit v_mul_lo_u32 the compiler chose for
   // an unbounded row index is a quarter-rate instruction, two of them per normal row of the sweep
   PBG_DEV int roff(int r) const { return (int)__umul24((unsigned)r, (unsigned)(ES * W)); }
-  PBG_DEV LW* P(int r) const { return rows + roff(r) + PW * lane; }
-  PBG_DEV LW* S(int r) const { return rows + roff(r) + SOFF + 4 * (lane >> 2); }
+  PBG_DEV LW* P(int r) const { return rows + roff(r) + (PL ? 2 : PW) * lane; }
+  PBG_DEV LW* S(int r) const { return rows + roff(r) + SOFF + (PL ? 2 : 4) * (lane >> 2); }
   // row words of lane k in the workspace ([word][env], stride n)
   PBG_DEV Sc* gP(int r, int k) const { return gbl + ((size_t)r * W + (size_t)k * PW) * n; }
   PBG_DEV Sc* gS(int r) const { return gbl + ((size_t)r * W + 4 * PW) * n; }
@@ -400,7 +407,17 @@ struct TRows {
       if (i == NDB) return yB[k];
       return k < 2 ? yB[k + 4] : 0.f;
     };
-    if (r < cap) {
+    if (r < cap && PL) {
+      LW* p0 = rows + roff(r) + 2 * (lane & ~3);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (slot < 0 && k != k0) continue;
+        *(LW2*)(p0 + 2 * k) = v2f{pw(k, 0), pw(k, 1)};
+        *(LW2*)(p0 + P1OFF + 2 * k) = v2f{pw(k, 2), pw(k, 3)};
+      }
+      *(LW2*)S(r) = v2f{meff, target};
+      *(LW2*)(S(r) + LAMO) = v2f{0.f, mu};
+    } else if (r < cap) {
       LW* p0 = rows + roff(r) + PW * (lane & ~3);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -437,7 +454,10 @@ struct TRows {
   template <bool LDS>
   PBG_DEV void load(int r, int kb, Row& row) const {
     if (LDS || r < cap) {
-      if constexpr (PW == 4) {
+      if constexpr (PL) {
+        const v2f a = *(const LW2*)P(r), c = *(const LW2*)(P(r) + P1OFF);
+        row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = c.x; row.yB[1] = c.y;
+      } else if constexpr (PW == 4) {
         const v4f a = *(const LW4*)P(r);
         row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
       } else {
@@ -450,7 +470,7 @@ struct TRows {
       // dead lets the allocator reuse it at once, and the write-after-write on the pending
       // load forces an lgkmcnt(0) wait right behind the look-ahead load (no pipelining)
       const v2f b = *(const LW2*)S(r);
-      row.meff = b.x; row.tgt = b.y; row.lam = S(r)[2];
+      row.meff = b.x; row.tgt = b.y; row.lam = S(r)[LAMO];
     } else {
       const Sc* p = gP(r, kb);
 #pragma unroll
@@ -463,24 +483,29 @@ struct TRows {
   // LDS-resident row at word offset o of the wave's row regions (P(r) = rows + o, o = roff(r) +
   // PW * lane; its S record at o + sdelta()): the normal sweep steps o by a compile-time stride
   // instead of recomputing the row address from the row index
-  PBG_DEV int poff(int r) const { return roff(r) + PW * lane; }
-  PBG_DEV int sdelta() const { return SOFF + 4 * (lane >> 2) - PW * lane; }
+  PBG_DEV int poff(int r) const { return roff(r) + (PL ? 2 : PW) * lane; }
+  PBG_DEV int sdelta() const { return SOFF + (PL ? 2 : 4) * (lane >> 2) - (PL ? 2 : PW) * lane; }
   static PBG_DEV void load_at(const LW* p, const LW* q, Row& row) {
-    const v4f a = *(const LW4*)p;
-    row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
+    if constexpr (PL) {
+      const v2f a = *(const LW2*)p, c = *(const LW2*)(p + P1OFF);
+      row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = c.x; row.yB[1] = c.y;
+    } else {
+      const v4f a = *(const LW4*)p;
+      row.yb[0] = a.x; row.yb[1] = a.y; row.yB[0] = a.z; row.yB[1] = a.w;
+    }
     const v2f b = *(const LW2*)q;
-    row.meff = b.x; row.tgt = b.y; row.lam = q[2];
+    row.meff = b.x; row.tgt = b.y; row.lam = q[LAMO];
   }
   template <bool LDS>
   PBG_DEV void set_lam(int r, Sc v) const {
-    if (LDS || r < cap) S(r)[2] = v;
+    if (LDS || r < cap) S(r)[LAMO] = v;
     else gS(r)[2 * (size_t)n] = v;
   }
   // friction bound of contact c: mu * lambda of its normal row (one ds_read_b64)
   template <bool LDS>
   PBG_DEV Sc fric_limit(int c) const {
     if (LDS || 3 * c < cap) {
-      const v2f v = *(const LW2*)(S(3 * c) + 2);
+      const v2f v = *(const LW2*)(S(3 * c) + LAMO);
       return v.y * v.x;
     }
     const Sc* q = gS(3 * c);
@@ -545,14 +570,14 @@ PBG_DEV void contact_sweep(const RW& rw, int nc, int kb, typename RW::Sc* ub, ty
       qB = (LW*)pB + sd;
       RW::load_at(pB, qB, B);
       Sc nl = RW::update(A, ub, uB, 0.f, 3.0e38f);
-      qA[2] = nl;
+      qA[RW::LAMO] = nl;
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
       pA = pB + NS < plast ? pB + NS : plast;
       qA = (LW*)pA + sd;
       RW::load_at(pA, qA, A);
       nl = RW::update(B, ub, uB, 0.f, 3.0e38f);
-      qB[2] = nl;
+      qB[RW::LAMO] = nl;
       pos |= (nl > 0.f ? 1u : 0u) << c;
       if (++c >= nc) break;
     }

@@ -258,9 +258,9 @@ def test_f64_atlas_is_refused():
 
 # ------------------------------------------------------------------ float64 kernel variants
 # The float64 walkers run the kernels of the float32 path instantiated on F64<R>: Ant the quad
-# kernel (pbg_team.hip, 4 lanes per env), the Humanoid family 32-lane gangs, the other walkers
-# (AntMuJoCo included: its float64 quad instance is miscompiled, pbg_robot.hip) the 16-lane gang
-# kernel (pbg_gang.hip; kernel=2 puts Ant on it too, gang_lanes=16 the Humanoids); kernel=0 selects the float64 lane-per-env kernel, which stays the
+# kernel (pbg_team.hip, 4 lanes per env; AntMuJoCo too), the Humanoid family 32-lane gangs, the
+# other walkers the 16-lane gang kernel (pbg_gang.hip; kernel=2 puts Ant on it too, gang_lanes=16
+# the Humanoids); kernel=0 selects the float64 lane-per-env kernel, which stays the
 # pendulums' path and the quad / gang kernels' cross-check.
 @pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HopperPyBulletEnv-v0",
                                     "HumanoidFlagrunHarderPyBulletEnv-v0"])
@@ -270,7 +270,7 @@ def test_f64_lane_kernel_teacher_forced(env_id):
 
 
 @pytest.mark.parametrize("env_id,kernel,lanes", [
-    ("AntPyBulletEnv-v0", None, 4), ("AntMuJoCoEnv-v0", None, 16), ("AntPyBulletEnv-v0", 2, 16),
+    ("AntPyBulletEnv-v0", None, 4), ("AntMuJoCoEnv-v0", None, 4), ("AntPyBulletEnv-v0", 2, 16),
     ("HumanoidPyBulletEnv-v0", "g16", 16), ("HumanoidFlagrunHarderPyBulletEnv-v0", "g16", 16),
     ("HumanoidPyBulletEnv-v0", None, 32), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
     ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 32),
