@@ -80,14 +80,15 @@ class ShardedVecEnv:
     ``reset`` / ``step`` works (the CPU tests drive the oracle through it)."""
 
     def __init__(self, env_id: str, num_global: int, rank: int, world: int, device, seed: int = 0,
-                 autoreset: bool = True, env_factory: Optional[Callable] = None):
+                 autoreset: bool = True, env_factory: Optional[Callable] = None, precision: int = 32):
         self.num_global = num_global
         self.offset, self.count = shard_range(num_global, rank, world)
         if env_factory is None:
             from .vec_env import VecEnv
 
             def env_factory(env_id, count, device, seed, env_offset, autoreset):
-                return VecEnv(env_id, count, device=device, seed=seed, env_offset=env_offset, autoreset=autoreset)
+                return VecEnv(env_id, count, device=device, seed=seed, env_offset=env_offset, autoreset=autoreset,
+                              precision=precision)
         self.env = env_factory(env_id, self.count, device, seed, self.offset, autoreset)
 
     def reset(self, **kw):

@@ -187,14 +187,16 @@ class VecEnv:
     def state_dict(self) -> dict:
         """Checkpoint of every env (pybullet saveState generalised): the state records plus the
         env id, the record-layout version (include/pbg.h PBG_RECORD_VERSION) and the scene
-        parameters the states were simulated under."""
+        parameters and physics precision the states were simulated under."""
         phys, aux = self.get_state()
         return {"env_id": self.env_id, "record_version": int(self.info.record_version), "phys": phys, "aux": aux,
-                "sim_params": self.sim_params.as_dict()}
+                "sim_params": self.sim_params.as_dict(), "precision": self.precision}
 
     def load_state_dict(self, sd: dict):
-        """Restore a state_dict(); refuses a checkpoint of another env id, record layout or scene
-        (a checkpoint without "sim_params" is taken to be of the reference's scene)."""
+        """Restore a state_dict(); refuses a checkpoint of another env id, record layout, scene or
+        physics precision (a float64 state rounded into a float32 handle is not the state that was
+        saved; a checkpoint without "sim_params" / "precision" is taken to be of the reference's
+        scene / of float32, the keys' round-4 defaults)."""
         if sd.get("env_id") != self.env_id:
             raise _native.PbgError(f"checkpoint of {sd.get('env_id')!r} loaded into {self.env_id!r}")
         if sd.get("record_version") != self.info.record_version:
@@ -203,6 +205,9 @@ class VecEnv:
         sp = sd.get("sim_params", self.default_sim_params(self.env_id))
         if sp != self.sim_params.as_dict():
             raise _native.PbgError(f"checkpoint scene {sp} != this handle's {self.sim_params.as_dict()}")
+        if sd.get("precision", 32) != self.precision:
+            raise _native.PbgError(f"checkpoint of a precision-{sd.get('precision', 32)} handle loaded into a "
+                                   f"precision-{self.precision} one")
         self.set_state(sd["phys"], sd["aux"])
 
     def set_state(self, phys: torch.Tensor, aux: torch.Tensor = None):

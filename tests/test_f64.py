@@ -32,6 +32,7 @@ import torch
 
 import oracle
 import pybulletgym_amd  # noqa: F401
+from pybulletgym_amd._native import PbgError
 from pybulletgym_amd.vec_env import VecEnv, sample_actions
 from test_gpu import ENVS, _discrete_terms, _first_exceed, _rel, _report
 
@@ -361,3 +362,30 @@ def test_f64_gang_determinism_and_offset_invariance():
     c, sc = run(56, 41)
     np.testing.assert_array_equal(a[:, 41:], c)
     np.testing.assert_array_equal(sa[41:], sc)
+
+
+def test_f64_checkpoint_round_trip_bitwise_and_precision_guard():
+    """A float64 handle's state_dict restores bit for bit across auto-resets (the float64 state
+    record is the state itself), and a float64 checkpoint is refused by a float32 handle (its
+    state would be rounded) and vice versa."""
+    n = 64
+    a = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True, precision=64)
+    a.reset()
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    acts = torch.rand((60, n, 8), device="cuda", generator=gen) * 2 - 1
+    for t in range(20):
+        a.step(acts[t])
+    sd = a.state_dict()
+    assert sd["precision"] == 64
+    b = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True, precision=64)
+    b.load_state_dict(sd)
+    for t in range(20, 60):
+        ra, rb = a.step(acts[t]), b.step(acts[t])
+        np.testing.assert_array_equal(ra.obs.cpu().numpy().view(np.uint32), rb.obs.cpu().numpy().view(np.uint32))
+    np.testing.assert_array_equal(a.get_state()[0].cpu().numpy().view(np.uint64),
+                                  b.get_state()[0].cpu().numpy().view(np.uint64))
+    f32 = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True)
+    with pytest.raises(PbgError):
+        f32.load_state_dict(sd)
+    with pytest.raises(PbgError):
+        b.load_state_dict(f32.state_dict())

@@ -38,12 +38,13 @@ def _run(env_id, vec, offset, count):
     return dones
 
 
-def _worker(rank, world, port, env_id, q):
+def _worker(rank, world, port, env_id, q, precision=32):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pybulletgym_amd import distributed as pd
-    env = pd.ShardedVecEnv(env_id, N_GLOBAL, rank, world, device="cuda:0", seed=SEED, autoreset=True)
+    env = pd.ShardedVecEnv(env_id, N_GLOBAL, rank, world, device="cuda:0", seed=SEED, autoreset=True,
+                           precision=precision)
     _run(env_id, env.env, env.offset, env.count)
     obs, rew, done = env.gather()
     assert obs.is_cuda and obs.shape[0] == N_GLOBAL
@@ -61,8 +62,9 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"])
-def test_two_process_shards_gather_bitwise_equal_single_process(env_id):
+@pytest.mark.parametrize("env_id,precision", [("AntPyBulletEnv-v0", 32), ("HumanoidPyBulletEnv-v0", 32),
+                                              ("AntPyBulletEnv-v0", 64), ("HumanoidPyBulletEnv-v0", 64)])
+def test_two_process_shards_gather_bitwise_equal_single_process(env_id, precision):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from pybulletgym_amd import distributed as pd
@@ -71,7 +73,7 @@ def test_two_process_shards_gather_bitwise_equal_single_process(env_id):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, env_id, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, env_id, q, precision)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -81,7 +83,7 @@ def test_two_process_shards_gather_bitwise_equal_single_process(env_id):
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert count0 == pd.shard_range(N_GLOBAL, 0, world)[1] == 501
-    ref = VecEnv(env_id, N_GLOBAL, seed=SEED, autoreset=True)
+    ref = VecEnv(env_id, N_GLOBAL, seed=SEED, autoreset=True, precision=precision)
     dones = _run(env_id, ref, 0, N_GLOBAL)
     assert dones > 0  # auto-resets happened inside the compared window
     np.testing.assert_array_equal(obs.view(np.uint32), ref.obs.cpu().numpy().view(np.uint32))
