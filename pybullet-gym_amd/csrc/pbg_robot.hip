@@ -250,7 +250,19 @@ template <class RR>
 constexpr bool team64_ok() { return Team<RR>::ok; }
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g);
 bool PBG_FN(launch_team64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s);
+int PBG_FN(debug_stamps_t64_)(unsigned long long* host_out);  // the diagnostic stamps of this TU's kernel
 #ifdef PBG_TEAM64_TU
+int PBG_FN(debug_stamps_t64_)(unsigned long long* host_out) {
+#ifdef PBG_STAMPS
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -3;
+  unsigned long long z[16] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -3;
+  return 0;
+#else
+  (void)host_out;
+  return -1;
+#endif
+}
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g) {
   if constexpr (team64_ok<R64>()) return plan_team<R64>(n_envs, cus, g);
   else { (void)n_envs; (void)cus; (void)g; return (int)hipErrorInvalidValue; }
@@ -340,6 +352,10 @@ int PBG_FN(debug_stamps_)(unsigned long long* host_out) {
   if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -3;
   unsigned long long z[16] = {0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -3;
+  // plus the float64 quad kernel's (its own translation unit and code object)
+  unsigned long long t64[16];
+  if (PBG_FN(debug_stamps_t64_)(t64) == 0)
+    for (int i = 0; i < 16; i++) host_out[i] += t64[i];
   return 0;
 #else
   (void)host_out;

@@ -1508,34 +1508,40 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     flags = (flags & 0xFFu) | (po.feet_out << 8);
   }
   STAMP(8)
+  // float64: the env index through an empty asm, so the stores below form their addresses here
+  // instead of reloading the 64-bit addresses the compiler formed at the kernel's start and spilled
+  // (each such scratch reload waited, vmcnt(0), for every store issued before it: 29 % of the
+  // float64 kernel's cycles went to this phase, 8 % in float32)
+  int eo = e;
+  if constexpr (sizeof(Sc) == 8) asm volatile("" : "+v"(eo));
   const bool term = po.done;
   const bool trunc = el >= R::max_episode_steps;
   if (kb == 0) {
-    io.rew[e] = (float)po.reward;
-    if (io.rew64) io.rew64[e] = po.reward;
+    io.rew[eo] = (float)po.reward;
+    if (io.rew64) io.rew64[eo] = po.reward;
     if (io.rew_terms) {
 #pragma unroll
-      for (int i = 0; i < 5; i++) io.rew_terms[(size_t)e * 5 + i] = po.terms[i];
+      for (int i = 0; i < 5; i++) io.rew_terms[(size_t)eo * 5 + i] = po.terms[i];
     }
-    io.done[e] = term || trunc;
-    if (io.trunc) io.trunc[e] = trunc && !term;
+    io.done[eo] = term || trunc;
+    if (io.trunc) io.trunc[eo] = trunc && !term;
   }
   if (io.autoreset && (term || trunc)) {
-    if (io.term_obs) lanes_store_row<R, 4>(obs, io.term_obs, e, kb);
+    if (io.term_obs) lanes_store_row<R, 4>(obs, io.term_obs, eo, kb);
     bool has_floor = flags & 1u;
     double pot;
     Sc z0;
-    team_reset<R, ES>(B, e, L, s, rw, obs, has_floor, pot, z0);
+    team_reset<R, ES>(B, eo, L, s, rw, obs, has_floor, pot, z0);
     if (kb == 0) {
-      B.pot[e] = pot;
-      z0_of<R>(B)[e] = z0;
-      B.elapsed[e] = 0;
-      B.flags[e] = has_floor ? 1u : 0u;
+      B.pot[eo] = pot;
+      z0_of<R>(B)[eo] = z0;
+      B.elapsed[eo] = 0;
+      B.flags[eo] = has_floor ? 1u : 0u;
     }
   } else if (kb == 0) {
-    B.pot[e] = po.potential;
-    B.elapsed[e] = el;
-    B.flags[e] = flags;
+    B.pot[eo] = po.potential;
+    B.elapsed[eo] = el;
+    B.flags[eo] = flags;
   }
   {
     // replicated base words and obs dealt over the quad (lane kb: elements kb, kb+4, ...)
@@ -1544,14 +1550,14 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     static_for<0, (PBG_BASE_WORDS + 3) / 4>([&](auto m_c) {
       constexpr int m = decltype(m_c)::value;
       const Sc v = lanes_pick<4, m, PBG_BASE_WORDS>(bw, kb);
-      if (4 * m + kb < PBG_BASE_WORDS) st_of<R>(B)[(size_t)(4 * m + kb) * B.n + e] = v;
+      if (4 * m + kb < PBG_BASE_WORDS) st_of<R>(B)[(size_t)(4 * m + kb) * B.n + eo] = v;
     });
-    lanes_store_row<R, 4>(obs, io.obs, e, kb);
+    lanes_store_row<R, 4>(obs, io.obs, eo, kb);
   }
 #pragma unroll
   for (int j = 0; j < NDB; j++) {
-    st_of<R>(B)[(size_t)(SB + kb * NDB + j) * B.n + e] = s.q[j];
-    st_of<R>(B)[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e] = s.qd[j];
+    st_of<R>(B)[(size_t)(SB + kb * NDB + j) * B.n + eo] = s.q[j];
+    st_of<R>(B)[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + eo] = s.qd[j];
   }
   STAMP(9)
   STAMP_FLUSH

@@ -17,13 +17,14 @@ gang_names = {0: "dist: forward levels", 1: "dist: inertia + motion", 2: "dist: 
               14: "pack: gather FK", 15: "pack: gather quat", 12: "pack: gather vel, parts, joints",
               8: "pack: walker pack (float64)", 9: "store (+ auto-reset)"}
 AUTORESET = os.environ.get("PBG_STAMPS_AUTORESET", "1") != "0"
-# ENV:N[:GANG_DIST[:GANG_LANES]]  (GANG_DIST 0/1 forces the gang kernel's replicated / distributed
-# dynamics, -1 the plan's; GANG_LANES 16 / 32 the gang width)
+# ENV:N[:GANG_DIST[:GANG_LANES[:PRECISION]]]  (GANG_DIST 0/1 forces the gang kernel's replicated /
+# distributed dynamics, -1 the plan's; GANG_LANES 16 / 32 the gang width, -1 the plan's; PRECISION 64:
+# the float64 handle)
 for spec in (sys.argv[1:] or ["AntPyBulletEnv-v0:16384"]):
     env_id, n, *rest = spec.split(":")
     n = int(n)
     env = VecEnv(env_id, n, seed=1, autoreset=AUTORESET, gang_dist=int(rest[0]) if rest else -1,
-                 gang_lanes=int(rest[1]) if len(rest) > 1 else -1)
+                 gang_lanes=int(rest[1]) if len(rest) > 1 else -1, precision=int(rest[2]) if len(rest) > 2 else 32)
     env.reset()
     acts = torch.rand((30, n, env.info.action_dim), device="cuda") * 2 - 1
     for i in range(200): env.step(acts[i % 30])  # pre-roll off the reset pose, as bench.py
