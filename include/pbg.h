@@ -134,7 +134,7 @@ typedef struct {
                             kernels) or 64 = float64, the reference's precision (pybullet's
                             btScalar is double: stepSimulation, scene_bases.py:75-76).  The
                             observation / reward pack is float64 in both, as in the reference.
-                            64: every env id but AtlasPyBulletEnv-v0 (PBG_E_HIP) */
+                            64: every env id (AtlasPyBulletEnv-v0: the gang kernel only) */
   int kernel;            /* as in pbg_debug_opts_t.  Precision 64: 1 (default) = the quad kernel for
                             Ant, the 16-lane gang kernel for the other walkers, the lane kernel for
                             the pendulums; 0 = the lane kernel for every robot; 2 = the gang kernel

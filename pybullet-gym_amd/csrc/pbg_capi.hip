@@ -255,7 +255,7 @@ int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int
   h->geo.gang_lanes = (opts && (opts->gang_lanes == 16 || opts->gang_lanes == 32)) ? opts->gang_lanes : -1;
   int e = hip_check(h->k->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
   if (e && co.precision == 64) {
-    snprintf(g_err, sizeof(g_err), "pbg_create: no float64 kernel for %s (Atlas' 886 contact slots have no lane kernel)",
+    snprintf(g_err, sizeof(g_err), "pbg_create: no float64 kernel of this variant for %s (Atlas' 886 contact slots have no lane kernel)",
              env_id);
     delete h;
     return PBG_E_HIP;

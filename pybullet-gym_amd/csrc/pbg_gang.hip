@@ -534,6 +534,9 @@ constexpr int gang_block() {
   using G = Gang<R, T>;
   constexpr long need =
       4L * GangTabs<R>::WORDS + (long)(PBG_GANG_BLOCK / T) * (long)sizeof(real_t<R>) * (G::FIXED + 4L * G::PERC);
+  // float64 Atlas: not even 8 envs' regions fit -- one-wave workgroups of 4 envs
+  constexpr long need8 = 4L * GangTabs<R>::WORDS + 8L * (long)sizeof(real_t<R>) * (G::FIXED + G::MIN_CONTACT_WORDS);
+  if constexpr (sizeof(real_t<R>) == 8 && T == 16 && need8 > 163840L) return PBG_GANG_BLOCK / 4;
   return sizeof(real_t<R>) == 8 && T == 16 && need > 163840L ? PBG_GANG_BLOCK / 2 : PBG_GANG_BLOCK;
 }
 #define PBG_GANG_SYNC                                    \

@@ -86,7 +86,7 @@ template <class RR, int T>
 constexpr bool gang_ok() {
   constexpr bool f64 = sizeof(real_t<RR>) == 8;
   return (RR::kind == 0 || RR::kind >= 2) && (!RR::harder || FP<RR>::NF > 0) && (T == 16 || gang32_ok<RR>()) &&
-         !(f64 && gang_big<RR>());
+         !(f64 && gang_big<RR>() && T != 16);
 }
 // Gang geometry (pbg_gang.hip): T = 16 or 32 lanes per env, 256 / T envs per 4-wave workgroup;
 // the per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor

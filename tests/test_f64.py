@@ -38,7 +38,7 @@ from test_gpu import ENVS, _discrete_terms, _first_exceed, _rel, _report
 
 pytestmark = pytest.mark.gpu
 
-ENVS64 = [e for e in ENVS if e != "AtlasPyBulletEnv-v0"]  # Atlas: no float64 kernel (include/pbg.h)
+ENVS64 = list(ENVS)  # every env id (Atlas on one-wave gang workgroups of 4 envs, round 5)
 STATE_REL64 = 1e-9
 HARD_MAX64 = 1e-6
 SHARE64 = 0.999
@@ -167,8 +167,12 @@ def test_f64_reset_matches_oracle(env_id):
 
 @pytest.mark.parametrize("env_id", ENVS64)
 def test_f64_step_teacher_forced_parity(env_id):
-    """Every float64 env id, 256 envs x 60 teacher-forced steps."""
-    _teacher_forced64(env_id, 256, 60)
+    """Every float64 env id, 256 envs x 60 teacher-forced steps (Atlas, whose oracle is slow:
+    128 x 30, as its float32 test)."""
+    if env_id == "AtlasPyBulletEnv-v0":
+        _teacher_forced64(env_id, 128, 30)
+    else:
+        _teacher_forced64(env_id, 256, 60)
 
 
 CONFIGS64 = [("InvertedPendulumPyBulletEnv-v0", 1024, None), ("HopperPyBulletEnv-v0", 4096, 512),
@@ -251,10 +255,10 @@ def test_f64_determinism_and_env_offset_invariance():
     np.testing.assert_array_equal(sa[32:], sc)
 
 
-def test_f64_atlas_is_refused():
-    from pybulletgym_amd._native import PbgError
+def test_f64_atlas_lane_kernel_is_refused():
+    """Atlas has no lane kernel (886 contact slots) in either precision: kernel=0 is refused."""
     with pytest.raises(PbgError):
-        VecEnv("AtlasPyBulletEnv-v0", 4, precision=64)
+        VecEnv("AtlasPyBulletEnv-v0", 4, precision=64, kernel=0)
 
 
 # ------------------------------------------------------------------ float64 kernel variants
