@@ -1210,7 +1210,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
   // u's base part sliced over the quad: lane kb owns components kb and kb + 4 (kb < 2)
   Sc uBs[2] = {kb == 0 ? uB[0] : (kb == 1 ? uB[1] : (kb == 2 ? uB[2] : uB[3])),
                   kb == 0 ? uB[4] : (kb == 1 ? uB[5] : 0.f)};
-  for (int it = 0; it < P.iterations; it++) {
+  // the limit rows of one sweep (Bullet's order: limits, then the contact normals and frictions)
+  auto limit_sweep = [&]() {
     static_for<0, 4>([&](auto k_c) {
       constexpr int kk = decltype(k_c)::value;
       static_for<0, NLIMB>([&](auto l_c) {
@@ -1251,10 +1252,23 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
         });
       });
     });
-    STAMP(11)
-    if (all_lds) contact_sweep<true>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
-    else contact_sweep<false>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
-    STAMP(13)
+  };
+  // one loop per row source: a wave-uniform branch inside the sweep loop made its back edge merge
+  // the LDS and workspace paths' register assignments (copies of every loop-carried value)
+  if (all_lds) {
+    for (int it = 0; it < P.iterations; it++) {
+      limit_sweep();
+      STAMP(11)
+      contact_sweep<true>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
+      STAMP(13)
+    }
+  } else {
+    for (int it = 0; it < P.iterations; it++) {
+      limit_sweep();
+      STAMP(11)
+      contact_sweep<false>(rw, nc, kb, ub, uBs SUB_STAMP_PASS);
+      STAMP(13)
+    }
   }
   // gather the base part back (replicated for the back-substitution)
   {

@@ -20,6 +20,7 @@ from pybulletgym_amd.vec_env import VecEnv, sample_actions
 env_id, n = "{env}", {n}
 kw = dict(gang_dist={gd})
 if {gl} > 0: kw["gang_lanes"] = {gl}
+if {pr} == 64: kw["precision"] = 64
 env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, **kw)
 env.reset()
 K, P = 300, 200
@@ -33,11 +34,11 @@ print("%.5f" % (e0.elapsed_time(e1) / K))
 '''
 
 
-def run(lib, env, n, gd=-1, gl=-1):
+def run(lib, env, n, gd=-1, gl=-1, pr=32):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if os.path.isdir(lib):
         repo, lib = lib, os.path.join(lib, "pybullet-gym_amd", "libpbg_amd.so")
-    code = CHILD.format(repo=os.path.abspath(repo), lib=os.path.abspath(lib), env=env, n=n, gd=gd, gl=gl)
+    code = CHILD.format(repo=os.path.abspath(repo), lib=os.path.abspath(lib), env=env, n=n, gd=gd, gl=gl, pr=pr)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if out.returncode:
         raise RuntimeError(out.stderr[-2000:])
@@ -47,11 +48,12 @@ def run(lib, env, n, gd=-1, gl=-1):
 if __name__ == "__main__":
     a, b = sys.argv[1], sys.argv[2]
     for spec in sys.argv[3:]:
-        env, n, *opt = spec.split(":")  # ENV:N[:GANG_DIST[:GANG_LANES]]
+        env, n, *opt = spec.split(":")  # ENV:N[:GANG_DIST[:GANG_LANES[:PRECISION]]]
         gd = int(opt[0]) if opt else -1
         gl = int(opt[1]) if len(opt) > 1 else -1
+        pr = int(opt[2]) if len(opt) > 2 else 32
         ta, tb = [], []
         for _ in range(2):
-            ta.append(run(a, env, int(n), gd, gl))
-            tb.append(run(b, env, int(n), gd, gl))
-        print(f"{env:28s} n={n:>6s}  A {min(ta):.4f} ms  B {min(tb):.4f} ms  B/A {min(tb) / min(ta):.3f}", flush=True)
+            ta.append(run(a, env, int(n), gd, gl, pr))
+            tb.append(run(b, env, int(n), gd, gl, pr))
+        print(f"{env:28s} n={n:>6s} f{pr} A {min(ta):.4f} ms  B {min(tb):.4f} ms  B/A {min(tb) / min(ta):.3f}", flush=True)
