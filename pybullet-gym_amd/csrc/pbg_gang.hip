@@ -1598,6 +1598,43 @@ PBG_DEV void gang_get_state(State<R>& s, const GangCtx<R>& X) {
   }
 }
 
+// HumanoidFlagrunHarder: the rows of the cube's corner contacts with the floor, one row per lane.
+// Their Jacobian has only the cube's 6 columns, so the robot's part of y = L^-1 J^T is exactly zero:
+// no Jacobian over the robot's dofs and no forward substitution, only the cube's
+// (nd / sqrt m | (r x nd) / sqrt I).  The row is stored in the sliced layout of every row (the PGS
+// reads it unchanged), with the same arithmetic as the general rows pass, bit for bit (that pass
+// added exact zeros for the robot's part).
+template <class R, int T>
+PBG_DEV void cube_floor_rows(const GangCtx<R>& X, int nr, int ncf, const SimPT<real_t<R>>& P) {
+  using Sc = real_t<R>;
+  using G = Gang<R, T>;
+#pragma unroll 1
+  for (int j = X.t; wave_any(j < 3 * ncf); j += T) {
+    if (j >= 3 * ncf) continue;
+    const int c = nr + j / 3, dir = j % 3;
+    V3<Sc> rA;
+    Sc dist = 0.f;
+    contact_at<R, T>(X, c, [&](auto p) { rA = mk3<Sc>(p[0], p[1], p[2]); dist = p[9]; });
+    // the floor's normal and btPlaneSpace1 basis
+    const V3<Sc> nd = dir == 0 ? mk3<Sc>(0, 0, 1) : (dir == 1 ? mk3<Sc>(0, -1, 0) : mk3<Sc>(1, 0, 0));
+    const V3<Sc> mc = cross3(rA, nd);
+    const Sc rm = Sc(1) / CubeK<Sc>::sm(), rI = Sc(1) / CubeK<Sc>::sI();
+    const V3<Sc> ycl = Sc(1) * rm * nd, cubes = Sc(1) * rI * mc;
+    const Sc D2 = dot3(ycl, ycl) + dot3(cubes, cubes);
+    const Sc meff = D2 > Sc(1e-12) ? fast_rcp(D2) : 0.f;
+    const Sc tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
+    contact_at<R, T>(X, c, [&](auto p0) {
+      auto p = p0 + G::RW0 + dir * G::CRW;
+      const Sc yc[6] = {ycl.x, ycl.y, ycl.z, cubes.x, cubes.y, cubes.z};
+#pragma unroll
+      for (int i = 0; i < G::YS; i++) p[G::yw(i)] = i >= G::N && i < G::NY ? yc[i - G::N] : Sc(0);
+      p[G::YS] = meff;
+      p[G::YS + 1] = tgt;
+      p[G::YS + 2] = 0.f;
+    });
+  }
+}
+
 // ------------------------------------------------------------------ one physics sub-step
 template <class R, int T, bool DIST>
 PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X, uint64_t& slot_bits, uint32_t sub,
@@ -1695,6 +1732,9 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
   const uint64_t gang_mask = ((T == 64) ? ~0ull : ((1ull << T) - 1ull)) << (X.le * T);
   const uint64_t below = (1ull << (X.le * T + X.t)) - 1ull;
   int nc = 0;
+  // HumanoidFlagrunHarder: contacts [nr, nr + ncf) are the cube's corners on the floor (their rows:
+  // cube_floor_rows); the robot's floor / self contacts come before them, the robot-cube ones after
+  int nr = 0, ncf = 0;
   // --- distributed: capsule ends of the self-collision geoms in world coordinates, one geom
   // per lane, in the limit-row area (dead until the rows pass); read by the pair pass ------
   constexpr int O_GE = G::O_LR;
@@ -1808,6 +1848,8 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
     const Sc h = (Sc)PBG_CUBE_HALF, thr = (Sc)PBG_CONTACT_THRESHOLD;
     const M3<Sc> Rc = quat_to_m3(X.l[G::O_CS + 3], X.l[G::O_CS + 4], X.l[G::O_CS + 5], X.l[G::O_CS + 6]);
     const V3<Sc> xc = mk3<Sc>(X.l[G::O_CS], X.l[G::O_CS + 1], X.l[G::O_CS + 2]);
+    static_assert(T >= 8, "the corners are the first round's lanes");
+    nr = nc;
 #pragma unroll
     for (int r = 0; r < (NCC + T - 1) / T; r++) {
       const int k = r * T + X.t;
@@ -1886,6 +1928,7 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
         }
       }
       const uint64_t bal = __ballot(act);
+      if (r == 0) ncf = __popcll(bal & gang_mask & (0xFFull << (X.le * T)));
       if (act) {
         csig += pbg_contact_hash(sub, (uint32_t)(R::NS + R::NPAIR + k));
         const int c = nc + __popcll(bal & gang_mask & below);
@@ -1918,7 +1961,8 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
 #ifdef PBG_DEV_NOROWS
   const int njobs = 0;
 #else
-  const int njobs = NLIM + 3 * nc;
+  // (HumanoidFlagrunHarder: the cube's floor contacts are built by cube_floor_rows below)
+  const int njobs = NLIM + 3 * (nc - ncf);
 #endif
   // the front path holds its staged factor in registers for the rows pass unless it is too big to
   // (Atlas: the register copy spilled 1.2 KB per lane; its rows read the LDS words instead) or the
@@ -1942,6 +1986,7 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
     } else {
       c = (j - NLIM) / 3;
       dir = (j - NLIM) - 3 * c;
+      if constexpr (R::harder) c += c >= nr ? ncf : 0;
       Sc v[G::DW];
       contact_at<R, T>(X, c, [&](auto p) {
 #pragma unroll
@@ -2024,6 +2069,7 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
       });
     }
   }
+  if constexpr (R::harder) cube_floor_rows<R, T>(X, nr, ncf, P);
   PBG_GANG_SYNC
   STAMP(11)
   // --- PGS: 5 sweeps, Bullet order (scene_bases.py:65 numSolverIterations=5) -------------

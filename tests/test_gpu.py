@@ -885,12 +885,14 @@ def test_gang_kernel_matches_lane_kernel_teacher_forced(env_id, opts):
     assert _variant_vs_lane(env_id, 256, 30, **opts) == opts.get("gang_lanes", 16)
 
 
-@pytest.mark.parametrize("lanes", [16, 32])
-def test_gang_workspace_contacts_bitwise_equal_lds_contacts(lanes):
+@pytest.mark.parametrize("env_id,lanes", [("HumanoidPyBulletEnv-v0", 16), ("HumanoidPyBulletEnv-v0", 32),
+                                           ("HumanoidFlagrunHarderPyBulletEnv-v0", 16)])
+def test_gang_workspace_contacts_bitwise_equal_lds_contacts(env_id, lanes):
     """Gang contacts past the LDS capacity live in the device workspace: forcing every
-    contact there (lds_rows=0) must not change a single bit (Humanoid: floor + self)."""
-    a, ca = _rollout("HumanoidPyBulletEnv-v0", gang_lanes=lanes)
-    b, cb = _rollout("HumanoidPyBulletEnv-v0", lds_rows=0, gang_lanes=lanes)
+    contact there (lds_rows=0) must not change a single bit (Humanoid: floor + self;
+    FlagrunHarder: + the cube's floor contacts, whose rows cube_floor_rows builds)."""
+    a, ca = _rollout(env_id, gang_lanes=lanes)
+    b, cb = _rollout(env_id, lds_rows=0, gang_lanes=lanes)
     assert ca.max() > 0
     np.testing.assert_array_equal(ca, cb)
     np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
