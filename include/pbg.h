@@ -96,8 +96,10 @@ typedef struct {
  * these four ints.  Callers that need another option use pbg_create_v2 (pbg_create_opts_t is
  * versioned by its struct_size). */
 typedef struct {
-  int kernel;     /* 0: one-lane-per-env kernel for every robot; 2: the 16-lane gang kernel for
-                     every walker (Ant included); -1 / 1: default (quad for Ant, gang otherwise) */
+  int kernel;     /* 0: one-lane-per-env kernel for every robot (PBG_E_ARG for Atlas, whose 886
+                     contact slots have no lane kernel, in either precision); 2: the 16-lane gang
+                     kernel for every walker (Ant included); -1 / 1: default (quad for Ant, gang
+                     otherwise) */
   int lds_rows;   /* k >= 0: at most k contact rows (gang: contacts) per env resident in LDS,
                      the rest in the device workspace (bitwise-equality tests of that path) */
   int gang_dist;  /* 0 / 1: force replicated / distributed gang dynamics (PBG_E_ARG when the planned
@@ -130,11 +132,12 @@ typedef struct {
  * their defaults), so options appended later never read past an older caller's struct. */
 typedef struct {
   uint32_t struct_size;  /* sizeof(pbg_create_opts_t) at the caller's build */
-  int precision;         /* physics state and arithmetic: 32 = float32 (the default; the fast
-                            kernels) or 64 = float64, the reference's precision (pybullet's
-                            btScalar is double: stepSimulation, scene_bases.py:75-76).  The
-                            observation / reward pack is float64 in both, as in the reference.
-                            64: every env id (AtlasPyBulletEnv-v0: the gang kernel only) */
+  int precision;         /* physics state and arithmetic: 64 = float64 (the default since round 6,
+                            as for pbg_create / pbg_create_ex: the reference's precision, pybullet's
+                            btScalar is double: stepSimulation, scene_bases.py:75-76) or 32 =
+                            float32, the opt-in fast kernels.  The observation / reward pack is
+                            float64 in both, as in the reference.  Every env id has both
+                            (AtlasPyBulletEnv-v0: the gang kernel only) */
   int kernel;            /* as in pbg_debug_opts_t.  Precision 64: 1 (default) = the quad kernel for
                             Ant, the 16-lane gang kernel for the other walkers, the lane kernel for
                             the pendulums; 0 = the lane kernel for every robot; 2 = the gang kernel
@@ -149,7 +152,8 @@ int pbg_default_sim_params(const char* env_id, pbg_sim_params_t* out);
 
 /* gym.make(env_id) for n envs (envs/__init__.py:4-103 registry entries; the env's
  * physics client is created here instead of lazily in BaseBulletEnv._reset,
- * env_bases.py:46-56).  env_id (robot_id order): "InvertedPendulumPyBulletEnv-v0",
+ * env_bases.py:46-56), with float64 physics (the reference's precision; pbg_create_v2 selects
+ * float32).  env_id (robot_id order): "InvertedPendulumPyBulletEnv-v0",
  * "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "AntPyBulletEnv-v0",
  * "HumanoidPyBulletEnv-v0", "Walker2DPyBulletEnv-v0", "InvertedPendulumSwingupPyBulletEnv-v0",
  * "InvertedDoublePendulumPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "HopperMuJoCoEnv-v0",
@@ -165,9 +169,10 @@ int pbg_create_debug(const char* env_id, int n_envs, int device, uint64_t seed, 
  * diagnostic launch options (NULL = defaults).  PBG_E_ARG for parameters out of range. */
 int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                   const pbg_sim_params_t* params, const pbg_debug_opts_t* opts, pbg_handle** out);
-/* pbg_create_ex with versioned options (opts NULL = defaults: float32, the default kernels).
- * PBG_E_ARG for a bad struct_size or precision; PBG_E_HIP when the env id has no kernel of the
- * requested precision. */
+/* pbg_create_ex with versioned options (opts NULL = defaults: float64, the default kernels).
+ * PBG_E_ARG for a bad struct_size (not a multiple of 4 in [8, sizeof]) or precision, and for a
+ * launch option the planned kernel cannot honour (in either precision); PBG_E_HIP when no kernel
+ * plan fits the device.  *out is NULL after every failure. */
 int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                   const pbg_sim_params_t* params, const pbg_create_opts_t* opts, pbg_handle** out);
 /* The handle's physics precision: 32 or 64 (PBG_E_ARG for NULL). */

@@ -45,11 +45,11 @@ class DebugOpts(ctypes.Structure):
 
 
 class CreateOpts(ctypes.Structure):
-    """pbg_create_opts_t (pbg_create_v2): versioned by struct_size; precision 32 or 64."""
+    """pbg_create_opts_t (pbg_create_v2): versioned by struct_size; precision 64 (default) or 32."""
     _fields_ = [("struct_size", ctypes.c_uint32), ("precision", ctypes.c_int), ("kernel", ctypes.c_int),
                 ("lds_rows", ctypes.c_int), ("gang_dist", ctypes.c_int), ("gang_lanes", ctypes.c_int)]
 
-    def __init__(self, precision=32, kernel=-1, lds_rows=-1, gang_dist=-1, gang_lanes=-1):
+    def __init__(self, precision=64, kernel=-1, lds_rows=-1, gang_dist=-1, gang_lanes=-1):
         super().__init__(ctypes.sizeof(CreateOpts), precision, kernel, lds_rows, gang_dist, gang_lanes)
 
 

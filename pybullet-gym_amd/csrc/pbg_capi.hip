@@ -189,7 +189,7 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
   pbg_create_opts_t o;
   memset(&o, 0, sizeof(o));
   o.struct_size = (uint32_t)sizeof(o);
-  o.precision = 32;
+  o.precision = 64;
   o.kernel = opts ? opts->kernel : -1;
   o.lds_rows = opts ? opts->lds_rows : -1;
   o.gang_dist = opts ? opts->gang_dist : -1;
@@ -200,12 +200,15 @@ int pbg_create_ex(const char* env_id, int n_envs, int device, uint64_t seed, int
 int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int env_offset,
                   const pbg_sim_params_t* params, const pbg_create_opts_t* copts, pbg_handle** out) {
   if (!out) return fail(PBG_E_ARG, "pbg_create: out is NULL%s%ld");
-  // versioned options: read only the fields the caller's struct holds (struct_size); absent = defaults
+  *out = nullptr;  // every failure below leaves the caller's handle NULL
+  // versioned options: read only the fields the caller's struct holds (struct_size, a whole number of
+  // the struct's 4-byte fields); absent fields = defaults
   pbg_create_opts_t co;
   memset(&co, 0, sizeof(co));
-  co.precision = 32; co.kernel = -1; co.lds_rows = -1; co.gang_dist = -1; co.gang_lanes = -1;
+  co.precision = 64; co.kernel = -1; co.lds_rows = -1; co.gang_dist = -1; co.gang_lanes = -1;
   if (copts) {
-    if (copts->struct_size < (uint32_t)(2 * sizeof(uint32_t)) || copts->struct_size > (uint32_t)sizeof(co))
+    if (copts->struct_size < (uint32_t)(2 * sizeof(uint32_t)) || copts->struct_size > (uint32_t)sizeof(co) ||
+        copts->struct_size % 4u != 0u)
       return fail(PBG_E_ARG, "pbg_create_v2: opts->struct_size %s%ld is not a pbg_create_opts_t size", "",
                   (long)copts->struct_size);
     memcpy(&co, copts, copts->struct_size);
@@ -214,7 +217,6 @@ int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int
     return fail(PBG_E_ARG, "pbg_create_v2: precision must be 32 or 64%s (got %ld)", "", co.precision);
   const pbg_debug_opts_t dbg = {co.kernel, co.lds_rows, co.gang_dist, co.gang_lanes};
   const pbg_debug_opts_t* opts = &dbg;
-  *out = nullptr;
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_create: unknown env id '%s'%ld", env_id ? env_id : "(null)");
   if (n_envs <= 0) return fail(PBG_E_ARG, "pbg_create: n_envs must be > 0%s (got %ld)", "", n_envs);
@@ -254,16 +256,13 @@ int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int
   h->geo.force_dist = opts ? opts->gang_dist : -1;
   h->geo.gang_lanes = (opts && (opts->gang_lanes == 16 || opts->gang_lanes == 32)) ? opts->gang_lanes : -1;
   int e = hip_check(h->k->plan(n_envs, cus, mode, &h->geo), "kernel attributes");
-  if (e && co.precision == 64) {
-    snprintf(g_err, sizeof(g_err), "pbg_create: no float64 kernel of this variant for %s (Atlas' 886 contact slots have no lane kernel)",
-             env_id);
-    delete h;
-    return PBG_E_HIP;
-  }
   // diagnostic options that the chosen kernel cannot honour are refused, not ignored: an A/B
-  // run must never measure another kernel than the one it asked for
+  // run must never measure another kernel than the one it asked for.  Checked before any plan failure is
+  // reported, so an option's refusal is PBG_E_ARG in both precisions.
   const char* bad = nullptr;
-  if (!e && opts->gang_lanes == 32 && h->geo.team != 32)
+  if (opts->kernel == 0 && (e || h->geo.team != 1))
+    bad = "kernel = 0: this robot has no lane-per-env kernel (Atlas' 886 contact slots)";
+  else if (!e && opts->gang_lanes == 32 && h->geo.team != 32)
     bad = "gang_lanes = 32 needs the 32-lane gang kernel (the Humanoid family on the default / gang plan)";
   else if (e && opts->gang_lanes == 32)
     bad = "gang_lanes = 32: this robot has no 32-lane gang kernel";
@@ -277,6 +276,12 @@ int pbg_create_v2(const char* env_id, int n_envs, int device, uint64_t seed, int
     snprintf(g_err, sizeof(g_err), "pbg_create: %s", bad);
     delete h;
     return PBG_E_ARG;
+  }
+  if (e) {
+    snprintf(g_err, sizeof(g_err), "pbg_create: no float%d kernel plan for %s at %d envs (HIP error %d)",
+             co.precision, env_id, n_envs, e);
+    delete h;
+    return PBG_E_HIP;
   }
   // cap on the LDS-resident contact rows (tests of the device-workspace path)
   if (opts && opts->lds_rows >= 0 && opts->lds_rows < h->geo.lds_rows) h->geo.lds_rows = opts->lds_rows;

@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#ifdef PBG_DEV_CHECKS
+#include <cassert>
+#endif
 
 #define PBG_DEV __device__ __forceinline__
 
@@ -59,8 +62,11 @@ PBG_DEV V3<S> cross3(V3<S> a, V3<S> b) {
   return mk3<S>(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 // Physics-side fast reciprocal / sqrt (v_rcp_f32 / v_sqrt_f32 / v_rsq_f32, ~1 ulp); the
-// numpy-exact pack keeps IEEE division and sqrt.  The double overloads are the IEEE operations
-// (correctly rounded division and sqrt): the reference-precision path's accuracy is float64's.
+// numpy-exact pack keeps IEEE division and sqrt.  The double overloads: fast_sqrt is the IEEE
+// (correctly rounded) sqrt, fast_rsq an IEEE division of it, and fast_rcp is NOT correctly rounded
+// -- it is within 1 ulp of the IEEE quotient for finite, non-zero, non-overflowing-reciprocal
+// arguments only (x = 0 gives NaN, not inf).  Every call site guards its argument; the checks build
+// (-DPBG_DEV_CHECKS) asserts it.
 PBG_DEV float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 PBG_DEV float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -68,6 +74,9 @@ PBG_DEV float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 // the finite non-zero arguments the physics passes; the IEEE division's scaling and fix-up cost
 // twice the instructions)
 PBG_DEV double fast_rcp(double x) {
+#ifdef PBG_DEV_CHECKS
+  assert(x != 0.0 && __builtin_isfinite(x));
+#endif
   double r = __builtin_amdgcn_rcp(x);
   double e = __builtin_fma(-x, r, 1.0);
   r = __builtin_fma(r, e, r);

@@ -263,6 +263,12 @@ int PBG_FN(debug_stamps_t64_)(unsigned long long* host_out) {
   return -1;
 #endif
 }
+#ifdef PBG_TRACE64  // diagnostic build (tools/f64_quad_trace.py): the trace of this TU's quad kernel
+extern "C" int pbg_debug_trace64(double* host_out) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_trace64), sizeof(g_trace64)) != hipSuccess) return -3;
+  return (int)(sizeof(g_trace64) / sizeof(double));
+}
+#endif
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g) {
   if constexpr (team64_ok<R64>()) return plan_team<R64>(n_envs, cus, g);
   else { (void)n_envs; (void)cus; (void)g; return (int)hipErrorInvalidValue; }

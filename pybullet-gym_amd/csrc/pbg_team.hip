@@ -69,6 +69,19 @@ PBG_DEV double quad_bcast(double x) { return qperm<K | (K << 2) | (K << 4) | (K 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
   }
 
+// Diagnostic build only (-DPBG_TRACE64, tools/f64_quad_trace.py; never the product library): the float64
+// quad kernel's per-lane values at its phase boundaries, in the last sub-step, as unconditional global
+// stores at the existing scheduling fences (no branch: the trace splits no scheduling region).  Slot
+// (block * 64 + lane) & 255: the diagnostic runs 64 envs (4 one-wave blocks).
+#ifdef PBG_TRACE64
+#define PBG_TRACE_PH 8
+__device__ double g_trace64[256][PBG_TRACE_PH][8];
+#define TRACE64(ph, i, v) \
+  do { if constexpr (sizeof(Sc) == 8) g_trace64[(blockIdx.x * 64 + threadIdx.x) & 255][ph][i] = (double)(v); } while (0)
+#else
+#define TRACE64(ph, i, v) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ branch decomposition
 template <int N, class S = float>
 struct BTab {  // per-branch constant: v[entry][branch]
@@ -785,6 +798,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
 #pragma unroll
     for (int c = 0; c < 6; c++) tJ.a[c] += Iw.a[c];
   }
+  TRACE64(0, 0, tm); TRACE64(0, 1, tp1.x); TRACE64(0, 2, tF.x); TRACE64(0, 3, tF.z); TRACE64(0, 4, tN.y);
+  TRACE64(0, 5, tJ.a[0]); TRACE64(0, 6, tJ.a[5]); TRACE64(0, 7, kb);
 
   // this branch's active slots, then their contact indices (exclusive quad prefix)
   auto detect_branch = [&]() {
@@ -817,6 +832,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     });
     detect_branch();
   }
+  TRACE64(1, 0, n0); TRACE64(1, 1, nc); TRACE64(1, 2, ci); TRACE64(1, 3, act); TRACE64(1, 4, base_bits);
+  TRACE64(1, 5, sdist[0]); TRACE64(1, 6, sP[0].x); TRACE64(1, 7, sP[0].z);
 
   STAMP(0)
   // --- mass matrix: branch block Lbr, base-branch block Lgb, base block Mbb; bias -------
@@ -865,6 +882,9 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     rb[a] += tau[j] - pk<T::DAMP, j>(L) * s.qd[j];
     if constexpr (has_springs<R>()) rb[a] -= pk<T::STIFF, j>(L) * s.q[j];  // mjcf.py B7
   });
+  TRACE64(2, 0, Lbr[0][0]); TRACE64(2, 1, Lbr[NDB - 1][0]); TRACE64(2, 2, Lbr[NDB - 1][NDB - 1]);
+  TRACE64(2, 3, Lgb[0][0]); TRACE64(2, 4, Lgb[5][NDB - 1]); TRACE64(2, 5, Mbb[3][3]); TRACE64(2, 6, rb[0]);
+  TRACE64(2, 7, rB[2]);
 
   STAMP(1)
   // --- Cholesky: branch columns (lane), Schur complement of the base (quad sum), 6x6 ----
@@ -928,6 +948,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     });
   });
 
+  TRACE64(3, 0, Ld[0]); TRACE64(3, 1, Ld[NDB - 1]); TRACE64(3, 2, Lbb[0][0]); TRACE64(3, 3, Lbb[5][5]);
+  TRACE64(3, 4, Ldb[5]); TRACE64(3, 5, Lbb[5][3]); TRACE64(3, 6, Lgb[2][0]); TRACE64(3, 7, Lbr[NDB - 1][0]);
   // --- unconstrained velocity nu_pred = nu + dt M^-1 (tau - C); u = L^T nu_pred --------
   Sc yb[NDB], yB[6];
   static_for<0, NDB>([&](auto a_c) {
@@ -994,6 +1016,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     static_for<gg, 6>([&](auto h_c) { t += Lbb[decltype(h_c)::value][gg] * nB[decltype(h_c)::value]; });
     uB[gg] = t;
   });
+  TRACE64(4, 0, yb[0]); TRACE64(4, 1, yB[0]); TRACE64(4, 2, xB[2]); TRACE64(4, 3, xb[0]); TRACE64(4, 4, nB[2]);
+  TRACE64(4, 5, nb[0]); TRACE64(4, 6, ub[0]); TRACE64(4, 7, uB[5]);
 
   STAMP(2)
   // --- joint-limit rows (lane: its branch dofs), in registers; base part broadcast ------
@@ -1202,6 +1226,10 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   PBG_QUAD_SYNC
+  if constexpr (OWN && NLIMB > 0) {
+    TRACE64(5, 0, Om[0]); TRACE64(5, 1, Orm[0]); TRACE64(5, 2, Otl[0]); TRACE64(5, 3, Oth[0]);
+    TRACE64(5, 4, BY[0][0][0]); TRACE64(5, 5, BY[1][0][1]); TRACE64(5, 6, Byb[0][0][0]); TRACE64(5, 7, Om[NLIMB - 1]);
+  }
   // wave-uniform: do all rows of the wave's envs live in LDS?
   const bool all_lds = __builtin_amdgcn_ballot_w64(3 * nc > rw.cap) == 0;
 
@@ -1276,6 +1304,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     uB[0] = quad_bcast<0>(s0); uB[1] = quad_bcast<1>(s0); uB[2] = quad_bcast<2>(s0); uB[3] = quad_bcast<3>(s0);
     uB[4] = quad_bcast<0>(s1); uB[5] = quad_bcast<1>(s1);
   }
+  TRACE64(6, 0, uBs[0]); TRACE64(6, 1, uBs[1]); TRACE64(6, 2, ub[0]); TRACE64(6, 3, ub[NDB - 1]);
+  TRACE64(6, 4, uB[0]); TRACE64(6, 5, uB[5]); TRACE64(6, 6, nc); TRACE64(6, 7, uB[2]);
 
   STAMP(5)
   // --- nu = L^-T u (base first, replicated; then the branch); clamp; integrate ---------
@@ -1324,6 +1354,8 @@ PBG_DEV int team_substep(TState<R>& s, const Lane& L, const real_t<R>* tau, uint
     const Sc inv = fast_rsq(nx * nx + ny * ny + nz * nz + nw * nw);
     s.bq[0] = nx * inv; s.bq[1] = ny * inv; s.bq[2] = nz * inv; s.bq[3] = nw * inv;
   }
+  TRACE64(7, 0, nB[0]); TRACE64(7, 1, nB[3]); TRACE64(7, 2, nb[0]); TRACE64(7, 3, nb[NDB - 1]);
+  TRACE64(7, 4, s.qd[0]); TRACE64(7, 5, s.bv[2]); TRACE64(7, 6, s.bw[0]); TRACE64(7, 7, s.bq[3]);
   STAMP(6)
   return nc;
 }

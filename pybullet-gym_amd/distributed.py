@@ -76,11 +76,12 @@ class ShardedVecEnv:
     """This rank's share of a global batch of envs, plus the optional flat gather.
 
     env_factory(env_id, count, device, seed, env_offset, autoreset) builds the per-rank env
-    (default: the HIP VecEnv); anything with ``obs`` / ``reward`` / ``done`` tensors and
-    ``reset`` / ``step`` works (the CPU tests drive the oracle through it)."""
+    (default: the HIP VecEnv at ``precision`` -- 64, the reference's double, unless 32 is asked
+    for); anything with ``obs`` / ``reward`` / ``done`` tensors and ``reset`` / ``step`` works (the
+    CPU tests drive the oracle through it)."""
 
     def __init__(self, env_id: str, num_global: int, rank: int, world: int, device, seed: int = 0,
-                 autoreset: bool = True, env_factory: Optional[Callable] = None, precision: int = 32):
+                 autoreset: bool = True, env_factory: Optional[Callable] = None, precision: int = 64):
         self.num_global = num_global
         self.offset, self.count = shard_range(num_global, rank, world)
         if env_factory is None:

@@ -157,37 +157,49 @@ HumanoidFlagrun.alive_bonus = _alive_bonus_humanoid
 # ----------------------------------------------------------------------------- envs
 class BaseBulletEnv:
     """env_bases.py:9-121 surface: reset() -> obs, step(a) -> (obs, reward, done, {}),
-    seed(), render(), close().  One env on one GPU via the batched kernel."""
+    seed(), render(), close().  One env on one GPU via the batched kernel.
+
+    ``precision`` is the physics scalar: 64 (the default) steps in float64 like the reference's
+    pybullet (btScalar is double; scene_bases.py:75-76 -> stepSimulation), 32 runs the float32
+    fast-mode kernels.  The handle (``_vec``, a one-env VecEnv) is created on first use -- the
+    reference connects its physics client in reset() (env_bases.py:60-67) -- and again after seed()."""
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 60}
     env_id = None
 
-    def __init__(self, robot, render=False, device="cuda:0"):
+    def __init__(self, robot, render=False, device="cuda:0", precision=64):
         self.robot = robot
         self.isRender = render
         self.action_space = robot.action_space
         self.observation_space = robot.observation_space
         self.device = device
+        self.precision = int(precision)
+        if self.precision not in (32, 64):
+            raise ValueError(f"precision must be 32 or 64, not {precision!r}")
         self._seed_value = 0
-        self._vec = None
+        self._vec_h = None
         self.scene = None
         self.reward = 0.0
         self.frame = 0
 
-    def _make_vec(self):
-        from .vec_env import VecEnv
-        self._vec = VecEnv(self.env_id, 1, device=self.device, seed=self._seed_value, autoreset=False)
+    @property
+    def _vec(self):
+        if self._vec_h is None:
+            from .vec_env import VecEnv
+            self._vec_h = VecEnv(self.env_id, 1, device=self.device, seed=self._seed_value, autoreset=False,
+                                 precision=self.precision)
+        return self._vec_h
+
+    @property
+    def unwrapped(self):
+        return self  # gym.Env.unwrapped
 
     def seed(self, seed=None):
         self._seed_value = 0 if seed is None else int(seed)
         self.action_space.seed(seed)
-        if self._vec is not None:
-            self._vec.close()
-            self._vec = None
+        self.close()
         return [self._seed_value]
 
     def reset(self):
-        if self._vec is None:
-            self._make_vec()
         self.frame = 0
         self.reward = 0.0
         obs = self._vec.reset()
@@ -195,7 +207,7 @@ class BaseBulletEnv:
 
     def step(self, a):
         import torch
-        if self._vec is None:
+        if self._vec_h is None:
             raise RuntimeError("call reset() before step()")
         a = np.asarray(a, dtype=np.float32).reshape(1, -1)
         assert np.isfinite(a).all()  # robot_locomotors.py:27
@@ -215,9 +227,9 @@ class BaseBulletEnv:
         return np.array([])  # env_bases.py:73-77 for non-rgb modes; rendering is out of scope
 
     def close(self):
-        if self._vec is not None:
-            self._vec.close()
-            self._vec = None
+        if self._vec_h is not None:
+            self._vec_h.close()
+            self._vec_h = None
 
     def HUD(self, state, a, done):
         pass
@@ -238,8 +250,8 @@ class WalkerBaseBulletEnv(BaseBulletEnv):
     foot_ground_object_names = set(["floor"])
     joints_at_limit_cost = -0.1
 
-    def __init__(self, robot, render=False, device="cuda:0"):
-        BaseBulletEnv.__init__(self, robot, render, device)
+    def __init__(self, robot, render=False, device="cuda:0", precision=64):
+        BaseBulletEnv.__init__(self, robot, render, device, precision)
         self.camera_x = 0
         self.walk_target_x = 1e3
         self.walk_target_y = 0
@@ -254,43 +266,43 @@ class WalkerBaseBulletEnv(BaseBulletEnv):
 class HopperBulletEnv(WalkerBaseBulletEnv):
     env_id = "HopperPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = Hopper()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
 
 
 class Walker2DBulletEnv(WalkerBaseBulletEnv):
     env_id = "Walker2DPyBulletEnv-v0"  # gym_locomotion_envs.py:128-131
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = Walker2D()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
 
 
 class HalfCheetahBulletEnv(WalkerBaseBulletEnv):
     env_id = "HalfCheetahPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = HalfCheetah()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
 
 
 class AntBulletEnv(WalkerBaseBulletEnv):
     env_id = "AntPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = Ant()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
 
 
 class HumanoidBulletEnv(WalkerBaseBulletEnv):
     env_id = "HumanoidPyBulletEnv-v0"
 
-    def __init__(self, robot=None, render=False, device="cuda:0"):
+    def __init__(self, robot=None, render=False, device="cuda:0", precision=64):
         # gym_locomotion_envs.py:147 shares one default Humanoid() between instances; each
         # env here owns its own robot record (the batched state is per env anyway).
         self.robot = robot if robot is not None else Humanoid()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
         self.electricity_cost = 4.25 * WalkerBaseBulletEnv.electricity_cost
         self.stall_torque_cost = 4.25 * WalkerBaseBulletEnv.stall_torque_cost
 
@@ -301,8 +313,8 @@ class HumanoidFlagrunBulletEnv(HumanoidBulletEnv):
     flag_timeout live in the device state (aux words), the draws are Philox (not np_random)."""
     env_id = "HumanoidFlagrunPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        HumanoidBulletEnv.__init__(self, HumanoidFlagrun(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        HumanoidBulletEnv.__init__(self, HumanoidFlagrun(), render, device, precision)
 
 
 class HumanoidFlagrunHarderBulletEnv(HumanoidBulletEnv):
@@ -316,8 +328,8 @@ class HumanoidFlagrunHarderBulletEnv(HumanoidBulletEnv):
     env_id = "HumanoidFlagrunHarderPyBulletEnv-v0"
     random_lean = True  # :168 (a class attribute of the env; the robot never reads it)
 
-    def __init__(self, render=False, device="cuda:0"):
-        HumanoidBulletEnv.__init__(self, HumanoidFlagrunHarder(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        HumanoidBulletEnv.__init__(self, HumanoidFlagrunHarder(), render, device, precision)
 
 
 class AtlasBulletEnv(WalkerBaseBulletEnv):
@@ -327,9 +339,9 @@ class AtlasBulletEnv(WalkerBaseBulletEnv):
     kernel."""
     env_id = "AtlasPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = Atlas()
-        WalkerBaseBulletEnv.__init__(self, self.robot, render, device)
+        WalkerBaseBulletEnv.__init__(self, self.robot, render, device, precision)
 
 
 class WalkerBaseMuJoCoEnv(WalkerBaseBulletEnv):
@@ -342,8 +354,8 @@ class HopperMuJoCoEnv(WalkerBaseMuJoCoEnv):
     reward x-progress + 1 - 1e-3 sum(a^2), done unless height > -0.3 and |angle| < .2."""
     env_id = "HopperMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        WalkerBaseMuJoCoEnv.__init__(self, HopperMuJoCo(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        WalkerBaseMuJoCoEnv.__init__(self, HopperMuJoCo(), render, device, precision)
 
 
 class Walker2DMuJoCoEnv(WalkerBaseMuJoCoEnv):
@@ -351,8 +363,8 @@ class Walker2DMuJoCoEnv(WalkerBaseMuJoCoEnv):
     -1 < angle < 1."""
     env_id = "Walker2DMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        WalkerBaseMuJoCoEnv.__init__(self, Walker2DMuJoCo(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        WalkerBaseMuJoCoEnv.__init__(self, Walker2DMuJoCo(), render, device, precision)
 
 
 class HalfCheetahMuJoCoEnv(WalkerBaseMuJoCoEnv):
@@ -360,8 +372,8 @@ class HalfCheetahMuJoCoEnv(WalkerBaseMuJoCoEnv):
     - 0.1 sum(a^2), never done."""
     env_id = "HalfCheetahMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        WalkerBaseMuJoCoEnv.__init__(self, HalfCheetahMuJoCo(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        WalkerBaseMuJoCoEnv.__init__(self, HalfCheetahMuJoCo(), render, device, precision)
 
 
 class AntMuJoCoEnv(WalkerBaseMuJoCoEnv):
@@ -369,8 +381,8 @@ class AntMuJoCoEnv(WalkerBaseMuJoCoEnv):
     reward alive(state[0] + initial_z) + progress - 0.1 joints_at_limit."""
     env_id = "AntMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        WalkerBaseMuJoCoEnv.__init__(self, AntMuJoCo(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        WalkerBaseMuJoCoEnv.__init__(self, AntMuJoCo(), render, device, precision)
 
     def _obs_out(self, obs):
         return obs[0].cpu().numpy().astype(np.float64)
@@ -381,8 +393,8 @@ class HumanoidMuJoCoEnv(WalkerBaseMuJoCoEnv):
     qfrc_actuator, cfrc_ext] (376; the last four are zeros in the reference)."""
     env_id = "HumanoidMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
-        WalkerBaseMuJoCoEnv.__init__(self, HumanoidMuJoCo(), render, device)
+    def __init__(self, render=False, device="cuda:0", precision=64):
+        WalkerBaseMuJoCoEnv.__init__(self, HumanoidMuJoCo(), render, device, precision)
 
     def _obs_out(self, obs):
         return obs[0].cpu().numpy().astype(np.float64)
@@ -392,9 +404,9 @@ class InvertedPendulumBulletEnv(BaseBulletEnv):
     """gym_pendulum_envs.py:7-42: obs float64 [x, vx, cos(theta), sin(theta), theta_dot]."""
     env_id = "InvertedPendulumPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = InvertedPendulum()
-        BaseBulletEnv.__init__(self, self.robot, render, device)
+        BaseBulletEnv.__init__(self, self.robot, render, device, precision)
         self.stateId = -1
         self.scene = self.create_single_player_scene(None)
 
@@ -410,9 +422,9 @@ class InvertedPendulumSwingupBulletEnv(InvertedPendulumBulletEnv):
     never done (the TimeLimit ends episodes)."""
     env_id = "InvertedPendulumSwingupPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = InvertedPendulumSwingup()
-        BaseBulletEnv.__init__(self, self.robot, render, device)
+        BaseBulletEnv.__init__(self, self.robot, render, device, precision)
         self.stateId = -1
         self.scene = self.create_single_player_scene(None)
 
@@ -422,9 +434,9 @@ class InvertedDoublePendulumBulletEnv(BaseBulletEnv):
     sin g, g']; reward 10 - (0.01 x2^2 + (y2 + 0.3 - 2)^2); done y2 + 0.3 <= 1."""
     env_id = "InvertedDoublePendulumPyBulletEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = InvertedDoublePendulum()
-        BaseBulletEnv.__init__(self, self.robot, render, device)
+        BaseBulletEnv.__init__(self, self.robot, render, device, precision)
         self.stateId = -1
         self.scene = self.create_single_player_scene(None)
 
@@ -440,9 +452,9 @@ class InvertedDoublePendulumMuJoCoEnv(InvertedDoublePendulumBulletEnv):
     clip(vx, th', g'), zeros(3)]; reward 10 - dist_penalty - (1e-3 th'^2 + 5e-3 g'^2)."""
     env_id = "InvertedDoublePendulumMuJoCoEnv-v0"
 
-    def __init__(self, render=False, device="cuda:0"):
+    def __init__(self, render=False, device="cuda:0", precision=64):
         self.robot = InvertedDoublePendulumMuJoCo()
-        BaseBulletEnv.__init__(self, self.robot, render, device)
+        BaseBulletEnv.__init__(self, self.robot, render, device, precision)
         self.stateId = -1
         self.scene = self.create_single_player_scene(None)
 
@@ -508,11 +520,12 @@ class TimeLimit:
         return getattr(self.env, k)
 
 
-def make(env_id: str, device="cuda:0"):
-    """gym.make(env_id) equivalent: the env class behind gym's TimeLimit."""
+def make(env_id: str, device="cuda:0", precision: int = 64):
+    """gym.make(env_id) equivalent: the env class behind gym's TimeLimit.  precision 64 (the
+    default) is the reference's double-precision physics; 32 the float32 fast mode."""
     if env_id not in ENV_CLASSES:
         raise KeyError(f"unknown env id {env_id!r}; known: {sorted(ENV_CLASSES)}")
-    return TimeLimit(ENV_CLASSES[env_id](device=device), MAX_EPISODE_STEPS[env_id])
+    return TimeLimit(ENV_CLASSES[env_id](device=device, precision=precision), MAX_EPISODE_STEPS[env_id])
 
 
 def register_with_gym():

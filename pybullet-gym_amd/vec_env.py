@@ -49,9 +49,10 @@ class VecEnv:
     pbg_sim_params_t, scene_bases.py:8-18,58-73), or a ``_native.SimParams``; None = the
     reference's values (``self.sim_params`` holds the ones in force).
 
-    ``precision``: 32 (float32 physics, the fast kernels) or 64 (float64 physics state and
-    arithmetic, the reference's btScalar precision; pbg_create_v2).  Observations stay float32 and
-    the reward pack float64 in both, as the reference's (robot_locomotors.py:64, gym_locomotion_envs.py:99-105).
+    ``precision``: 64 (the default: float64 physics state and arithmetic, the reference's btScalar
+    precision, scene_bases.py:75-76 -> stepSimulation) or 32 (float32 physics, the opt-in fast mode);
+    pbg_create_v2.  Observations stay float32 and the reward pack float64 in both, as the reference's
+    (robot_locomotors.py:64, gym_locomotion_envs.py:99-105).
 
     ``kernel`` / ``lds_rows`` / ``gang_dist`` / ``gang_lanes`` are test and diagnostic launch
     options (``pbg_create_debug``): the lane-per-env (0) or gang (2) kernel instead of the default,
@@ -61,7 +62,7 @@ class VecEnv:
 
     def __init__(self, env_id: str, num_envs: int, device="cuda:0", seed: int = 0, env_offset: int = 0,
                  autoreset: bool = True, kernel: int = -1, lds_rows: int = -1, gang_dist: int = -1,
-                 sim_params=None, gang_lanes: int = -1, precision: int = 32):
+                 sim_params=None, gang_lanes: int = -1, precision: int = 64):
         if not torch.cuda.is_available():
             raise _native.PbgError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.env_id = env_id

@@ -12,7 +12,7 @@ the unpinned physics, not a numeric pin (SURVEY.md section 8c "Known-answer test
 ``episode_returns_device`` through the HIP step (libpbg_amd.so) -- the same episodes,
 since the reset draws come from the same host RNG.
 
-  python tests/policies.py [oracle|gpu] [env_id ...]   # prints the score table
+  python tests/policies.py [oracle|gpu|gpu32] [env_id ...]   # prints the score table
 """
 from __future__ import annotations
 
@@ -88,12 +88,14 @@ def episode_returns_oracle(env_id: str, n: int, seed: int = 0, steps: int = MAX_
     return ret, length
 
 
-def episode_returns_device(env_id: str, n: int, seed: int = 0, steps: int = MAX_STEPS):
-    """Same episodes through the HIP step kernel (libpbg_amd.so), reset draws passed in."""
+def episode_returns_device(env_id: str, n: int, seed: int = 0, steps: int = MAX_STEPS, precision: int = 64):
+    """Same episodes through the HIP step kernel (libpbg_amd.so), reset draws passed in; precision
+    64: the float64 handle (the reference's btScalar), 32: the float32 fast mode."""
     import torch
     from pybulletgym_amd.vec_env import VecEnv
     pi = Policy(env_id)
-    env = VecEnv(env_id, n, device="cuda:0", seed=seed, autoreset=False)
+    env = VecEnv(env_id, n, device="cuda:0", seed=seed, autoreset=False, precision=precision)
+    assert env.precision == precision
     obs = env.reset(init_q=torch.from_numpy(reset_draws(n, env.info.reset_dofs, seed).astype(np.float32)))
     ret = torch.zeros(n, dtype=torch.float64, device=env.device)
     length = torch.zeros(n, dtype=torch.int64, device=env.device)
@@ -133,9 +135,9 @@ if __name__ == "__main__":
     ids = sys.argv[2:] or list(POLICY_FILES)
     for env_id in ids:
         n = 16
-        if mode == "gpu":
+        if mode in ("gpu", "gpu32"):
             import pybulletgym_amd  # noqa: F401
-            ret, ln = episode_returns_device(env_id, n)
+            ret, ln = episode_returns_device(env_id, n, precision=32 if mode == "gpu32" else 64)
         else:
             ret, ln = episode_returns_oracle(env_id, n)
         rr = random_returns_oracle(env_id, n) if mode == "oracle" else np.zeros(1)

@@ -3,7 +3,8 @@
 pybullet steps in double (btScalar; stepSimulation, /root/reference/pybulletgym/envs/roboschool/
 scene_bases.py:75-76).  ``VecEnv(..., precision=64)`` (pbg_create_v2) keeps the physical state in
 float64 and runs the same algorithm as the float32 kernels -- and as the oracle -- in float64
-arithmetic, with IEEE division / sqrt and the device library's sin / cos.  Against the float64
+arithmetic, with the IEEE sqrt, reciprocals within 1 ulp of IEEE division (v_rcp_f64 + two Newton
+steps, finite non-zero arguments; pbg_math.h) and the device library's sin / cos.  Against the float64
 oracle the remaining differences are float64 rounding (summation orders, the kernels' inertia-
 about-O formulation of M), so the bounds here are nine orders tighter than the float32 tests':
 
@@ -58,10 +59,11 @@ def _state_rel(a, b):
     return (np.abs(a - b) / np.maximum(1.0, np.abs(b))).max(axis=1)
 
 
-def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None, **opts):
+def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None, on_step=None, **opts):
     """The GPU float64 handle steps all n envs (auto-reset, Philox actions); before each step the
     sampled envs' float64 state records go to the oracle (and to N probes perturbed by 1e-12
-    relative), which steps them; compared as in the module docstring."""
+    relative), which steps them; compared as in the module docstring.  on_step(t, env) sees every
+    step's whole-batch outputs (tests/test_full_configs.py digests them)."""
     if sim is not None:
         sp = VecEnv.default_sim_params(env_id)
         sp.update(sim)
@@ -91,6 +93,8 @@ def _teacher_forced64(env_id, n, steps, sample=None, seed=3, name=None, sim=None
                 p.state[:] = orc.state + pert.uniform(-1, 1, orc.state.shape) * (PROBE_REL64 * np.abs(orc.state) + PROBE_ABS64)
                 p.aux[:] = orc.aux
             res = env.step(acts[t], want_reward64=True, want_contacts=True, want_terms=True)
+            if on_step is not None:
+                on_step(t, env)
             done_g = res.done.bool()
             og = torch.where(done_g[:, None], res.terminal_obs, res.obs).index_select(0, tidx).cpu().numpy()
             dg = (done_g & ~res.truncated.bool()).index_select(0, tidx).cpu().numpy()
@@ -255,10 +259,54 @@ def test_f64_determinism_and_env_offset_invariance():
     np.testing.assert_array_equal(sa[32:], sc)
 
 
-def test_f64_atlas_lane_kernel_is_refused():
-    """Atlas has no lane kernel (886 contact slots) in either precision: kernel=0 is refused."""
-    with pytest.raises(PbgError):
-        VecEnv("AtlasPyBulletEnv-v0", 4, precision=64, kernel=0)
+@pytest.mark.parametrize("env_id", ENVS64)
+def test_f64_facade_default_is_float64_and_matches_oracle(env_id):
+    """the reference-compatible surface (``make`` and the per-env gym classes,
+    envs/__init__.py:59-84) steps the reference's double-precision physics by default
+    (scene_bases.py:75-76).  One env through ``make(env_id)`` -- the TimeLimit wrapper, the env class,
+    its one-env handle -- teacher-forced against the float64 oracle for 40 steps (Atlas 20): the
+    float64 state after every step within STATE_REL64 = 1e-9 relative, the returned reward within
+    1e-9, the observation within one float32 rounding, done identical."""
+    from pybulletgym_amd import make
+    env = make(env_id)
+    assert env.unwrapped.precision == 64 and env.unwrapped._vec.precision == 64
+    env.seed(7)
+    env.reset()
+    vec = env.unwrapped._vec
+    assert vec.precision == 64
+    orc = oracle.OracleEnvs(env_id, 1, seed=7)
+    rng = np.random.default_rng(7)
+    errs = []
+    for t in range(20 if env_id == "AtlasPyBulletEnv-v0" else 40):
+        phys, aux = vec.get_state()
+        orc.state[:] = phys.cpu().numpy()
+        orc.aux[:] = aux.cpu().numpy()
+        a = rng.uniform(-1, 1, env.action_space.shape).astype(np.float32)
+        o, r, d, info = env.step(a)
+        oo, ro, do, _ = orc.step(a[None])
+        errs.append(float(_state_rel(vec.get_state()[0].cpu().numpy(), orc.state)[0]))
+        assert abs(r - ro[0]) <= STATE_REL64 * max(1.0, abs(ro[0])), (t, r, ro[0])
+        assert _rel(np.asarray(o, np.float32)[None], oo).max() <= 1.01 * OBS_ULP, t
+        assert d == bool(do[0]), t
+        if d:
+            break
+    _report(dict(test=f"f64_facade[{env_id}]", steps=len(errs), state_max_rel=max(errs)))
+    assert max(errs) <= STATE_REL64, errs
+    env.close()
+    f32 = make(env_id, precision=32)
+    assert f32.unwrapped._vec.precision == 32
+    f32.close()
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_f64_atlas_lane_kernel_is_refused(precision):
+    """Atlas has no lane kernel (886 contact slots) in either precision: kernel=0 is refused with
+    PBG_E_ARG (-1), never a silent run of the gang kernel; gang_lanes = 32 on a robot
+    without 32-lane gangs is PBG_E_ARG at float64 as at float32."""
+    with pytest.raises(PbgError, match=r"failed \(-1\).*kernel = 0"):
+        VecEnv("AtlasPyBulletEnv-v0", 4, precision=precision, kernel=0)
+    with pytest.raises(PbgError, match=r"failed \(-1\).*gang_lanes = 32"):
+        VecEnv("HopperPyBulletEnv-v0", 4, precision=precision, gang_lanes=32)
 
 
 # ------------------------------------------------------------------ float64 kernel variants
@@ -388,7 +436,7 @@ def test_f64_checkpoint_round_trip_bitwise_and_precision_guard():
         np.testing.assert_array_equal(ra.obs.cpu().numpy().view(np.uint32), rb.obs.cpu().numpy().view(np.uint32))
     np.testing.assert_array_equal(a.get_state()[0].cpu().numpy().view(np.uint64),
                                   b.get_state()[0].cpu().numpy().view(np.uint64))
-    f32 = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True)
+    f32 = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True, precision=32)
     with pytest.raises(PbgError):
         f32.load_state_dict(sd)
     with pytest.raises(PbgError):

@@ -6,9 +6,11 @@
 (a) ``test_full_batch_teacher_forced``: one VecEnv holding the whole batch (launch geometry,
     LDS capacity and envs per CU of the full size), 200 teacher-forced steps with auto-reset
     against the float64 oracle on 384 envs spread evenly over the batch (every workgroup
-    position), through the same class A/B/C bounds and outlier explanation as the per-GPU
-    config tests (tests/test_gpu.py SplitStats).  Every step's (obs | reward | done) of all envs
-    is digested (sha256) for (b).
+    position).  Float32 handles go through the class A/B/C bounds and outlier explanation of the
+    per-GPU config tests (tests/test_gpu.py SplitStats); float64 handles (the reference's
+    precision and the facade's default) through tests/test_f64.py's bounds --
+    every same-contact-set step's state within 1e-9 of the oracle.  Every step's
+    (obs | reward | done) of all envs is digested (sha256) for (b).
 (b) ``test_full_batch_eight_shards_bitwise``: the product's multi-GPU path on one device -- 8
     processes on cuda:0, each a ``ShardedVecEnv`` owning 1/8 of the batch (env_offset = its first
     global env id, Philox reset noise and actions keyed by the global id), stepping with
@@ -38,8 +40,9 @@ import pybulletgym_amd  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 FULL = [("HalfCheetahPyBulletEnv-v0", 65536), ("HumanoidPyBulletEnv-v0", 32768)]
+FULLP = [(e, n, p) for p in (32, 64) for e, n in FULL]
 STEPS, SEED, SAMPLE, WORLD, GATHER_EVERY = 200, 29, 384, 8, 4
-_DIGESTS = {}  # env_id -> per-step sha256 of the whole batch (filled by (a), reused by (b))
+_DIGESTS = {}  # (env_id, precision) -> per-step sha256 of the whole batch (filled by (a), reused by (b))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -57,11 +60,11 @@ def _digest(obs, rew, done):
     return h.hexdigest()
 
 
-def _single_process_digests(env_id, n):
+def _single_process_digests(env_id, n, precision):
     """(a)'s GPU trajectory without the oracle (when (b) runs alone): the same handle, actions and
     seed -- teacher forcing only reads the device state, it never writes it."""
     from pybulletgym_amd.vec_env import VecEnv, sample_actions
-    env = VecEnv(env_id, n, seed=SEED, autoreset=True)
+    env = VecEnv(env_id, n, seed=SEED, autoreset=True, precision=precision)
     env.reset()
     acts = sample_actions(env.info.action_dim, n, STEPS, seed=SEED)
     out, dones = [], 0
@@ -74,30 +77,37 @@ def _single_process_digests(env_id, n):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("env_id,n", FULL)
-def test_full_batch_teacher_forced(env_id, n):
-    from test_gpu import _teacher_forced
+@pytest.mark.parametrize("env_id,n,precision", FULLP)
+def test_full_batch_teacher_forced(env_id, n, precision):
     digests, dones = [], [0]
 
     def on_step(t, env):
+        assert env.precision == precision
         dones[0] += int(env.done.sum())
         digests.append(_digest(env.obs, env.reward, env.done))
 
-    rec = _teacher_forced(env_id, n, STEPS, sample=SAMPLE, seed=SEED, name=f"full_batch[{env_id},{n}x{STEPS}]",
-                          on_step=on_step)
+    if precision == 64:
+        from test_f64 import _teacher_forced64
+        rec = _teacher_forced64(env_id, n, STEPS, sample=SAMPLE, seed=SEED,
+                                name=f"f64_full_batch[{env_id},{n}x{STEPS}]", on_step=on_step)
+    else:
+        from test_gpu import _teacher_forced
+        rec = _teacher_forced(env_id, n, STEPS, sample=SAMPLE, seed=SEED, name=f"full_batch[{env_id},{n}x{STEPS}]",
+                              on_step=on_step)
     assert len(digests) == STEPS
     assert dones[0] > 0, "no auto-reset inside the window"
-    _DIGESTS[env_id] = (digests, dones[0])
+    _DIGESTS[(env_id, precision)] = (digests, dones[0])
     assert rec["env_steps"] == SAMPLE * STEPS
 
 
-def _worker(rank, world, port, env_id, n, q):
+def _worker(rank, world, port, env_id, n, precision, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pybulletgym_amd import distributed as pd
     from pybulletgym_amd.vec_env import sample_actions
-    env = pd.ShardedVecEnv(env_id, n, rank, world, device="cuda:0", seed=SEED, autoreset=True)
+    env = pd.ShardedVecEnv(env_id, n, rank, world, device="cuda:0", seed=SEED, autoreset=True, precision=precision)
+    assert env.env.precision == precision
     acts = sample_actions(env.env.info.action_dim, env.count, STEPS, seed=SEED, env_offset=env.offset)
     env.reset()
     out, dones = {}, 0
@@ -129,13 +139,13 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env_id,n", FULL)
-def test_full_batch_eight_shards_bitwise(env_id, n):
+@pytest.mark.parametrize("env_id,n,precision", FULLP)
+def test_full_batch_eight_shards_bitwise(env_id, n, precision):
     from pybulletgym_amd import distributed as pd
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, env_id, n, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, env_id, n, precision, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     try:
@@ -147,7 +157,7 @@ def test_full_batch_eight_shards_bitwise(env_id, n):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert count0 == pd.shard_range(n, 0, WORLD)[1] == n // WORLD
-    ref, ref_dones = _DIGESTS.get(env_id) or _single_process_digests(env_id, n)
+    ref, ref_dones = _DIGESTS.get((env_id, precision)) or _single_process_digests(env_id, n, precision)
     assert shard_dones == ref_dones > 0  # the same auto-resets, inside the compared window
     assert len(shard_digests) >= STEPS // GATHER_EVERY
     bad = [t for t, d in sorted(shard_digests.items()) if d != ref[t]]

@@ -115,7 +115,7 @@ def test_device_pack_matches_reference_golden(env_id):
 @pytest.mark.parametrize("env_id", ENVS)
 def test_reset_matches_oracle(env_id):
     n = 128
-    env = VecEnv(env_id, n, seed=5, autoreset=False)
+    env = VecEnv(env_id, n, seed=5, autoreset=False, precision=32)
     orc = oracle.OracleEnvs(env_id, n, seed=5)
     q0 = np.random.default_rng(0).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
     obs = env.reset(init_q=torch.from_numpy(q0)).cpu().numpy()
@@ -129,7 +129,7 @@ def test_reset_matches_oracle(env_id):
 @pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"])
 def test_rng_reset_matches_host_philox(env_id):
     n, seed, off = 64, 1234, 1000
-    env = VecEnv(env_id, n, seed=seed, env_offset=off, autoreset=False)
+    env = VecEnv(env_id, n, seed=seed, env_offset=off, autoreset=False, precision=32)
     env.reset()
     env.reset()  # second episode
     phys, _ = env.get_state()
@@ -476,7 +476,7 @@ def _teacher_forced(env_id, n, steps, sample=None, seed=3, name=None, sim=None, 
 
 def _teacher_forced_run(env_id, n, steps, sample, seed, name, sim, init=None, probes=N_PROBES,
                         strict_share=STRICT_SHARE, on_step=None):
-    env = VecEnv(env_id, n, seed=seed, autoreset=True, sim_params=sim)
+    env = VecEnv(env_id, n, seed=seed, autoreset=True, sim_params=sim, precision=32)
     env.reset()
     if init is not None:  # rewrite the reset state records (phys, aux) before the first step
         phys, aux = env.get_state()
@@ -596,7 +596,7 @@ def _first_exceed(err, thr):
 
 @pytest.mark.parametrize("env_id,n,sample", FREE_CONFIGS)
 def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, steps=1000):
-    env = VecEnv(env_id, n, seed=17, autoreset=False)
+    env = VecEnv(env_id, n, seed=17, autoreset=False, precision=32)
     env.reset()
     idx = np.linspace(0, n - 1, sample).astype(np.int64)
     tidx = torch.from_numpy(idx).cuda()
@@ -671,7 +671,7 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
 def test_free_running_short_horizon_ant():
     """No teacher forcing: 10 steps from identical resets stay within 1e-3 (obs)."""
     n = 128
-    env = VecEnv("AntPyBulletEnv-v0", n, seed=3, autoreset=False)
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=3, autoreset=False, precision=32)
     orc = oracle.OracleEnvs("AntPyBulletEnv-v0", n)
     r = np.random.default_rng(2)
     q0 = r.uniform(-0.1, 0.1, (n, 8)).astype(np.float32)
@@ -687,7 +687,7 @@ def test_free_running_short_horizon_ant():
 # ------------------------------------------------------------------ episode bookkeeping
 def test_autoreset_and_time_limit():
     n = 64
-    env = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True)
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=9, autoreset=True, precision=32)
     env.reset()
     phys, aux = env.get_state()
     aux[:, 2] = 999.0  # elapsed: next step hits max_episode_steps = 1000
@@ -705,7 +705,7 @@ def test_determinism_and_env_offset_invariance():
     """Same seed -> bitwise identical rollouts; env i of a shard with env_offset k equals
     env k+i of a bigger batch (sharding does not change trajectories)."""
     def run(n, off):
-        env = VecEnv("HopperPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True)
+        env = VecEnv("HopperPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True, precision=32)
         env.reset()
         g = torch.Generator(device="cuda").manual_seed(0)
         acts = torch.rand((30, 64, 3), device="cuda", generator=g) * 2 - 1
@@ -723,7 +723,7 @@ def test_determinism_and_env_offset_invariance():
 def test_large_batch_stays_finite():
     """BASELINE config sizes: Ant 16,384 envs for 200 random steps with auto-reset."""
     n = 16384
-    env = VecEnv("AntPyBulletEnv-v0", n, seed=4, autoreset=True)
+    env = VecEnv("AntPyBulletEnv-v0", n, seed=4, autoreset=True, precision=32)
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(1)
     dones = 0
@@ -754,10 +754,10 @@ def test_sanity_check_every_env(env_id):
 
 def test_facade_matches_vecenv_and_time_limit():
     from pybulletgym_amd import make
-    env = make("HopperPyBulletEnv-v0")
+    env = make("HopperPyBulletEnv-v0")  # the reference's double precision by default
     env.seed(3)
     o = env.reset()
-    vec = VecEnv("HopperPyBulletEnv-v0", 1, seed=3, autoreset=False)
+    vec = VecEnv("HopperPyBulletEnv-v0", 1, seed=3, autoreset=False, precision=64)
     ov = vec.reset()
     np.testing.assert_array_equal(o, ov[0].cpu().numpy())
     a = np.array([0.3, -0.2, 0.5], np.float32)
@@ -774,7 +774,7 @@ def test_facade_matches_vecenv_and_time_limit():
 # ------------------------------------------------------------------ kernel variants
 def _rollout(env_id, n=128, steps=40, seed=11, **opts):
     """Auto-reset rollout with torch-RNG actions; returns (obs, contact counts) per step."""
-    e = VecEnv(env_id, n, seed=seed, autoreset=True, **opts)
+    e = VecEnv(env_id, n, seed=seed, autoreset=True, **opts, precision=32)
     e.reset()
     g = torch.Generator(device="cuda").manual_seed(5)
     obs, nc = [], []
@@ -799,8 +799,8 @@ def _variant_vs_lane(env_id, n, steps, seed=3, **opts):
     """Teacher-forced comparison of a kernel variant against the lane kernel from the same
     states each step, split by contact-set signature like the oracle comparison (same set:
     max relative obs error <= 1e-4, identical done and contact counts)."""
-    var = VecEnv(env_id, n, seed=seed, autoreset=False, **opts)
-    lane = VecEnv(env_id, n, seed=seed, autoreset=False, kernel=0)
+    var = VecEnv(env_id, n, seed=seed, autoreset=False, **opts, precision=32)
+    lane = VecEnv(env_id, n, seed=seed, autoreset=False, kernel=0, precision=32)
     assert lane.info.lanes_per_env == 1
     r = np.random.default_rng(7)
     na, nr = var.info.action_dim, var.info.reset_dofs
@@ -856,7 +856,7 @@ def test_quad_kernel_matches_lane_kernel_teacher_forced():
 
 def test_quad_kernel_determinism_and_offset_invariance():
     def run(n, off):
-        env = VecEnv("AntPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True)
+        env = VecEnv("AntPyBulletEnv-v0", n, seed=21, env_offset=off, autoreset=True, precision=32)
         env.reset()
         g = torch.Generator(device="cuda").manual_seed(0)
         acts = torch.rand((30, 96, 8), device="cuda", generator=g) * 2 - 1
@@ -904,7 +904,7 @@ def test_gang_kernel_determinism_and_offset_invariance(env_id, lanes):
     """Bitwise reruns; env i of a batch starting at env_offset k == env k+i of a full batch
     (a partially filled last wave must not disturb the others)."""
     def run(n, off):
-        env = VecEnv(env_id, n, seed=21, env_offset=off, autoreset=True, gang_lanes=lanes)
+        env = VecEnv(env_id, n, seed=21, env_offset=off, autoreset=True, gang_lanes=lanes, precision=32)
         assert env.info.lanes_per_env == lanes
         env.reset()
         g = torch.Generator(device="cuda").manual_seed(0)
@@ -920,8 +920,8 @@ def test_gang_plan_many_envs_plans_for_resident_workgroups():
     time, so the plan sizes the LDS contact capacity for one resident workgroup -- the capacity
     of the 4,096-env plan -- instead of a 1/32 share that would hold no contact (round 5); the
     workgroup fits the 160 KiB LDS (no unsigned underflow in the plan) and the step runs."""
-    small = VecEnv("HumanoidPyBulletEnv-v0", 4096, seed=1)
-    env = VecEnv("HumanoidPyBulletEnv-v0", 131072, seed=1)
+    small = VecEnv("HumanoidPyBulletEnv-v0", 4096, seed=1, precision=32)
+    env = VecEnv("HumanoidPyBulletEnv-v0", 131072, seed=1, precision=32)
     assert env.info.lds_rows == small.info.lds_rows > 0, (env.info.lds_rows, small.info.lds_rows)
     assert 0 < env.info.lds_bytes <= 160 * 1024
     small.close()
@@ -945,7 +945,7 @@ def test_reward_terms_match_oracle_and_sum(env_id):
     and the MuJoCo / pendulum variants); the reward is their left-to-right sum, and each term
     matches the oracle's (teacher-forced, 20 steps, same contact set)."""
     n = 128
-    env = VecEnv(env_id, n, seed=2, autoreset=False)
+    env = VecEnv(env_id, n, seed=2, autoreset=False, precision=32)
     orc = oracle.OracleEnvs(env_id, n, nthreads=8, seed=2)
     prb = oracle.OracleEnvs(env_id, n, nthreads=8, seed=2)
     pert = np.random.default_rng(0)
@@ -980,12 +980,12 @@ def test_checkpoint_restore_is_bitwise_across_resets():
     """get_state -> set_state into a fresh handle carries the episode counter (the reset-noise
     Philox counter): after several auto-resets both handles stay bitwise identical."""
     n = 64
-    a = VecEnv("HopperPyBulletEnv-v0", n, seed=4, autoreset=True)
+    a = VecEnv("HopperPyBulletEnv-v0", n, seed=4, autoreset=True, precision=32)
     a.reset()
     acts = sample_actions(3, n, 120, seed=1)
     for t in range(40):
         a.step(acts[t])
-    b = VecEnv("HopperPyBulletEnv-v0", n, seed=4, autoreset=True)
+    b = VecEnv("HopperPyBulletEnv-v0", n, seed=4, autoreset=True, precision=32)
     b.set_state(*a.get_state())
     resets = 0
     for t in range(40, 120):
@@ -1018,7 +1018,7 @@ def test_flagrun_redraws_match_oracle():
     steps, past the 150-calc_state timeout: walk target, flag_timeout and the draw counter
     identical to the oracle's (same Philox stream), obs within the step tolerances."""
     n, steps, seed = 64, 155, 17
-    env = VecEnv("HumanoidFlagrunPyBulletEnv-v0", n, seed=seed, autoreset=False)
+    env = VecEnv("HumanoidFlagrunPyBulletEnv-v0", n, seed=seed, autoreset=False, precision=32)
     orc = oracle.OracleEnvs("HumanoidFlagrunPyBulletEnv-v0", n, nthreads=8, seed=seed)
     r = np.random.default_rng(2)
     env.reset(init_q=torch.from_numpy(r.uniform(-0.1, 0.1, (n, 17)).astype(np.float32)))
@@ -1068,7 +1068,7 @@ def test_harder_cube_launch_and_impact_teacher_forced():
     n, steps = 256, 40
     _teacher_forced(HARDER, n, steps, seed=11, name=f"harder_launch[{n}x{steps}]", init=_harder_launch_now, probes=8,
                     strict_share=0.998)
-    env = VecEnv(HARDER, n, seed=11, autoreset=False)
+    env = VecEnv(HARDER, n, seed=11, autoreset=False, precision=32)
     env.reset()
     phys, aux = env.get_state()
     _harder_launch_now(phys, aux)
@@ -1101,14 +1101,14 @@ def test_harder_cube_launch_and_impact_teacher_forced():
 def test_state_dict_round_trip_and_record_version():
     """VecEnv.state_dict / load_state_dict carry PBG_RECORD_VERSION: a restored
     handle steps bitwise like the original; a checkpoint of another layout is refused."""
-    a = VecEnv("HopperPyBulletEnv-v0", 32, seed=4, autoreset=True)
+    a = VecEnv("HopperPyBulletEnv-v0", 32, seed=4, autoreset=True, precision=32)
     a.reset()
     acts = sample_actions(3, 32, 20, seed=1)
     for t in range(10):
         a.step(acts[t])
     sd = a.state_dict()
     assert sd["record_version"] == 2 and sd["aux"].shape[1] == a.info.aux_words
-    b = VecEnv("HopperPyBulletEnv-v0", 32, seed=4, autoreset=True)
+    b = VecEnv("HopperPyBulletEnv-v0", 32, seed=4, autoreset=True, precision=32)
     b.load_state_dict(sd)
     for t in range(10, 20):
         np.testing.assert_array_equal(a.step(acts[t]).obs.cpu().numpy().view(np.uint32),
@@ -1151,17 +1151,17 @@ def test_sim_params_defaults_bitwise_and_changes_trajectory():
         other, _ = _rollout(env_id, n=128, steps=30, sim_params=over)
         assert np.isfinite(other).all()
         assert np.abs(other[-1] - base[-1]).max() > 1e-2, over
-    e = VecEnv(env_id, 4, sim_params={"frame_skip": 6, "gravity": 1.6})
+    e = VecEnv(env_id, 4, sim_params={"frame_skip": 6, "gravity": 1.6}, precision=32)
     assert e.info.substeps == 6 and e.sim_params.frame_skip == 6 and e.sim_params.gravity == 1.6
     sd = e.state_dict()
     assert sd["sim_params"]["gravity"] == 1.6
     from pybulletgym_amd._native import PbgError
     with pytest.raises(PbgError):
-        VecEnv(env_id, 4).load_state_dict(sd)  # a checkpoint of another scene
+        VecEnv(env_id, 4, precision=32).load_state_dict(sd)  # a checkpoint of another scene
     for bad in ({"frame_skip": 0}, {"timestep": -0.01}, {"solver_iterations": 0}, {"contact_erp": 1.5},
                 {"gravity": float("nan")}, {"no_such_field": 1}):
         with pytest.raises(PbgError):
-            VecEnv(env_id, 4, sim_params=bad)
+            VecEnv(env_id, 4, sim_params=bad, precision=32)
 
 
 def test_sim_params_flagrun_timeout_follows_frame_skip():
@@ -1171,7 +1171,7 @@ def test_sim_params_flagrun_timeout_follows_frame_skip():
     env_id, n = "HumanoidFlagrunPyBulletEnv-v0", 16
     for fs, want in ((4, 149), (7, 85)):
         over = {"frame_skip": fs, "timestep": 0.0165 / fs}
-        env = VecEnv(env_id, n, seed=5, autoreset=False, sim_params=over)
+        env = VecEnv(env_id, n, seed=5, autoreset=False, sim_params=over, precision=32)
         q0 = np.random.default_rng(1).uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
         env.reset(init_q=torch.from_numpy(q0))
         _, aux = env.get_state()
@@ -1198,4 +1198,4 @@ def test_debug_options_the_plan_cannot_honour_are_refused(opts):
     from pybulletgym_amd._native import PbgError
     env_id = "HumanoidPyBulletEnv-v0" if opts.get("gang_dist") == 0 and "kernel" not in opts else "AntPyBulletEnv-v0"
     with pytest.raises(PbgError, match="pbg_create"):
-        VecEnv(env_id, 64, **opts)
+        VecEnv(env_id, 64, **opts, precision=32)

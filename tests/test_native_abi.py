@@ -98,6 +98,7 @@ def test_create_opts_struct_matches_header():
     assert [(n, ct[t]) for t, n in fields] == list(_native.CreateOpts._fields_)
     o = _native.CreateOpts(precision=64)
     assert o.struct_size == ctypes.sizeof(_native.CreateOpts) and o.precision == 64 and o.kernel == -1
+    assert _native.CreateOpts().precision == 64  # the reference's double is the default (round 6)
 
 
 @pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="libpbg_amd.so not built")
@@ -105,10 +106,11 @@ def test_create_v2_refuses_bad_options_without_gpu():
     """pbg_create_v2 validates its versioned options before it touches a device: a struct_size that
     is no pbg_create_opts_t size and a precision other than 32 / 64 are PBG_E_ARG."""
     L = _native.lib()
-    h = ctypes.c_void_p()
-    for o in (_native.CreateOpts(precision=16), _native.CreateOpts(precision=64)):
-        if o.precision == 64:
-            o.struct_size = 4  # shorter than struct_size + precision
+    for size in (None, 4, 10, ctypes.sizeof(_native.CreateOpts) + 4):
+        o = _native.CreateOpts(precision=16 if size is None else 64)
+        if size is not None:
+            o.struct_size = size  # shorter than struct_size + precision / not whole fields / too long
+        h = ctypes.c_void_p(0x1234)  # a stale handle value: every failure must leave NULL (ADVICE r5)
         rc = L.pbg_create_v2(b"AntPyBulletEnv-v0", 4, 0, 0, 0, None, ctypes.byref(o), ctypes.byref(h))
-        assert rc == -1, rc
-        assert not h.value
+        assert rc == -1, (size, rc)
+        assert not h.value, size

@@ -77,10 +77,15 @@ TWO_SAMPLE_Z = 3.0
 KS_P_MIN = 0.01
 
 
+_ORACLE_EPISODES = {}  # env_id -> the float64 oracle's (returns, lengths), shared by both precisions
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", [64, 32])
 @pytest.mark.parametrize("env_id", list(BANDS))
-def test_pretrained_policy_device(env_id):
-    """The bands through the HIP step kernel (256 episodes), and the device's return and
+def test_pretrained_policy_device(env_id, precision):
+    """The bands through the HIP step kernel (256 episodes) at both physics precisions (64: the
+    reference's double, the facade's default; 32: the fast mode), and the device's return and
     episode-length distributions against the float64 oracle's over the same 256 episodes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -89,8 +94,11 @@ def test_pretrained_policy_device(env_id):
     import pybulletgym_amd  # noqa: F401
     _, floor, ratio = BANDS[env_id]
     n = POLICY_EPISODES
-    ret, length = policies.episode_returns_device(env_id, n, seed=0)
-    ret_o, len_o = policies.episode_returns_oracle(env_id, n, seed=0, nthreads=min(16, os.cpu_count() or 1))
+    ret, length = policies.episode_returns_device(env_id, n, seed=0, precision=precision)
+    if env_id not in _ORACLE_EPISODES:
+        _ORACLE_EPISODES[env_id] = policies.episode_returns_oracle(env_id, n, seed=0,
+                                                                   nthreads=min(16, os.cpu_count() or 1))
+    ret_o, len_o = _ORACLE_EPISODES[env_id]
     rnd = policies.random_returns_oracle(env_id, 8, seed=0)
     assert np.isfinite(ret).all()
     assert ret.mean() >= floor, (ret.mean(), length.mean())
@@ -102,7 +110,7 @@ def test_pretrained_policy_device(env_id):
     z = (ret.mean() - ret_o.mean()) / max(se, 1e-300)
     ks = stats.ks_2samp(length, len_o).pvalue if (length.std() > 0 or len_o.std() > 0 or
                                                    length[0] != len_o[0]) else 1.0
-    rec = dict(env=env_id, device_mean=float(ret.mean()), oracle_mean=float(ret_o.mean()), se=float(se),
+    rec = dict(env=env_id, precision=precision, device_mean=float(ret.mean()), oracle_mean=float(ret_o.mean()), se=float(se),
                z=float(z), device_len=float(length.mean()), oracle_len=float(len_o.mean()), ks_p=float(ks))
     print(rec)
     assert abs(ret.mean() - ret_o.mean()) <= TWO_SAMPLE_Z * se + 1e-9 * max(1.0, abs(ret_o.mean())), rec

@@ -7,7 +7,7 @@ import pybulletgym_amd
 from pybulletgym_amd.vec_env import VecEnv
 for env_id, n in [("HumanoidPyBulletEnv-v0", 4096), ("AntPyBulletEnv-v0", 16384)]:
     for ar in (True, False):
-        env = VecEnv(env_id, n, seed=2, autoreset=ar)
+        env = VecEnv(env_id, n, seed=2, autoreset=ar, precision=32)
         env.reset()
         K = 100
         acts = torch.rand((K, n, env.info.action_dim), device="cuda") * 2 - 1

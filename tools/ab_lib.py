@@ -20,7 +20,7 @@ from pybulletgym_amd.vec_env import VecEnv, sample_actions
 env_id, n = "{env}", {n}
 kw = dict(gang_dist={gd})
 if {gl} > 0: kw["gang_lanes"] = {gl}
-if {pr} == 64: kw["precision"] = 64
+kw["precision"] = {pr}
 env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, **kw)
 env.reset()
 K, P = 300, 200

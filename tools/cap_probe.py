@@ -8,7 +8,7 @@ from pybulletgym_amd.vec_env import VecEnv, sample_actions
 env_id, n = sys.argv[1].split(":")
 n = int(n)
 for cap in [int(c) for c in sys.argv[2:]]:
-    env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, lds_rows=cap)
+    env = VecEnv(env_id, n, seed=0x5EED, autoreset=True, lds_rows=cap, precision=32)
     env.reset()
     K, P = 300, 200
     acts = sample_actions(env.info.action_dim, n, P + K, seed=0x5EED)

@@ -20,7 +20,7 @@ ENVS = ["HumanoidPyBulletEnv-v0", "HumanoidFlagrunPyBulletEnv-v0", "HumanoidFlag
 for env_id in ENVS:
     for n in (256, 4096):
         for lds_rows in (-1, 0):
-            env = VecEnv(env_id, n, seed=7, autoreset=True, lds_rows=lds_rows)
+            env = VecEnv(env_id, n, seed=7, autoreset=True, lds_rows=lds_rows, precision=32)
             env.reset()
             acts = sample_actions(env.info.action_dim, n, 60, seed=7)
             for i in range(60):

@@ -5,7 +5,7 @@ import torch
 import pybulletgym_amd  # noqa: F401
 from pybulletgym_amd.vec_env import VecEnv
 for env_id, n in [(a, int(b)) for a, b in (x.split(":") for x in (sys.argv[1:] or ["HumanoidPyBulletEnv-v0:4096"]))]:
-    env = VecEnv(env_id, n, seed=3, autoreset=True)
+    env = VecEnv(env_id, n, seed=3, autoreset=True, precision=32)
     env.reset()
     h = torch.zeros(64, dtype=torch.int64, device="cuda")
     hw = torch.zeros(64, dtype=torch.int64, device="cuda")  # max over each wave's 16 envs (quad kernel)

@@ -10,7 +10,7 @@ import oracle
 robots = sys.argv[1:] or ["InvertedPendulumPyBulletEnv-v0", "HopperPyBulletEnv-v0", "HalfCheetahPyBulletEnv-v0", "AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0"]
 for env_id in robots:
     n = 256
-    env = VecEnv(env_id, n, seed=1, autoreset=False)
+    env = VecEnv(env_id, n, seed=1, autoreset=False, precision=32)
     orc = oracle.OracleEnvs(env_id, n, nthreads=16)
     rng = np.random.default_rng(0)
     q0 = rng.uniform(-0.1, 0.1, (n, env.info.reset_dofs)).astype(np.float32)
@@ -34,7 +34,7 @@ for env_id in robots:
     print("   60 teacher-forced steps: obs maxdiff %.3g reward maxdiff %.3g done mismatches %d contact-count mismatches %d  last state maxdiff %.3g" % (worst, rmax, dmis, cmis, np.nanmax(sd)))
     # throughput
     N = 16384 if "Humanoid" not in env_id else 4096
-    env2 = VecEnv(env_id, N, seed=2, autoreset=True)
+    env2 = VecEnv(env_id, N, seed=2, autoreset=True, precision=32)
     env2.reset()
     acts = torch.rand((50, N, env2.info.action_dim), device="cuda") * 2 - 1
     for i in range(5): env2.step(acts[i])

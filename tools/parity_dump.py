@@ -21,7 +21,7 @@ def rel(a, b):
 
 
 def main(env_id, n, steps, tag, kernel=-1):
-    env = VecEnv(env_id, n, seed=7, autoreset=True, kernel=kernel)
+    env = VecEnv(env_id, n, seed=7, autoreset=True, kernel=kernel, precision=32)
     env.reset()
     orc = oracle.OracleEnvs(env_id, n, nthreads=16, seed=7)
     prb = oracle.OracleEnvs(env_id, n, nthreads=16, seed=7, precision=32)

@@ -25,7 +25,7 @@ def main(env_id, dump_tag, tag):
             s = st.copy()
             if rep > 0:  # relative perturbation ~1e-6 of every state word
                 s = s * (1.0 + rng.uniform(-1e-6, 1e-6, s.shape))
-            env = VecEnv(env_id, n, seed=7, autoreset=False, kernel=kernel)
+            env = VecEnv(env_id, n, seed=7, autoreset=False, kernel=kernel, precision=32)
             env.set_state(torch.from_numpy(s), torch.from_numpy(ax))
             r = env.step(torch.from_numpy(act).float().cuda())
             res.append(r.obs.cpu().numpy().copy())

@@ -13,7 +13,7 @@ cfg = [("InvertedPendulumPyBulletEnv-v0", 16384), ("HopperPyBulletEnv-v0", 4096)
 if len(sys.argv) > 1:
     cfg = [(a, int(b)) for a, b in (x.split(":") for x in sys.argv[1:])]
 for env_id, n in cfg:
-    env = VecEnv(env_id, n, seed=2, autoreset=True)
+    env = VecEnv(env_id, n, seed=2, autoreset=True, precision=32)
     env.reset()
     K = 100
     acts = torch.rand((K, n, env.info.action_dim), device="cuda") * 2 - 1
