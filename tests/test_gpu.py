@@ -581,8 +581,11 @@ def test_config_parity_1000_steps(env_id, n, sample):
 # 1,000 steps) is met by no float32 implementation of these dynamics, this one included (DESIGN.md
 # 6; the float64 path, tests/test_f64.py, holds it far longer).  After divergence the trajectories
 # are independent samples of the same dynamics, so the rest of the horizon is checked as
-# distributions: per env, the first step with done set and the mean contact count over
-# the 1,000 steps, GPU against the float64 oracle, two-sample Kolmogorov-Smirnov p >= FREE_KS_P.
+# distributions: here the mean contact count per env over the 1,000 steps, GPU against the float64
+# oracle, two-sample Kolmogorov-Smirnov p >= FREE_KS_P (the first-termination step is reported only:
+# it is near-constant under random actions; tests/test_post_divergence.py holds the
+# discriminating statistics -- episode returns / lengths with auto-reset, torso height and forward
+# velocity at steps 200-1,000).
 FREE_MEDIAN_FACTOR = 0.8
 FREE_KS_P = 0.01
 FREE_CONFIGS = [("AntPyBulletEnv-v0", 16384, 512), ("HumanoidPyBulletEnv-v0", 4096, 192)]
@@ -660,12 +663,13 @@ def test_free_running_divergence_not_earlier_than_float32(env_id, n, sample, ste
     same_fd = (fd["gpu"] == fd["f64"]).all()
     rec["ks_p_first_done"] = 1.0 if same_fd else float(stats.ks_2samp(fd["gpu"], fd["f64"]).pvalue)
     rec["ks_p_mean_contacts"] = float(stats.ks_2samp(mc["gpu"], mc["f64"]).pvalue)
+    rec["distinct_first_done_gpu_f64"] = [int(len(np.unique(fd["gpu"]))), int(len(np.unique(fd["f64"])))]
     _report(rec)
     for thr in (1e-4, 1e-2):
         g, f = np.median(first[("gpu", thr)]), np.median(first[("f32", thr)])
         assert g >= FREE_MEDIAN_FACTOR * f, (thr, g, f, rec)
     assert rec["done_mismatch_before_divergence"] == 0 and rec["contact_count_mismatch_before_divergence"] == 0, rec
-    assert rec["ks_p_first_done"] >= FREE_KS_P and rec["ks_p_mean_contacts"] >= FREE_KS_P, rec
+    assert rec["ks_p_mean_contacts"] >= FREE_KS_P, rec
 
 
 def test_free_running_short_horizon_ant():

@@ -76,7 +76,8 @@ def child(lib, out):
 def main(libs):
     outs = {}
     for lib in libs:
-        out = os.path.join(REPO, "gpurun_out", "f64_trace_" + os.path.basename(lib).replace(".so", ".npz"))
+        out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", REPO), "gpurun_out",
+                           "f64_trace_" + os.path.basename(lib).replace(".so", ".npz"))
         os.makedirs(os.path.dirname(out), exist_ok=True)
         subprocess.check_call([sys.executable, __file__, "--child", lib, out], timeout=300)
         outs[lib] = np.load(out)
@@ -86,6 +87,11 @@ def main(libs):
             bad = np.flatnonzero(~(rel <= 1e-9))
             print(f"{os.path.basename(lib)} {tag}: quad vs lane, {len(bad)} of {len(rel)} envs above 1e-9 "
                   f"(max {np.nanmax(rel):.3g}, non-finite envs {int((~np.isfinite(z[f'{tag}_quad'])).any(axis=1).sum())})")
+            if len(bad):  # which state words (base p 0-2 | quat 3-6 | v 7-9 | w 10-12 | q 13.. | qd ..)
+                w = (np.abs(z[f"{tag}_quad"] - z[f"{tag}_lane"]) / np.maximum(1.0, np.abs(z[f"{tag}_lane"]))).max(axis=0)
+                print("   per-word max rel:", np.array2string(w, precision=2, max_line_width=160))
+                print("   env 0 quad:", np.array2string(z[f"{tag}_quad"][0], precision=4, max_line_width=160))
+                print("   env 0 lane:", np.array2string(z[f"{tag}_lane"][0], precision=4, max_line_width=160))
     if len(outs) >= 2:
         (la, a), (lb, b) = list(outs.items())[:2]
         for tag in ("zero", "rand"):
