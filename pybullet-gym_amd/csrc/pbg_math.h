@@ -14,9 +14,12 @@
 #endif
 
 #define PBG_DEV __device__ __forceinline__
+#define PBG_SC64_FN __host__ __device__ __forceinline__
 
 #include <type_traits>
 #include <utility>
+
+#include "pbg_sincos64.h"
 
 // Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Guarantees a
 // constant induction variable where `#pragma unroll` may give up on big bodies.
@@ -114,8 +117,17 @@ PBG_DEV void sincos_fast(float x, float* sp, float* cp) {
   *sp = (q & 2) ? -s0 : s0;
   *cp = ((q + 1) & 2) ? -c0 : c0;
 }
-// float64: the device library's sincos (ocml, within 1 ulp), as the oracle's libm sin / cos
-PBG_DEV void sincos_fast(double x, double* sp, double* cp) { sincos(x, sp, cp); }
+// float64: Cody-Waite reduction + the msun minimax kernels (pbg_sincos64.h): within 0.8 ulp for
+// |x| <= 1e5, 1e-15 absolute to 1e6 (tests/test_sincos64.py), ~45 instructions and no branch, where the
+// device library's sincos takes ~150 with its Payne-Hanek path behind a branch (the physics' joint
+// angles and half-angle increments never need it; NaN and inf give NaN, as the library does)
+PBG_DEV void sincos_fast(double x, double* sp, double* cp) {
+#ifdef PBG_SC64_LIB  // diagnostic builds: the device library's sincos
+  sincos(x, sp, cp);
+#else
+  pbg::sincos_reduced64(x, sp, cp);
+#endif
+}
 
 // row-major 3x3
 template <class S>
@@ -198,11 +210,18 @@ PBG_DEV M3<S> quat_to_m3c(double x, double y, double z, double w) {
   R.m[6] = (S)(2 * (x * z - w * y)); R.m[7] = (S)(2 * (y * z + w * x)); R.m[8] = (S)(1 - 2 * (x * x + y * y));
   return R;
 }
+// sin / cos of the physics: the kernels' own (sincos_fast), or the device library's when LIB (the
+// float64 lane kernel, pbg_types.h F64L)
+template <bool LIB = false, class S>
+PBG_DEV void sincos_phys(S x, S* sp, S* cp) {
+  if constexpr (LIB && sizeof(S) == 8) sincos(x, sp, cp);
+  else sincos_fast(x, sp, cp);
+}
 // rotation about a constant unit axis
-template <class S>
+template <class S, bool LIB = false>
 PBG_DEV M3<S> axis_angle_m3c(nd<S> ax, nd<S> ay, nd<S> az, S ang) {
   S s, c;
-  sincos_fast(ang, &s, &c);
+  sincos_phys<LIB>(ang, &s, &c);
   const S t = 1 - c;
   M3<S> R;
   R.m[0] = kmul<S>(ax * ax, t) + c;       R.m[1] = kmul<S>(ax * ay, t) - kmul<S>(az, s); R.m[2] = kmul<S>(ax * az, t) + kmul<S>(ay, s);

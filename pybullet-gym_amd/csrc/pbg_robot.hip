@@ -17,6 +17,7 @@
 namespace pbg {
 using R = pbg_models::PBG_ROBOT;
 using R64 = F64<R>;
+using R64L = F64L<R>;  // the float64 lane kernel's robot (library sin / cos: pbg_types.h)
 
 static inline unsigned blocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
 
@@ -237,15 +238,13 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
   }
 }
 
-// ---- the float64 quad kernel (Team<R64>::ok: Ant, AntMuJoCo) is its own translation unit, compiled
-// with -DPBG_TEAM64_TU and the AMDGPU register-pressure trackers in the machine scheduler
-// (Makefile): with the default scheduler this ROCm's backend miscompiles it -- NaN velocities
-// from the first sub-step in every env, while the LLVM IR is free of undef / poison, the same
-// source with printf calls or the trackers schedule is bit-exact against the float64 lane kernel,
-// and moving the double quad permutes from DPP to ds_bpermute does not change it (DESIGN.md
-// section 4).  The float32 kernels keep the default scheduler (their ISA is unchanged).  (AntMuJoCo's
-// instance was wrong under both schedules until the float64 sub-step was reordered; with the
-// current source both instances pass the float64 parity tests.)
+// ---- the float64 quad kernel (Team<R64>::ok: Ant, AntMuJoCo) is its own translation unit
+// (-DPBG_TEAM64_TU, Makefile T64FLAGS).  Round 5 compiled it with the AMDGPU register-pressure trackers
+// in the machine scheduler: under the default schedule the round-5 source computed NaN velocities in
+// every env.  Round 6 reproduced that on the round-5 source and localised it to the pre-RA machine
+// scheduler's reordering (opt-bisect; every other schedule tried is wrong too, instrumented builds are
+// right); the current source is exact under both schedules and ships on the default one (DESIGN.md
+// section 4, tools/f64_quad_trace.py).
 template <class RR>
 constexpr bool team64_ok() { return Team<RR>::ok; }
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g);
@@ -333,12 +332,12 @@ int PBG_FN(plan64_)(int n_envs, int cus, int mode, Geometry* g) {
       return plan_gang_t<R64, 16>(n_envs, cus, g);
     }
   }
-  return plan_lane<R64>(n_envs, cus, g);
+  return plan_lane<R64L>(n_envs, cus, g);
 }
 int PBG_FN(launch_step64_)(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if (PBG_FN(launch_team64_)(B, io, scratch, g, s)) return (int)hipGetLastError();
   if (launch_gang<R64>(B, io, scratch, g, s)) return (int)hipGetLastError();
-  return launch_lane<R64>(B, io, scratch, g, s);
+  return launch_lane<R64L>(B, io, scratch, g, s);
 }
 int PBG_FN(launch_reset64_)(const Buffers& B, const ResetIO& io, hipStream_t s) {
   hipLaunchKernelGGL(reset_kernel<R64>, dim3(blocks(B.n, 64)), dim3(64), 0, s, B, io);

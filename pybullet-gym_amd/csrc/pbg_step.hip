@@ -412,7 +412,7 @@ PBG_DEV void fk_pos(const State<R>& s, Kin<R>& k, V3<real_t<R>>* ja = nullptr, V
     const f3 anl = mk3<T>((T)R::link_anchor[l][0], (T)R::link_anchor[l][1], (T)R::link_anchor[l][2]);
     constexpr int jt = R::link_jtype[l], d = R::link_dof[l];
     if constexpr (jt == 0) {
-      const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
+      const m3 Rj = axis_angle_m3c<T, lib_trig_v<R>>(axl.x, axl.y, axl.z, s.q[d]);
       k.Rm[l + 1] = mul(R0, Rj);
       k.x[l + 1] = x0 + mul(R0, anl - mulc(Rj, anl));
       if constexpr (AXES) { ja[d] = mulc(R0, axl); jo[d] = x0 + mulc(R0, anl); }
@@ -619,7 +619,7 @@ PBG_DEV void dyn_mass(const State<R>& s, const real_t<R>* tau, real_t<R>* L, rea
         const f3 axl = mk3<T>((T)R::link_axis[l][0], (T)R::link_axis[l][1], (T)R::link_axis[l][2]);
         const f3 anl = mk3<T>((T)R::link_anchor[l][0], (T)R::link_anchor[l][1], (T)R::link_anchor[l][2]);
         if constexpr (jt == 0) {
-          const m3 Rj = axis_angle_m3c(axl.x, axl.y, axl.z, s.q[d]);
+          const m3 Rj = axis_angle_m3c<T, lib_trig_v<R>>(axl.x, axl.y, axl.z, s.q[d]);
           k.Rm[b] = mul(R0, Rj);
           k.x[b] = x0 + mul(R0, anl - mulc(Rj, anl));
         } else if constexpr (jt == 1) {
@@ -818,13 +818,13 @@ PBG_DEV void dynamics(const State<R>& s, const real_t<R>* tau, real_t<R>* L, rea
 
 // exponential-map quaternion update of a free body (the floating base, the cube) with its
 // world angular velocity  [EXT] btMultiBody pQuatUpdateFun
-template <class S>
+template <bool LIB = false, class S>
 PBG_DEV void free_body_quat(S* q, V3<S> wv, const SimPT<S>& P) {
   const S dt = P.dt;
   S ang = norm3(wv);
   if (ang * dt > (S)PBG_ANGULAR_MOTION_THRESHOLD) ang = P.ang_max;
   S sh, dw;
-  sincos_fast(S(0.5f) * ang * dt, &sh, &dw);
+  sincos_phys<LIB>(S(0.5f) * ang * dt, &sh, &dw);
   V3<S> ax;
   if (ang < S(0.001)) ax = (S(0.5f) * dt - P.dt3c * ang * ang) * wv;
   else ax = (sh / ang) * wv;
@@ -882,7 +882,7 @@ PBG_DEV void cube_integrate(State<R>& s, const real_t<R>* uc, const SimPT<real_t
       s.cube.w[i] = clampf(uc[3 + i] * rI, -vmax, vmax);
       s.cube.p[i] += P.dt * s.cube.v[i];
     }
-    free_body_quat(s.cube.q, mk3<T>(s.cube.w[0], s.cube.w[1], s.cube.w[2]), P);
+    free_body_quat<lib_trig_v<R>>(s.cube.q, mk3<T>(s.cube.w[0], s.cube.w[1], s.cube.w[2]), P);
   } else {
     (void)s; (void)uc; (void)P;
   }
@@ -926,7 +926,7 @@ PBG_DEV void integrate(State<R>& s, const real_t<R>* L, const real_t<R>* Ld, con
       s.bw[i] = nu[NJ + 3 + i];
       s.bp[i] += dt * s.bv[i];
     }
-    free_body_quat(s.bq, mk3<T>(s.bw[0], s.bw[1], s.bw[2]), P);
+    free_body_quat<lib_trig_v<R>>(s.bq, mk3<T>(s.bw[0], s.bw[1], s.bw[2]), P);
   }
 }
 

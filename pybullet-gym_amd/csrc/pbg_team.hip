@@ -1483,11 +1483,21 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     s.q[j] = st_of<R>(B)[(size_t)(SB + kb * NDB + j) * B.n + e];
     s.qd[j] = st_of<R>(B)[(size_t)(SB + R::NJ + kb * NDB + j) * B.n + e];
   }
-  // the pack's bookkeeping loads, issued here so their latency overlaps the physics
-  const int el = B.elapsed[e] + 1;
-  uint32_t flags = B.flags[e];
-  const double pot_old = B.pot[e];
-  const Sc z0_old = z0_of<R>(B)[e];
+  // the pack's bookkeeping loads: float32 issues them here so their latency overlaps the physics;
+  // float64 after the physics, and it re-reads the actions there too (the registers those values would
+  // hold through the sub-steps are the ones its physics spills for)
+  constexpr bool LATE = sizeof(Sc) == 8;
+  int el = 0;
+  uint32_t flags = 0;
+  double pot_old = 0.0;
+  Sc z0_old = 0.f;
+  auto book = [&]() {
+    el = B.elapsed[e] + 1;
+    flags = B.flags[e];
+    pot_old = B.pot[e];
+    z0_old = z0_of<R>(B)[e];
+  };
+  if constexpr (!LATE) book();
   float act[R::NA];
 #pragma unroll
   for (int i = 0; i < R::NA; i++) act[i] = io.act[(size_t)e * R::NA + i];
@@ -1528,6 +1538,13 @@ __global__ __launch_bounds__(64) void team_step_kernel(Buffers B, StepIO io, flo
     sig += (uint32_t)qperm_i<0xB1>((int)sig);
     sig += (uint32_t)qperm_i<0x4E>((int)sig);
     if (kb == 0) io.csig[e] = sig;
+  }
+  if constexpr (LATE) {
+    book();
+    const float* ap = io.act;
+    asm volatile("" : "+s"(ap));  // a fresh pointer: the loads are not merged with the ones above
+#pragma unroll
+    for (int i = 0; i < R::NA; i++) act[i] = ap[(size_t)e * R::NA + i];
   }
   // feet contact flags of the last sub-step: this branch's feet, OR-ed over the quad
   uint32_t fb = 0;

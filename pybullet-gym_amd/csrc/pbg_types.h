@@ -64,6 +64,26 @@ template <class R0>
 struct F64 : R0 {
   using real = double;
 };
+// F64L<R>: the float64 robot as the LANE kernel instantiates it -- the same tables and scalar, with the
+// device library's sin / cos in the physics (lib_trig).  The float64 lane kernels of the Humanoid family
+// (7 KB of scratch per lane) computed wrong states with the float64 kernels' own sincos
+// (pbg_sincos64.h) under both machine schedules, while the gang kernels running the same function on
+// the same inputs stay within 1e-9 of the oracle: the lane kernel, the parity
+// cross-check of the others, keeps the trigonometry it was validated with.
+template <class R0>
+struct F64L : F64<R0> {
+  static constexpr bool lib_trig = true;
+};
+template <class R, class = void>
+struct LibTrig {
+  static constexpr bool value = false;
+};
+template <class R>
+struct LibTrig<R, std::void_t<decltype(R::lib_trig)>> {
+  static constexpr bool value = R::lib_trig;
+};
+template <class R>
+inline constexpr bool lib_trig_v = LibTrig<R>::value;
 
 struct Buffers {
   int n;                   // envs on this device

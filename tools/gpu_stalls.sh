@@ -6,7 +6,7 @@ TAG=${1:-stalls}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-for W in ${PROF_ROBOTS:-ant humanoid ant_f64}; do
+for W in ${PROF_ROBOTS:-ant humanoid ant_f64 humanoid_f64}; do
   case $W in
     ant) A="--env AntPyBulletEnv-v0 --envs-per-gpu 16384 --precision 32";;
     humanoid) A="--env HumanoidPyBulletEnv-v0 --envs-per-gpu 4096 --precision 32";;

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../pybullet-gym_amd"
 TAG=$1; shift
 mkdir -p build/obj_var
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -DPBG_TEAM64_TU \
-  -mllvm -amdgpu-use-amdgpu-trackers=1 "$@" -DPBG_ROBOT=Ant -c -o build/obj_var/team64_Ant_$TAG.o csrc/pbg_robot.hip
+  "$@" -DPBG_ROBOT=Ant -c -o build/obj_var/team64_Ant_$TAG.o csrc/pbg_robot.hip
 objs=$(ls build/obj/*.o | grep -v "/team64_Ant.o$")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o libpbg_$TAG.so build/obj_var/team64_Ant_$TAG.o $objs
 echo built libpbg_$TAG.so
