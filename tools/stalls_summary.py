@@ -15,7 +15,8 @@ import sys
 src, rnd = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 res = {}
-WORK = (("ant", "pbg_models::Ant", False), ("humanoid", "pbg_models::Humanoid", False), ("ant_f64", "pbg_models::Ant", True))
+WORK = (("ant", "pbg_models::Ant", False), ("humanoid", "pbg_models::Humanoid", False), ("ant_f64", "pbg_models::Ant", True),
+        ("humanoid_f64", "pbg_models::Humanoid", True))
 for w, key, f64 in WORK:
     if not glob.glob(os.path.join(src, w, "pmc_wait", "**", "*counter_collection.csv"), recursive=True):
         continue
