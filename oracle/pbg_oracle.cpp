@@ -113,6 +113,7 @@ struct MV {
   int robot_id, kind, floating, NL, NJ, NDOF, NA, NO, NR, NF, NP, NS, NPAIR, OBS, alive, substeps,
       floor, max_steps, robot_body, tip_link, flagrun, harder, NCG, head_link;
   double power, elec, stall, jal, z0fixed, dt_sub, base_mass, power_cost, qvel_clip, contact_erp, cube_floor_mu;
+  double restitution, spin_mu, roll_mu;  // robot x floor material (codegen.py: Bullet's combiners)
   const double *base_inertia, *base_pos, *base_quat;
   const int *link_parent, *link_jtype, *link_dof;
   const double (*off_pos)[3], (*axis)[3], (*anchor)[3], (*com)[3], (*off_quat)[4], (*inertia)[6];
@@ -140,7 +141,8 @@ MV view() {
   m.cg_link = R::cgeom_link; m.cg_p0 = R::cgeom_p0; m.cg_p1 = R::cgeom_p1; m.cg_r = R::cgeom_r; m.cg_mu = R::cgeom_mu;
   m.power = R::power; m.elec = R::electricity_cost; m.stall = R::stall_torque_cost;
   m.jal = R::joints_at_limit_cost; m.z0fixed = R::initial_z_fixed; m.dt_sub = R::dt_sub;
-  m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.contact_erp = R::contact_erp; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
+  m.base_mass = R::base_mass; m.power_cost = R::power_cost; m.qvel_clip = R::qvel_clip; m.contact_erp = R::contact_erp;
+  m.restitution = R::restitution; m.spin_mu = R::spin_mu; m.roll_mu = R::roll_mu; m.base_inertia = R::base_inertia; m.base_pos = R::base_pos;
   m.base_quat = R::base_quat; m.link_parent = R::link_parent; m.link_jtype = R::link_jtype;
   m.link_dof = R::link_dof; m.off_pos = R::link_offset_pos; m.axis = R::link_axis;
   m.anchor = R::link_anchor; m.com = R::link_com; m.off_quat = R::link_offset_quat;

@@ -737,7 +737,40 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
     const bool deep = dist <= T(g_opt[OPT_DEEP_THR]);
     const double e = deep ? (g_opt[OPT_DEEP_MODE] != 0.0 ? -1.0 : deep_erp) : erp;
     setup_row(n, M, nu, r, dist, 1, e, dt, g_opt[OPT_SEP_ABS] != 0.0, g_opt[OPT_CONTACT_CFM]);
+    // restitution of a robot-floor contact (HalfCheetahMuJoCo: 0.5 x 0.5): [EXT]
+    // btMultiBodyConstraintSolver::setupMultiBodyContactConstraint takes restitutionCurve(rel_vel) of
+    // the pre-solve normal velocity -- e * (-v_n) when |v_n| >= the threshold, clamped at 0 -- into
+    // velocityError = restitution - rel_vel, i.e. the target of J nu_new rises by it
+    if (m.restitution > 0.0 && cts[c].body_b == -1 && cts[c].body_a != CUBE_BODY) {
+      const T vn = dotn(n, r.J, nu);
+      const T av = vn < T(0) ? T(0) - vn : vn;
+      const T rest = av < T(PBG_RESTITUTION_VELOCITY_THRESHOLD) ? T(0) : T(m.restitution) * (T(0) - vn);
+      if (rest > T(0)) r.target = r.target + rest;
+    }
     r.lo = T(0); r.hi = T(1e30); r.normal = -1; r.mu = cts[c].mu;
+  }
+  // spinning (about the normal) and rolling (about the two tangents) friction: angular rows of
+  // the robot-floor contacts, bounded by +-mu_t lambda_n under a positive normal impulse, solved
+  // after the normals and before the lateral friction ([EXT] btMultiBodyConstraintSolver's
+  // torsional friction constraints, addMultiBodyTorsionalFrictionConstraint: angular Jacobian,
+  // zero target).  mu_t: the model's combined coefficients (HalfCheetahMuJoCo 0.1 x 0.8); the rule
+  // study's OPT_SPIN_MU / OPT_ROLL_MU override them for every robot.
+  const double spin = g_opt[OPT_SPIN_MU] > 0.0 ? g_opt[OPT_SPIN_MU] : m.spin_mu;
+  const double roll = g_opt[OPT_ROLL_MU] > 0.0 ? g_opt[OPT_ROLL_MU] : m.roll_mu;
+  const int first_torsion = nr;
+  if (spin > 0.0 || roll > 0.0) {
+    for (int c = 0; c < nc; c++) {
+      V3T<T> t1, t2;
+      plane_space(cts[c].n, t1, t2);
+      for (int a = 0; a < 3; a++) {
+        const double mu = a == 0 ? spin : roll;
+        if (!(mu > 0.0)) continue;
+        RowT<T>& r = rows[nr++];
+        contact_angular_jacobian(m, k, cts[c], a == 0 ? cts[c].n : (a == 1 ? t1 : t2), r.J);
+        setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false, g_opt[OPT_CONTACT_CFM]);
+        r.normal = first_normal + c; r.mu = T(mu); r.lo = r.hi = T(0);
+      }
+    }
   }
   int first_friction = nr;
   const int fric_dirs = g_opt[OPT_FRIC_MODE] == 2.0 ? 1 : 2;
@@ -749,24 +782,6 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
       contact_row_jacobian(m, k, cts[c], f == 0 ? t1 : t2, r.J);
       setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false, g_opt[OPT_CONTACT_CFM]);
       r.normal = first_normal + c; r.mu = cts[c].mu; r.lo = r.hi = T(0);
-    }
-  }
-  // rule study: spinning (about the normal) and rolling (about the tangents) friction rows,
-  // solved after the friction rows under the same positive-normal rule, bounded by mu * lambda_n
-  // (btMultiBodyConstraintSolver's torsional friction constraints)
-  const double spin = g_opt[OPT_SPIN_MU], roll = g_opt[OPT_ROLL_MU];
-  if (spin > 0.0 || roll > 0.0) {
-    for (int c = 0; c < nc; c++) {
-      V3T<T> t1, t2;
-      plane_space(cts[c].n, t1, t2);
-      for (int a = 0; a < 3; a++) {
-        const double mu = a == 0 ? spin : roll;
-        if (!(mu > 0.0)) continue;
-        RowT<T>& r = rows[nr++];
-        contact_angular_jacobian(m, k, cts[c], a == 0 ? cts[c].n : (a == 1 ? t1 : t2), r.J);
-        setup_row(n, M, nu, r, T(0), 0, 0.0, dt, false);
-        r.normal = first_normal + c; r.mu = T(mu); r.lo = r.hi = T(0);
-      }
     }
   }
   // warm start: last sub-step's impulses of the same candidates (Bullet's persistent
@@ -796,12 +811,19 @@ int substep(const MV& m, T* s, const T* tau, uint8_t* slot_active, int sub, uint
   };
   auto crow = [&](int i) {  // the event row id of constraint row i
     if (i < first_normal) return i;
-    if (i < first_friction) return first_normal + 3 * (i - first_normal);
+    if (i < first_torsion) return first_normal + 3 * (i - first_normal);
     const int c = (i - first_friction) / fric_dirs;
     return first_normal + 3 * c + 1 + (i - first_friction - fric_dirs * c);
   };
   for (int it = 0; it < iters; it++) {
-    for (int i = 0; i < first_friction; i++) event(it, crow(i), solve_row(n, rows[i], nu));
+    for (int i = 0; i < first_torsion; i++) event(it, crow(i), solve_row(n, rows[i], nu));
+    for (int i = first_torsion; i < first_friction; i++) {  // torsional rows (no solver events)
+      const T ln = rows[rows[i].normal].lambda;
+      if (!(ln > T(0))) continue;
+      rows[i].lo = T(0) - rows[i].mu * ln;
+      rows[i].hi = rows[i].mu * ln;
+      solve_row(n, rows[i], nu);
+    }
     for (int i = first_friction; i < nr; i += (cone ? 2 : 1)) {
       T ln = rows[rows[i].normal].lambda;
       if (!(ln > T(0)) && (i - first_friction) % fric_dirs == 0) event(it, crow(i), 3u);

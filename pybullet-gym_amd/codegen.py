@@ -274,6 +274,10 @@ def build_tables(spec: robots.RobotSpec, model: mjcf.RobotModel, ov: Dict = None
         cgeom_r=[g[1].radius for g in cgeoms], cgeom_mu=[g[1].friction * CUBE_FRICTION for g in cgeoms],
         cube_floor_mu=(CUBE_FRICTION * floor_mu if spec.harder else 0.0),
         contact_erp=float(ov.get("contact_erp", CONTACT_ERP_DEFAULT)),
+        # robot-floor material, Bullet's btManifoldResult combiners: restitution r_a r_b; spinning
+        # and rolling friction s_a mu_b + mu_a s_b (the floor has none of its own: s_b = 0)
+        restitution=spec.restitution * mjcf.FLOOR_RESTITUTION,
+        spin_mu=spec.spinning_friction * floor_mu, roll_mu=spec.rolling_friction * floor_mu,
     )
     return t
 
@@ -329,7 +333,8 @@ def emit_struct(t: Dict) -> str:
               "floor", "max_episode_steps", "robot_body", "tip_link", "flagrun", "harder", "NCG", "head_link"):
         L.append(f"  static constexpr int {k} = {int(t[k])};")
     for k in ("power", "electricity_cost", "stall_torque_cost", "joints_at_limit_cost",
-              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp", "cube_floor_mu"):
+              "initial_z_fixed", "dt_sub", "base_mass", "power_cost", "qvel_clip", "contact_erp", "cube_floor_mu",
+              "restitution", "spin_mu", "roll_mu"):
         L.append(f"  static constexpr double {k} = {_num(t[k])};")
     L.append(_arr1("base_inertia", "double", t["base_inertia"]))
     L.append(_arr1("base_pos", "double", t["base_pos"]))

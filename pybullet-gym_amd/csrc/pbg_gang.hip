@@ -457,7 +457,10 @@ struct Gang {
   static constexpr bool LIM_WS = gang_big<R>() || R::harder;
   static constexpr int LRSZ = (!LIM_WS && NLIM * LRW > NB * CW) ? NLIM * LRW : NB * CW;
   static constexpr int FIXED = O_LR + LRSZ + (Y64 ? ((O_LR + LRSZ + RW0) & 1) : 0);  // Y64: rows start even
-  static constexpr int PERC = RW0 + 3 * CRW + (Y64 ? ((RW0 + 3 * CRW) & 1) : 0);
+  // rows per contact: normal, 2 lateral friction (+ spinning, 2 rolling: HalfCheetahMuJoCo's links)
+  static constexpr int NRC = (R::spin_mu > 0.0 || R::roll_mu > 0.0) ? 6 : 3;
+  static_assert(NRC == 3 || (!R::harder && R::NPAIR == 0), "torsional rows: robot-floor contacts only");
+  static constexpr int PERC = RW0 + NRC * CRW + (Y64 ? ((RW0 + NRC * CRW) & 1) : 0);
   // the kinematic parts are dead once M and the bias are built, before any contact is
   // written: they share the start of the contact area (the env region holds >= KW*NB words)
   static constexpr int O_KV = KAL ? al4(FIXED) : FIXED;
@@ -631,6 +634,16 @@ PBG_DEV real_t<R> gang_fric_limit(const GangCtx<R>& X, int c) {
   const Sc* p = X.g + coff<R, T>(c);
   return p[G::DW] * p[w];
 }
+// lambda of contact c's normal row
+template <class R, int T, bool LDS>
+PBG_DEV real_t<R> gang_normal_lam(const GangCtx<R>& X, int c) {
+  using Sc = real_t<R>;
+  using LW = lds_t<Sc>;
+  using G = Gang<R, T>;
+  constexpr int w = G::RW0 + G::YS + 2;
+  if (LDS || c < X.cap) return X.l[G::FIXED + coff<R, T>(c) + w];
+  return X.g[coff<R, T>(c) + w];
+}
 template <class R, int T, bool LDS>
 PBG_DEV void gang_set_lam(const GangCtx<R>& X, int c, int dir, real_t<R> v) {
   using Sc = real_t<R>;
@@ -681,13 +694,27 @@ PBG_DEV void gang_contact_sweep(const GangCtx<R>& X, int nc, real_t<R>* us) {
   // branch-free (selects over the words) -- the 64-bit mask with a branch per word cost 6-8 %
   // of the step; the three-word selects of the Humanoid's 95 candidates were 12 of a normal
   // row's ~50 instructions, hence the one-word instantiation for the common case
-  if constexpr (NW > 4) {
-    // more than 128 contact candidates (Atlas): the plain order -- every normal, then the two
-    // friction rows of each contact whose normal impulse came out positive, a load-then-test
+  if constexpr (NW > 4 || G::NRC == 6) {
+    // more than 128 contact candidates (Atlas), or torsional rows (HalfCheetahMuJoCo): the plain
+    // order -- every normal, [the spinning and rolling rows,] then the two friction rows of each
+    // contact whose normal impulse came out positive, a load-then-test
     for (int c = 0; c < nc; c++) {
       Row A;
       gang_load_row<R, T, LDS>(X, c, 0, A);
       gang_set_lam<R, T, LDS>(X, c, 0, gang_update<R, T>(A, us, 0.f, 3.0e38f));
+    }
+    if constexpr (G::NRC == 6) {  // +-mu_t lambda_n, before the lateral friction (the oracle's order)
+      for (int c = 0; c < nc; c++) {
+        const Sc ln = gang_normal_lam<R, T, LDS>(X, c);
+        if (!(ln > 0.f)) continue;
+#pragma unroll
+        for (int dir = 3; dir < 6; dir++) {
+          const Sc lim = (Sc)(dir == 3 ? R::spin_mu : R::roll_mu) * ln;
+          Row A;
+          gang_load_row<R, T, LDS>(X, c, dir, A);
+          gang_set_lam<R, T, LDS>(X, c, dir, gang_update<R, T>(A, us, -lim, lim));
+        }
+      }
     }
     for (int c = 0; c < nc; c++) {
       const Sc lim = gang_fric_limit<R, T, LDS>(X, c);
@@ -1962,7 +1989,7 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
   const int njobs = 0;
 #else
   // (HumanoidFlagrunHarder: the cube's floor contacts are built by cube_floor_rows below)
-  const int njobs = NLIM + 3 * (nc - ncf);
+  const int njobs = NLIM + G::NRC * (nc - ncf);
 #endif
   // the front path holds its staged factor in registers for the rows pass unless it is too big to
   // (Atlas: the register copy spilled 1.2 KB per lane; its rows read the LDS words instead) or the
@@ -1984,8 +2011,8 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
 #pragma unroll
       for (int i = 0; i < N; i++) J[i] = i == g ? 1.f : 0.f;
     } else {
-      c = (j - NLIM) / 3;
-      dir = (j - NLIM) - 3 * c;
+      c = (j - NLIM) / G::NRC;
+      dir = (j - NLIM) - G::NRC * c;
       if constexpr (R::harder) c += c >= nr ? ncf : 0;
       Sc v[G::DW];
       contact_at<R, T>(X, c, [&](auto p) {
@@ -2007,7 +2034,9 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
         t1 = mk3<Sc>(-nrm.y * kinv, nrm.x * kinv, 0);
         t2 = mk3<Sc>(-nrm.z * t1.y, nrm.z * t1.x, a2 * kinv);
       }
-      const V3<Sc> nd = dir == 0 ? nrm : (dir == 1 ? t1 : t2);
+      // rows 3-5 (NRC = 6): spinning about n, rolling about t1, t2 -- angular Jacobians
+      const int ax = G::NRC == 6 && dir >= 3 ? dir - 3 : dir;
+      const V3<Sc> nd = ax == 0 ? nrm : (ax == 1 ? t1 : t2);
       const V3<Sc> mmA = cross3(rA, nd), mmB = cross3(rB, nd);
       cubef = v[15];
       cubes = mk3<Sc>(0, 0, 0);
@@ -2026,8 +2055,13 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
         const V3<Sc> sw = mk3<Sc>(X.l[G::O_SW + G::SS * i], X.l[G::O_SW + G::SS * i + 1], X.l[G::O_SW + G::SS * i + 2]);
         const V3<Sc> sv = mk3<Sc>(X.l[G::O_SV + G::SS * i], X.l[G::O_SV + G::SS * i + 1], X.l[G::O_SV + G::SS * i + 2]);
         Sc tj = 0.f;
-        if (inA) tj += dot3(nd, sv) + dot3(mmA, sw);
-        if (inB) tj -= dot3(nd, sv) + dot3(mmB, sw);
+        if (G::NRC == 6 && dir >= 3) {
+          if (inA) tj += dot3(nd, sw);
+          if (inB) tj -= dot3(nd, sw);
+        } else {
+          if (inA) tj += dot3(nd, sv) + dot3(mmA, sw);
+          if (inB) tj -= dot3(nd, sv) + dot3(mmB, sw);
+        }
         J[i] = tj;
       }
     }
@@ -2057,7 +2091,18 @@ PBG_DEV int gang_substep(State<R>& s, const real_t<R>* tau, const GangCtx<R>& X,
       });
     } else {
       const int w0r = G::RW0 + dir * G::CRW;
-      const Sc tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
+      Sc tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : 0.f;
+      if constexpr (R::restitution > 0.0) {
+        // restitution (sim_params.h): e (-v_n) when |v_n| >= the threshold, v_n = J nu = y.u before the solve
+        static_assert(R::NPAIR == 0 && !R::harder, "restitution: robot-floor contacts only");
+        if (dir == 0) {
+          Sc vn = 0.f;
+#pragma unroll
+          for (int i = 0; i < N; i++) vn += y[i] * X.l[G::O_U + i];
+          const Sc rest = tabs(vn) < Sc(PBG_RESTITUTION_VELOCITY_THRESHOLD) ? Sc(0) : Sc(R::restitution) * -vn;
+          tgt += rest > Sc(0) ? rest : Sc(0);
+        }
+      }
       contact_at<R, T>(X, c, [&](auto p0) {
         auto p = p0 + w0r;
         const Sc yc[6] = {ycl.x, ycl.y, ycl.z, cubes.x, cubes.y, cubes.z};

@@ -461,7 +461,11 @@ struct Rows {
   using D = Dims<R>;
   using T = real_t<R>;
   static constexpr int N = D::NY, W = N + 3;  // contact row: y | meff | target | lambda (N: robot [+ cube])
-  static constexpr int MR = 3 * D::NC > 0 ? 3 * D::NC : 1;
+  // rows per contact: normal, 2 lateral friction (+ spinning, 2 rolling: robots whose links carry
+  // torsional friction, HalfCheetahMuJoCo); contact c's rows are NRC c + dir
+  static constexpr int NRC = (R::spin_mu > 0.0 || R::roll_mu > 0.0) ? 6 : 3;
+  static_assert(NRC == 3 || (!R::harder && R::NPAIR == 0), "torsional rows: robot-floor contacts only");
+  static constexpr int MR = NRC * D::NC > 0 ? NRC * D::NC : 1;
   static constexpr int NC = D::NC > 0 ? D::NC : 1;
   static constexpr int WORDS = MR * W;  // global workspace words per env
   static constexpr int ls = LS;  // LDS stride = lanes per workgroup
@@ -971,7 +975,7 @@ PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const V3<real_t<R>
       T D2 = 0.f;
 #pragma unroll
       for (int i = N; i < NY; i++) D2 += y[i] * y[i];
-      rw.put(3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(p.z, P.k_contact, P.k_sep) : T(0));
+      rw.put(Rows<R, LS>::NRC * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(p.z, P.k_contact, P.k_sep) : T(0));
     }
     rw.mu(nc) = (T)R::cube_floor_mu;
     nc++;
@@ -1064,7 +1068,7 @@ PBG_DEV int cube_contacts(const State<R>& s, const Kin<R>& k, const V3<real_t<R>
       y[N + 3] = -mB.x * rI; y[N + 4] = -mB.y * rI; y[N + 5] = -mB.z * rI;
 #pragma unroll
       for (int i = N; i < NY; i++) D2 += y[i] * y[i];
-      rw.put(3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(dist, P.k_contact, P.k_sep) : T(0));
+      rw.put(Rows<R, LS>::NRC * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), dir == 0 ? pos_target(dist, P.k_contact, P.k_sep) : T(0));
     }
     rw.mu(nc) = (T)R::cgeom_mu[g];
     nc++;
@@ -1121,6 +1125,8 @@ PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, co
   });
   STAMP(3)
   constexpr int first_normal = 0;
+  constexpr int NRC = Rows<R, LS>::NRC;  // rows per contact
+  static_assert(R::restitution == 0.0 || (R::NPAIR == 0 && !R::harder), "restitution: robot-floor contacts only");
   int nc = 0;
   // positions, joint axes and motion vectors again: recomputing them is cheaper than
   // keeping phase A's copies live through the factorisation
@@ -1144,13 +1150,16 @@ PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, co
     const f3 rP = cp - O;
     const int lnk = R::slot_link[sl];
 #pragma unroll
-    for (int dir = 0; dir < 3; dir++) {
-      // n = +z, t1 = (0,-1,0), t2 = (1,0,0)  (btPlaneSpace1 of +z)
-      const f3 nd = dir == 0 ? mk3<T>(0, 0, 1) : (dir == 1 ? mk3<T>(0, -1, 0) : mk3<T>(1, 0, 0));
+    for (int dir = 0; dir < NRC; dir++) {
+      // n = +z, t1 = (0,-1,0), t2 = (1,0,0)  (btPlaneSpace1 of +z); rows 3-5 (NRC = 6): the
+      // spinning and rolling rows about n, t1, t2, an angular Jacobian
+      const int ax = dir < 3 ? dir : dir - 3;
+      const f3 nd = ax == 0 ? mk3<T>(0, 0, 1) : (ax == 1 ? mk3<T>(0, -1, 0) : mk3<T>(1, 0, 0));
       const f3 mm = cross3(rP, nd);
       T Jr[N];
 #pragma unroll
-      for (int i = 0; i < N; i++) Jr[i] = D::in_chain(i, lnk) ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : T(0);
+      for (int i = 0; i < N; i++)
+        Jr[i] = !D::in_chain(i, lnk) ? T(0) : (dir < 3 ? dot3(nd, sv[i]) + dot3(mm, sw[i]) : dot3(nd, sw[i]));
       T y[NY];
 #pragma unroll
       for (int i = N; i < NY; i++) y[i] = 0.f;
@@ -1166,8 +1175,18 @@ PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, co
       T D2 = 0.f;
 #pragma unroll
       for (int i = 0; i < N; i++) { D2 += y[i] * y[i]; }
-      rw.put(first_normal + 3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0),
-             dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : T(0));
+      T tgt = dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : T(0);
+      if constexpr (R::restitution > 0.0) {
+        // restitution (sim_params.h): e (-v_n) when |v_n| >= the threshold, v_n = J nu = y.u before the solve
+        if (dir == 0) {
+          T vn = 0.f;
+#pragma unroll
+          for (int i = 0; i < N; i++) vn += y[i] * u[i];
+          const T rest = tabs(vn) < T(PBG_RESTITUTION_VELOCITY_THRESHOLD) ? T(0) : T(R::restitution) * -vn;
+          tgt += rest > T(0) ? rest : T(0);
+        }
+      }
+      rw.put(first_normal + NRC * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0), tgt);
     }
     rw.mu(nc) = (T)R::slot_mu[sl];
     nc++;
@@ -1250,7 +1269,7 @@ PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, co
           D2 += y[i] * y[i];
          
         }
-        rw.put(first_normal + 3 * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0),
+        rw.put(first_normal + NRC * nc + dir, y, D2 > T(1e-12) ? fast_rcp(D2) : T(0),
                dir == 0 ? (pos_target(dist, P.k_contact, P.k_sep)) : T(0));
       }
       rw.mu(nc) = (T)R::pair_mu[pp];
@@ -1291,13 +1310,23 @@ PBG_DEV int substep(State<R>& s, const real_t<R>* tau, uint32_t* slot_active, co
       for (int i = 0; i < N; i++)
         if (D::LIMPOS.v[li][i] >= 0) u[i] += yv[i] * dl;
     });
-    for (int c = 0; c < nc; c++) rw.solve(first_normal + 3 * c, u, T(0), T(3.0e38f));   // contact normals
+    for (int c = 0; c < nc; c++) rw.solve(first_normal + NRC * c, u, T(0), T(3.0e38f));   // contact normals
+    if constexpr (NRC == 6) {  // spinning, rolling: +-mu_t lambda_n, before the lateral friction (oracle order)
+      for (int c = 0; c < nc; c++) {
+        const T ln = rw.lam(first_normal + NRC * c);
+        if (!(ln > T(0))) continue;
+        const T ls = (T)R::spin_mu * ln, lr = (T)R::roll_mu * ln;
+        rw.solve(first_normal + NRC * c + 3, u, -ls, ls);
+        rw.solve(first_normal + NRC * c + 4, u, -lr, lr);
+        rw.solve(first_normal + NRC * c + 5, u, -lr, lr);
+      }
+    }
     for (int c = 0; c < nc; c++) {                                                  // frictions
-      const T ln = rw.lam(first_normal + 3 * c);
+      const T ln = rw.lam(first_normal + NRC * c);
       if (!(ln > T(0))) continue;  // [EXT] friction rows only under a positive normal impulse
       const T lim = rw.mu(c) * ln;
-      rw.solve(first_normal + 3 * c + 1, u, -lim, lim);
-      rw.solve(first_normal + 3 * c + 2, u, -lim, lim);
+      rw.solve(first_normal + NRC * c + 1, u, -lim, lim);
+      rw.solve(first_normal + NRC * c + 2, u, -lim, lim);
     }
   }
 

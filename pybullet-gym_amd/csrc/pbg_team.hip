@@ -136,6 +136,8 @@ struct Team {
       if (R::foot_link[f] < 0) return false;
     for (int i = 0; i < R::NA; i++)
       if (R::act_dof[i] < 0 || R::act_dof[i] >= NJ) return false;
+    // no restitution or torsional friction rows (the gang and lane kernels model them)
+    if (R::restitution != 0.0 || R::spin_mu != 0.0 || R::roll_mu != 0.0) return false;
     return true;
   }
   static constexpr bool ok = check();

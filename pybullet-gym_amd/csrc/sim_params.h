@@ -19,7 +19,11 @@
 #define PBG_ANGULAR_DAMPING 0.04        // [EXT] btMultiBody m_angularDamping (k1 = k2)
 #define PBG_MAX_COORD_VELOCITY 100.0    // [EXT] btMultiBody m_maxCoordinateVelocity
 #define PBG_ANGULAR_MOTION_THRESHOLD 0.7853981633974483  // [EXT] 0.5*SIMD_HALF_PI
-#define PBG_WALK_TARGET_X 1000.0        // robot_locomotors.py:12 walk_target_x = 1e3
+// Restitution (models_gen.h restitution, the combined robot x floor coefficient e): a contact
+// normal's target gains e * (-v_n) when the approach speed |v_n| >= the threshold
+// [EXT] btSequentialImpulseConstraintSolver::restitutionCurve, btContactSolverInfo::m_restitutionVelocityThreshold
+#define PBG_RESTITUTION_VELOCITY_THRESHOLD 0.2
+#define PBG_WALK_TARGET_X 1000.0       // robot_locomotors.py:12 walk_target_x = 1e3
 #define PBG_WALK_TARGET_Y 0.0           // robot_locomotors.py:13
 // HumanoidFlagrun (robot_locomotors.py:203-213): flag at U(+-halflen) x U(+-halfwidth) times
 // 0.5, re-drawn when the walk target is within 1 m or after 600 / frame_skip calc_states

@@ -30,7 +30,9 @@ unpinned by anything in this container):
   exclude every ancestor pair (URDF_USE_SELF_COLLISION_EXCLUDE_ALL_PARENTS,
   ``robot_bases.py:116``).
 * B5 friction: geom friction[0] times the floor's lateral friction 0.8
-  (``scene_stadium.py:33``); restitution 0 x 0.5 = 0.
+  (``scene_stadium.py:33``); restitution 0 x 0.5 = 0, except where the env sets the links'
+  material itself (HalfCheetahMuJoCo: restitution 0.5 x 0.5, spinning and rolling friction
+  0.1 x 0.8 -- codegen.py).
 * B6 damping: the joint element's own ``damping`` attribute, applied as -d*qdot from each
   sub-step's velocity (pybullet applies it per stepSimulation; per sub-step is the stable
   choice at dt/4); a ``<default><joint damping=..>`` is not inherited (pybullet's importer takes
@@ -70,6 +72,7 @@ GEOM_BOX = 2       # URDF robots (urdf.py): half extents + rotation in the link 
 GEOM_CYLINDER = 3  # URDF robots: a Z cylinder, p0 / p1 its cap centres
 
 FLOOR_FRICTION = 0.8  # scene_stadium.py:33
+FLOOR_RESTITUTION = 0.5  # scene_stadium.py:33
 
 
 # ----------------------------------------------------------------------------- math

@@ -64,6 +64,11 @@ class RobotSpec:
     knees: Optional[List[str]] = None                            # Atlas alive_bonus: the knee joints
     power_cost: float = 0.0                                      # MuJoCo planar: coef of sum(a^2)
     qvel_clip: float = 0.0                                       # MuJoCo planar: obs qvel clip (0: none)
+    # the robot links' changeDynamics material (mujoco HalfCheetah, robot_locomotors.py:210); the
+    # defaults are btCollisionObject's (restitution, spinning and rolling friction 0)
+    restitution: float = 0.0
+    spinning_friction: float = 0.0
+    rolling_friction: float = 0.0
 
 
 SPECS: Dict[str, RobotSpec] = OrderedDict()
@@ -147,7 +152,10 @@ _add(RobotSpec("Walker2DMuJoCoEnv-v0", "walker2d_mujoco", "walker2d.xml", "torso
 _add(RobotSpec("HalfCheetahMuJoCoEnv-v0", "halfcheetah_mujoco", "half_cheetah.xml", "torso", action_dim=6,
                obs_dim=17, kind=KIND_MUJOCO_PLANAR, power=1.0, alive=ALIVE_MJ_CHEETAH,
                power_coef={"bthigh": 120.0, "bshin": 90.0, "bfoot": 60.0, "fthigh": 140.0,
-                           "fshin": 60.0, "ffoot": 30.0}, power_cost=-0.1, qvel_clip=0.0))
+                           "fshin": 60.0, "ffoot": 30.0}, power_cost=-0.1, qvel_clip=0.0,
+               # robot_specific_reset :207-210: changeDynamics(lateralFriction=0.8,
+               # spinningFriction=0.1, rollingFriction=0.1, restitution=0.5) on every part
+               restitution=0.5, spinning_friction=0.1, rolling_friction=0.1))
 
 # MuJoCo-observation floating-base walkers: obs [qpos[2:], qvel, zeros] (float64 in the
 # reference), reward alive(state[0] + initial_z) + progress + joints_at_limit (no electricity);

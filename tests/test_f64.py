@@ -316,7 +316,7 @@ def test_f64_atlas_lane_kernel_is_refused(precision):
 # the Humanoids); kernel=0 selects the float64 lane-per-env kernel, which stays the
 # pendulums' path and the quad / gang kernels' cross-check.
 @pytest.mark.parametrize("env_id", ["AntPyBulletEnv-v0", "HumanoidPyBulletEnv-v0", "HopperPyBulletEnv-v0",
-                                    "HumanoidFlagrunHarderPyBulletEnv-v0"])
+                                    "HumanoidFlagrunHarderPyBulletEnv-v0", "HalfCheetahMuJoCoEnv-v0"])
 def test_f64_lane_kernel_teacher_forced(env_id):
     """The float64 lane kernel against the float64 oracle, same bounds."""
     _teacher_forced64(env_id, 128, 40, name=f"f64_lane[{env_id}]", kernel=0)
@@ -327,7 +327,8 @@ def test_f64_lane_kernel_teacher_forced(env_id):
     ("HumanoidPyBulletEnv-v0", "g16", 16), ("HumanoidFlagrunHarderPyBulletEnv-v0", "g16", 16),
     ("HumanoidPyBulletEnv-v0", None, 32), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
     ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 32),
-    ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 32), ("HumanoidMuJoCoEnv-v0", None, 32)])
+    ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 32), ("HumanoidMuJoCoEnv-v0", None, 32),
+    ("HalfCheetahMuJoCoEnv-v0", None, 16)])  # restitution + torsional rows (tests/test_contact_material.py)
 def test_f64_quad_and_gang_match_f64_lane(env_id, kernel, lanes):
     """Float64 quad / gang vs float64 lane kernel from the same states every step: the same contact
     sets and the state within 1e-9 (different summation orders in float64)."""
@@ -378,16 +379,17 @@ def test_f64_quad_workspace_rows_bitwise_equal_lds_rows():
     np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
 
 
-def test_f64_gang_workspace_contacts_bitwise_equal_lds_contacts():
+@pytest.mark.parametrize("env_id", ["HumanoidPyBulletEnv-v0", "HalfCheetahMuJoCoEnv-v0"])
+def test_f64_gang_workspace_contacts_bitwise_equal_lds_contacts(env_id):
     """Float64 gang contacts past the LDS capacity (lds_rows=0: all in the device workspace) change
-    no bit (Humanoid: floor + self contacts)."""
+    no bit (Humanoid: floor + self contacts; HalfCheetahMuJoCo: six rows per contact)."""
     def run(**kw):
-        e = VecEnv("HumanoidPyBulletEnv-v0", 128, seed=11, autoreset=True, precision=64, **kw)
+        e = VecEnv(env_id, 128, seed=11, autoreset=True, precision=64, **kw)
         e.reset()
         gen = torch.Generator(device="cuda").manual_seed(5)
         out, nc = [], []
         for _ in range(40):
-            e.step(torch.rand((128, 17), device="cuda", generator=gen) * 2 - 1, want_contacts=True)
+            e.step(torch.rand((128, e.info.action_dim), device="cuda", generator=gen) * 2 - 1, want_contacts=True)
             out.append(e.get_state()[0].clone())
             nc.append(e.ncontact.clone())
         return torch.stack(out).cpu().numpy(), torch.stack(nc).cpu().numpy()

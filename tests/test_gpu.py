@@ -240,8 +240,11 @@ COND_FRAC_ENV = {"InvertedPendulumPyBulletEnv-v0": 0.05, "InvertedPendulumSwingu
                  "HopperPyBulletEnv-v0": 0.14, "HalfCheetahPyBulletEnv-v0": 0.19, "AntPyBulletEnv-v0": 0.51,
                  "HumanoidPyBulletEnv-v0": 0.40, "Walker2DPyBulletEnv-v0": 0.19,
                  "HumanoidFlagrunPyBulletEnv-v0": 0.37, "HopperMuJoCoEnv-v0": 0.19, "Walker2DMuJoCoEnv-v0": 0.40,
-                 "HalfCheetahMuJoCoEnv-v0": 0.44, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.84,
+                 "HalfCheetahMuJoCoEnv-v0": 0.66, "AntMuJoCoEnv-v0": 0.83, "HumanoidMuJoCoEnv-v0": 0.84,
                  "HumanoidFlagrunHarderPyBulletEnv-v0": 0.53, "AtlasPyBulletEnv-v0": 0.62}
+# (HalfCheetahMuJoCo, round 6: its contact material -- restitution switching at |v_n| = 0.2 m/s and
+# the torsional rows' +-mu_t lambda_n clamps -- raised the oracle's own ill-conditioned share from
+# 0.34 to 0.56 of the 60-step test: 0.66.)
 # The kernel-variant tests (a kernel against the lane kernel from the same states, random actions,
 # no auto-reset: fallen robots lying on the floor) have their own ceilings, derived the same way
 # from their own measurements (r03r) plus 0.1.
@@ -789,12 +792,15 @@ def _rollout(env_id, n=128, steps=40, seed=11, **opts):
     return torch.stack(obs).cpu().numpy(), torch.stack(nc).cpu().numpy()
 
 
-@pytest.mark.parametrize("kernel", [-1, 0])
-def test_workspace_rows_bitwise_equal_lds_rows(kernel):
+@pytest.mark.parametrize("env_id,kernel", [("AntPyBulletEnv-v0", -1), ("AntPyBulletEnv-v0", 0),
+                                           ("HalfCheetahMuJoCoEnv-v0", 0)])
+def test_workspace_rows_bitwise_equal_lds_rows(env_id, kernel):
     """Contact rows past the LDS capacity live in the device workspace: forcing every row
-    there (lds_rows=0) must not change a single bit (quad and lane kernels)."""
-    a, ca = _rollout("AntPyBulletEnv-v0", n=256, steps=30, kernel=kernel)
-    b, cb = _rollout("AntPyBulletEnv-v0", n=256, steps=30, kernel=kernel, lds_rows=0)
+    there (lds_rows=0) must not change a single bit (quad and lane kernels; HalfCheetahMuJoCo's
+    lane kernel: six rows per contact)."""
+    a, ca = _rollout(env_id, n=256, steps=30, kernel=kernel)
+    b, cb = _rollout(env_id, n=256, steps=30, kernel=kernel, lds_rows=0)
+    assert ca.max() > 0
     np.testing.assert_array_equal(ca, cb)
     np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
@@ -880,7 +886,8 @@ def test_quad_kernel_determinism_and_offset_invariance():
                                          ("HumanoidPyBulletEnv-v0", {"gang_lanes": 32}),
                                          ("HumanoidFlagrunPyBulletEnv-v0", {"gang_lanes": 32}),
                                          ("HumanoidFlagrunHarderPyBulletEnv-v0", {}),
-                                         ("HumanoidFlagrunHarderPyBulletEnv-v0", {"gang_lanes": 32})])
+                                         ("HumanoidFlagrunHarderPyBulletEnv-v0", {"gang_lanes": 32}),
+                                         ("HalfCheetahMuJoCoEnv-v0", {})])  # restitution + torsional rows
 def test_gang_kernel_matches_lane_kernel_teacher_forced(env_id, opts):
     """Gang kernel (16 or 32 lanes per env; distributed dynamics with the front-parallel
     factorisation, or replicated dynamics) vs the lane kernel: same physics and row order,
@@ -890,7 +897,8 @@ def test_gang_kernel_matches_lane_kernel_teacher_forced(env_id, opts):
 
 
 @pytest.mark.parametrize("env_id,lanes", [("HumanoidPyBulletEnv-v0", 16), ("HumanoidPyBulletEnv-v0", 32),
-                                           ("HumanoidFlagrunHarderPyBulletEnv-v0", 16)])
+                                           ("HumanoidFlagrunHarderPyBulletEnv-v0", 16),
+                                           ("HalfCheetahMuJoCoEnv-v0", 16)])
 def test_gang_workspace_contacts_bitwise_equal_lds_contacts(env_id, lanes):
     """Gang contacts past the LDS capacity live in the device workspace: forcing every
     contact there (lds_rows=0) must not change a single bit (Humanoid: floor + self;
