@@ -193,7 +193,11 @@ int pbg_reset(pbg_handle* h, const uint8_t* mask, const float* init_q, float* ob
 
 /* WalkerBaseBulletEnv._step (gym_locomotion_envs.py:54-114): apply_action
  * (robot_locomotors.py:26-29) -> stepSimulation x substeps (scene_bases.py:75-76) ->
- * calc_state / potential / alive / feet contacts / costs.  No auto-reset. */
+ * calc_state / potential / alive / feet contacts / costs.  No auto-reset.
+ * act: [n, action_dim] float32, clipped to [-1, 1] for the torques (+-inf -> +-1, NaN -> -1: IEEE
+ * max); the electricity cost takes the unclipped value (a NaN action gives a NaN reward).  The
+ * reference asserts finite actions (robot_locomotors.py:27); the per-env facade does too, the
+ * batch API does not check them (that would cost a host sync per step). */
 int pbg_step(pbg_handle* h, const float* act, float* obs, float* rew, uint8_t* done, void* stream);
 /* pbg_step with optional outputs and in-launch auto-reset (gym TimeLimit + reset). */
 int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
@@ -214,6 +218,13 @@ int pbg_step_ex(pbg_handle* h, const pbg_step_io_t* io, void* stream);
  * so later resets continue that handle's reset-noise stream, not the checkpoint's. */
 int pbg_get_state(pbg_handle* h, double* phys, double* aux, void* stream);
 int pbg_set_state(pbg_handle* h, const double* phys, const double* aux, void* stream);
+
+/* Test support: fill every CU's LDS (160 KB each) with the 32-bit pattern and, when h is not NULL,
+ * h's device workspace (the contact / limit rows past the LDS capacity), stream-ordered before the
+ * next launch.  The kernels write everything they read in a launch, so a step after a poison must
+ * give the same bits whatever the pattern (tests/test_gpu.py test_uninitialised_memory_invariance).
+ * h NULL: the current device's LDS only. */
+int pbg_debug_poison(pbg_handle* h, uint32_t pattern, void* stream);
 
 /* The observation/reward/done pack alone (calc_state + the reward half of _step) on
  * explicit inputs, for golden-vector parity; layouts in pbg_pack_record_sizes. */

@@ -442,6 +442,35 @@ int pbg_sample_actions(int action_dim, int n_envs, int n_steps, uint64_t seed, u
   return hip_check((int)hipGetLastError(), "sample_actions launch");
 }
 
+// Test support (pbg_debug_poison): fill a whole CU's LDS with a 32-bit pattern, so the next kernel's
+// workgroups on that CU start on it instead of on whatever an earlier kernel left there
+__global__ __launch_bounds__(256) void poison_lds_kernel(uint32_t pattern) {
+  extern __shared__ uint32_t lds_poison[];
+  for (int i = threadIdx.x; i < 163840 / 4; i += 256) lds_poison[i] = pattern;
+  __syncthreads();
+}
+
+int pbg_debug_poison(pbg_handle* h, uint32_t pattern, void* stream) {
+  int dev = 0;
+  if (h) dev = h->device;
+  else if (hipGetDevice(&dev) != hipSuccess) return fail(PBG_E_HIP, "pbg_debug_poison: no device%s%ld");
+  DeviceGuard dg(dev);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return fail(PBG_E_HIP, "pbg_debug_poison: no CU count%s%ld");
+  int e = hip_check((int)hipFuncSetAttribute((const void*)poison_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             163840), "poison attribute");
+  if (e) return e;
+  // one 160 KB workgroup fills a CU; 8 per CU reach every CU of every XCD whatever the dispatch order
+  hipLaunchKernelGGL(poison_lds_kernel, dim3((unsigned)(8 * cus)), dim3(256), 163840, (hipStream_t)stream, pattern);
+  e = hip_check((int)hipGetLastError(), "poison launch");
+  if (e || !h) return e;
+  const size_t words = (size_t)h->geo.word_bytes * (size_t)h->B.n * (size_t)h->geo.scratch_words_per_env / 4;
+  if (words) e = hip_check((int)hipMemsetD32Async((hipDeviceptr_t)h->scratch, (int)pattern, words, (hipStream_t)stream),
+                           "poison workspace");
+  return e;
+}
+
 int pbg_pack(const char* env_id, int n, const double* in_rec, double* out_rec, void* stream) {
   const int rid = env_robot_id(env_id);
   if (rid < 0) return fail(PBG_E_ENV, "pbg_pack: unknown env id '%s'%ld", env_id ? env_id : "(null)");

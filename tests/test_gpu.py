@@ -1009,6 +1009,76 @@ def test_checkpoint_restore_is_bitwise_across_resets():
     np.testing.assert_array_equal(a.get_state()[1].cpu().numpy(), b.get_state()[1].cpu().numpy())
 
 
+@pytest.mark.parametrize("env_id,precision,opts", [
+    ("AntPyBulletEnv-v0", 32, {}), ("AntPyBulletEnv-v0", 64, {}), ("AntPyBulletEnv-v0", 64, {"lds_rows": 0}),
+    ("HumanoidPyBulletEnv-v0", 32, {}), ("HumanoidPyBulletEnv-v0", 64, {}), ("HumanoidPyBulletEnv-v0", 32, {"lds_rows": 0}),
+    ("HumanoidFlagrunHarderPyBulletEnv-v0", 32, {}), ("HalfCheetahMuJoCoEnv-v0", 64, {}),
+    ("HopperPyBulletEnv-v0", 64, {"kernel": 0}), ("HalfCheetahPyBulletEnv-v0", 32, {"kernel": 0}),
+    ("AtlasPyBulletEnv-v0", 32, {}), ("InvertedDoublePendulumPyBulletEnv-v0", 64, {})])
+def test_uninitialised_memory_invariance(env_id, precision, opts):
+    """Every kernel writes what it reads within a launch.  pbg_debug_poison fills every CU's LDS and the
+    handle's device workspace with a pattern before each step (float NaN 0x7FC00000 -- a double NaN
+    too when paired --, zero, 0x5A5A5A5A): states, observations and rewards must be bit-identical
+    across the patterns, for the quad, gang and lane kernels at both precisions, LDS and workspace
+    rows.  (Round 5's float64 quad build under the default machine schedule read memory it had not
+    written in that launch: its wrong results changed from box to box and stayed put within one
+    process sequence)"""
+    from pybulletgym_amd import _native
+    from pybulletgym_amd.vec_env import _stream
+    n = 64 if env_id.startswith("Atlas") else 256
+    runs = []
+    for pat in (0x7FC00000, 0x00000000, 0x5A5A5A5A):
+        e = VecEnv(env_id, n, seed=9, autoreset=True, precision=precision, **opts)
+        e.reset()
+        gen = torch.Generator(device="cuda").manual_seed(3)
+        st, ob, rw = [], [], []
+        for _ in range(12):
+            a = torch.rand((n, e.info.action_dim), device="cuda", generator=gen) * 2 - 1
+            _native.check(_native.lib().pbg_debug_poison(e._h, pat, _stream(e.device)), "pbg_debug_poison")
+            r = e.step(a, want_reward64=True)
+            st.append(e.get_state()[0].clone())
+            ob.append(r.obs.clone())
+            rw.append(e.reward64.clone())
+        runs.append([torch.stack(x).cpu().numpy() for x in (st, ob, rw)])
+        e.close()
+    for other in runs[1:]:
+        np.testing.assert_array_equal(runs[0][0].view(np.uint64), other[0].view(np.uint64))
+        np.testing.assert_array_equal(runs[0][1].view(np.uint32), other[1].view(np.uint32))
+        np.testing.assert_array_equal(runs[0][2].view(np.uint64), other[2].view(np.uint64))
+    assert np.isfinite(runs[0][0]).all()
+
+
+@pytest.mark.parametrize("precision", [32, 64])
+def test_non_finite_actions(precision):
+    """include/pbg.h pbg_step: the batch API clips +-inf to +-1 and NaN to -1 for the torques (the
+    state is bitwise the run with those values substituted and stays finite), the unclipped NaN
+    reaches the electricity cost (NaN reward); the per-env facade asserts finite actions like the
+    reference (robot_locomotors.py:27)."""
+    import pybulletgym_amd.envs as envs
+    n, env_id = 8, "HopperPyBulletEnv-v0"
+    bad = torch.full((n, 3), 0.3)
+    bad[1, 0], bad[2, 1], bad[3, 2] = float("nan"), float("inf"), -float("inf")
+    sub = bad.clone()
+    sub[1, 0], sub[2, 1], sub[3, 2] = -1.0, 1.0, -1.0
+    out = []
+    for a in (bad, sub):
+        e = VecEnv(env_id, n, seed=4, autoreset=False, precision=precision)
+        e.reset()
+        r = e.step(a.cuda(), want_reward64=True)
+        out.append((e.get_state()[0].cpu().numpy(), e.reward64.cpu().numpy(), r.obs.cpu().numpy()))
+        e.close()
+    (s0, r0, o0), (s1, r1, o1) = out
+    np.testing.assert_array_equal(s0.view(np.uint64), s1.view(np.uint64))
+    np.testing.assert_array_equal(o0, o1)
+    assert np.isfinite(s0).all() and np.isnan(r0[1]) and np.isfinite(np.delete(r0, [1, 2, 3])).all()
+    np.testing.assert_array_equal(np.delete(r0, [1, 2, 3]), np.delete(r1, [1, 2, 3]))
+    f = envs.make(env_id, precision=precision)
+    f.reset()
+    with pytest.raises(AssertionError):
+        f.step(np.array([np.nan, 0.0, 0.0], dtype=np.float32))
+    f.close()
+
+
 def test_facade_time_limit_is_truncation_not_termination():
     """The facade's inner env reports termination only; gym's TimeLimit sets the truncation
     flag at step 1000 (a survived episode must not look terminal)."""

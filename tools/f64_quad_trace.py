@@ -55,11 +55,22 @@ def child(lib, out):
     r = np.random.default_rng(7)
     q.reset(init_q=torch.from_numpy(r.uniform(-0.1, 0.1, (n, q.info.reset_dofs)).astype(np.float32)))
     res = {}
+    # PBG_POISON=0xPATTERN: every CU's LDS filled with the pattern before the quad step (pbg_debug_poison
+    # of PBG_POISON_LIB, default the product library -- so a library without the entry point, such as
+    # round 5's, can be probed for reads of LDS it never wrote)
+    poison = os.environ.get("PBG_POISON")
+    if poison:
+        PL = ctypes.CDLL(os.environ.get("PBG_POISON_LIB", os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd.so")))
+        PL.pbg_debug_poison.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     for tag in ("zero", "rand"):
         phys, aux = q.get_state()
         ln.set_state(phys, aux)
         a = torch.zeros((n, 8), device="cuda") if tag == "zero" else \
             torch.from_numpy(r.uniform(-1, 1, (n, 8)).astype(np.float32)).cuda()
+        if poison:
+            torch.cuda.synchronize()
+            assert PL.pbg_debug_poison(None, int(poison, 16), None) == 0
+            torch.cuda.synchronize()
         q.step(a)
         torch.cuda.synchronize()
         buf = np.full(256 * 8 * 8, np.nan)
@@ -77,7 +88,8 @@ def main(libs):
     outs = {}
     for lib in libs:
         out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", REPO), "gpurun_out",
-                           "f64_trace_" + os.path.basename(lib).replace(".so", ".npz"))
+                           "f64_trace_" + os.path.basename(lib).replace(".so", "")
+                           + (f"_poison{os.environ['PBG_POISON']}" if os.environ.get("PBG_POISON") else "") + ".npz")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         subprocess.check_call([sys.executable, __file__, "--child", lib, out], timeout=300)
         outs[lib] = np.load(out)
