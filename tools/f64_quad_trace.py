@@ -58,8 +58,15 @@ def child(lib, out):
     # PBG_POISON=0xPATTERN: every CU's LDS filled with the pattern before the quad step (pbg_debug_poison
     # of PBG_POISON_LIB, default the product library -- so a library without the entry point, such as
     # round 5's, can be probed for reads of LDS it never wrote)
+    # PBG_POISON_RANGE=b:e: only LDS words [b, e) get the pattern, the rest zero (tools/liblds_poison.so;
+    # tools/lds_poison_bisect.py)
     poison = os.environ.get("PBG_POISON")
-    if poison:
+    prange = os.environ.get("PBG_POISON_RANGE")
+    if poison and prange:
+        RL = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblds_poison.so"))
+        RL.lds_poison_range.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        b_, e_ = (int(x) for x in prange.split(":"))
+    elif poison:
         PL = ctypes.CDLL(os.environ.get("PBG_POISON_LIB", os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd.so")))
         PL.pbg_debug_poison.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     for tag in ("zero", "rand"):
@@ -69,7 +76,10 @@ def child(lib, out):
             torch.from_numpy(r.uniform(-1, 1, (n, 8)).astype(np.float32)).cuda()
         if poison:
             torch.cuda.synchronize()
-            assert PL.pbg_debug_poison(None, int(poison, 16), None) == 0
+            if prange:
+                assert RL.lds_poison_range(int(poison, 16), b_, e_) == 0
+            else:
+                assert PL.pbg_debug_poison(None, int(poison, 16), None) == 0
             torch.cuda.synchronize()
         q.step(a)
         torch.cuda.synchronize()
