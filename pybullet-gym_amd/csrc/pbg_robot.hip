@@ -92,6 +92,14 @@ constexpr bool gang_ok() {
 // Gang geometry (pbg_gang.hip): T = 16 or 32 lanes per env, 256 / T envs per 4-wave workgroup;
 // the per-env LDS region holds the staged dynamics, limit rows and `cap` contacts (descriptor
 // + 3 rows), contacts past the capacity spill to the device workspace.
+// the replicated-dynamics variant (the whole dynamics per lane, no distributed mass matrix): float32
+// walkers, and the float64 robots under 8 dofs (Hopper: 512 registers, no spill, -4.5 % at 4,096 envs;
+// the float64 HalfCheetah / Walker2D variants spill 1.2-1.3 KB and run 2.1-2.5x slower,
+// profiles/r06_ab_f64_repl.txt)
+template <class RR, int T>
+constexpr bool gang_repl() {
+  return T == 16 && !RR::harder && (sizeof(real_t<RR>) == 4 || RR::NDOF < 8);
+}
 template <class RR, int T>
 static int plan_gang_t(int n_envs, int cus, Geometry* g) {
   if constexpr (gang_ok<RR, T>()) {
@@ -124,10 +132,9 @@ static int plan_gang_t(int n_envs, int cus, Geometry* g) {
     while (cap > 0 && (long)region(cap) * EPB * WB > budget) cap--;
     // distributed dynamics from 8 dofs (Walker2D, HalfCheetah, Humanoid: round-2 A/B) or more than one wave per SIMD (its
     // smaller register footprint lets two waves share a SIMD); replicated otherwise
-    // (float64: distributed always -- the replicated dynamics() of a whole robot per lane spills in float64)
-    constexpr bool REPL = T == 16 && !RR::harder && sizeof(real_t<RR>) == 4;  // has a replicated variant
+    constexpr bool REPL = gang_repl<RR, T>();  // has a replicated variant
     g->gang_dist = !REPL || RR::NDOF >= 8 || (size_t)n_envs * T > (size_t)64 * 4 * cus;
-    // pbg_create_debug (32-lane gangs, the cube robot and float64 have no replicated-dynamics variant)
+    // pbg_create_debug (32-lane gangs, the cube robot and float64 from 8 dofs have no replicated-dynamics variant)
     if ((g->force_dist == 0 || g->force_dist == 1) && REPL) g->gang_dist = g->force_dist;
     g->team = T;
     g->block = gang_block<RR, T>();
@@ -162,7 +169,7 @@ template <class RR, int T>
 static bool launch_gang_t(const Buffers& B, const StepIO& io, float* scratch, const Geometry& g, hipStream_t s) {
   if constexpr (gang_ok<RR, T>()) {
     const dim3 grid(blocks(B.n, gang_block<RR, T>() / T)), blk(gang_block<RR, T>());
-    if constexpr (T == 16 && !RR::harder && sizeof(real_t<RR>) == 4) {
+    if constexpr (gang_repl<RR, T>()) {
       if (!g.gang_dist) {
         hipLaunchKernelGGL((gang_step_kernel<RR, T, false>), grid, blk, g.lds_bytes, s, B, io, scratch, g.lds_rows,
                            g.env_words);

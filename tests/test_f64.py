@@ -309,6 +309,16 @@ def test_f64_atlas_lane_kernel_is_refused(precision):
         VecEnv("HopperPyBulletEnv-v0", 4, precision=precision, gang_lanes=32)
 
 
+def test_f64_replicated_dynamics_only_under_8_dofs():
+    """The float64 replicated-dynamics gang variant exists for robots under 8 dofs (Hopper); the
+    float64 HalfCheetah has none (it would spill 1.3 KB): gang_dist = 0 is PBG_E_ARG there, and
+    Hopper honours both variants."""
+    with pytest.raises(PbgError, match=r"failed \(-1\).*replicated-dynamics"):
+        VecEnv("HalfCheetahPyBulletEnv-v0", 64, precision=64, gang_dist=0)
+    for d in (0, 1):
+        VecEnv("HopperPyBulletEnv-v0", 64, precision=64, gang_dist=d).close()
+
+
 # ------------------------------------------------------------------ float64 kernel variants
 # The float64 walkers run the kernels of the float32 path instantiated on F64<R>: Ant the quad
 # kernel (pbg_team.hip, 4 lanes per env; AntMuJoCo too), the Humanoid family 32-lane gangs, the
@@ -326,14 +336,17 @@ def test_f64_lane_kernel_teacher_forced(env_id):
     ("AntPyBulletEnv-v0", None, 4), ("AntMuJoCoEnv-v0", None, 4), ("AntPyBulletEnv-v0", 2, 16),
     ("HumanoidPyBulletEnv-v0", "g16", 16), ("HumanoidFlagrunHarderPyBulletEnv-v0", "g16", 16),
     ("HumanoidPyBulletEnv-v0", None, 32), ("HalfCheetahPyBulletEnv-v0", None, 16), ("Walker2DPyBulletEnv-v0", None, 16),
-    ("HopperPyBulletEnv-v0", None, 16), ("HumanoidFlagrunPyBulletEnv-v0", None, 32),
+    ("HopperPyBulletEnv-v0", None, 16), ("HopperPyBulletEnv-v0", "dist", 16), ("HopperMuJoCoEnv-v0", None, 16),
+    ("HumanoidFlagrunPyBulletEnv-v0", None, 32),
     ("HumanoidFlagrunHarderPyBulletEnv-v0", None, 32), ("HumanoidMuJoCoEnv-v0", None, 32),
     ("HalfCheetahMuJoCoEnv-v0", None, 16)])  # restitution + torsional rows (tests/test_contact_material.py)
 def test_f64_quad_and_gang_match_f64_lane(env_id, kernel, lanes):
     """Float64 quad / gang vs float64 lane kernel from the same states every step: the same contact
-    sets and the state within 1e-9 (different summation orders in float64)."""
+    sets and the state within 1e-9 (different summation orders in float64).  The float64 Hopper runs
+    the replicated-dynamics gang variant by default (round 6); "dist" forces its distributed one."""
     n = 256
-    kw = {} if kernel is None else ({"gang_lanes": 16} if kernel == "g16" else {"kernel": kernel})
+    kw = {} if kernel is None else ({"gang_lanes": 16} if kernel == "g16" else
+                                    ({"gang_dist": 1} if kernel == "dist" else {"kernel": kernel}))
     g = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, **kw)
     ln = VecEnv(env_id, n, seed=3, autoreset=False, precision=64, kernel=0)
     assert g.info.lanes_per_env == lanes and ln.info.lanes_per_env == 1
