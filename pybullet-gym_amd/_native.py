@@ -98,11 +98,13 @@ def lib():
     L.pbg_set_state.argtypes = [H, P, P, P]
     L.pbg_pack_record_sizes.argtypes = [ctypes.c_char_p, ctypes.POINTER(I), ctypes.POINTER(I)]
     L.pbg_pack.argtypes = [ctypes.c_char_p, I, P, P, P]
-    L.pbg_debug_poison.argtypes = [H, ctypes.c_uint32, P]
+    if hasattr(L, "pbg_debug_poison"):  # diagnostic entry (tools/vgpr_poison_probe.py also loads older builds)
+        L.pbg_debug_poison.argtypes = [H, ctypes.c_uint32, P]
+        L.pbg_debug_poison.restype = I
     L.pbg_last_error.restype = ctypes.c_char_p
     for f in ("pbg_info", "pbg_reset", "pbg_step", "pbg_step_ex", "pbg_get_state", "pbg_set_state",
               "pbg_pack_record_sizes", "pbg_pack", "pbg_create_debug", "pbg_sample_actions", "pbg_create_ex",
-              "pbg_default_sim_params", "pbg_get_sim_params", "pbg_create_v2", "pbg_precision", "pbg_debug_poison"):
+              "pbg_default_sim_params", "pbg_get_sim_params", "pbg_create_v2", "pbg_precision"):
         getattr(L, f).restype = I
     _lib = L
     return L

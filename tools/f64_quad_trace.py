@@ -69,11 +69,33 @@ def child(lib, out):
     elif poison:
         PL = ctypes.CDLL(os.environ.get("PBG_POISON_LIB", os.path.join(REPO, "pybullet-gym_amd", "libpbg_amd.so")))
         PL.pbg_debug_poison.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    # PBG_VGPR_POISON=0xBASE: every SIMD's whole register file (256 VGPRs + 256 AGPRs) set to BASE | index
+    # right before the quad step (tools/libvgpr_poison.so), after any LDS poison
+    # PBG_VGPR_POISON=A:B:W0,..,W15 (hex): register r gets A where bit r of the 512-bit mask is set, else B
+    vpoison = os.environ.get("PBG_VGPR_POISON")
+    if vpoison:
+        VL = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvgpr_poison.so"))
+        VL.vgpr_poison.argtypes = [ctypes.c_uint32, ctypes.c_int]
+        VL.vgpr_poison_mask.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
+        if ":" in vpoison:
+            pa, pb, pm = vpoison.split(":")
+            vmask = np.array([int(x, 16) for x in pm.split(",")], dtype=np.uint32)
+            assert vmask.size == 16
+
+    def vgpr_poison():
+        if ":" in vpoison:
+            assert VL.vgpr_poison_mask(int(pa, 16), int(pb, 16), vmask.ctypes.data, 8192) == 0
+        else:
+            assert VL.vgpr_poison(int(vpoison, 16), 8192) == 0
     for tag in ("zero", "rand"):
         phys, aux = q.get_state()
         ln.set_state(phys, aux)
         a = torch.zeros((n, 8), device="cuda") if tag == "zero" else \
             torch.from_numpy(r.uniform(-1, 1, (n, 8)).astype(np.float32)).cuda()
+        if vpoison and not poison:
+            torch.cuda.synchronize()
+            vgpr_poison()
+            torch.cuda.synchronize()
         if poison:
             torch.cuda.synchronize()
             if prange:
@@ -81,6 +103,9 @@ def child(lib, out):
             else:
                 assert PL.pbg_debug_poison(None, int(poison, 16), None) == 0
             torch.cuda.synchronize()
+            if vpoison:
+                vgpr_poison()
+                torch.cuda.synchronize()
         q.step(a)
         torch.cuda.synchronize()
         buf = np.full(256 * 8 * 8, np.nan)

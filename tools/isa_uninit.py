@@ -62,6 +62,12 @@ def width(mn):
     return 4
 
 
+def kernels(path):
+    """The mangled names of the kernels (function labels) of an ISA file."""
+    return [ln.split(":")[0] for ln in open(path).read().split("\n")
+            if ln.startswith("_Z") and ":" in ln and "@" in ln]
+
+
 def parse(path, kernel):
     lines = open(path).read().split("\n")
     start = None
@@ -241,6 +247,97 @@ def analyse(insts):
     return blocks, reports
 
 
+COPY = ("v_accvgpr_write_b32", "v_accvgpr_read_b32", "v_mov_b32_e32", "v_mov_b32", "v_accvgpr_mov_b32",
+        "v_mov_b64_e32", "v_mov_b64")
+
+
+def exec_copies(insts):
+    """Copies of a live-through value placed under a partial EXEC: a register move (or a spill to a
+    constant-offset scratch slot) in the join block of a
+    divergent region (after its last label, before the `s_or_b64 exec, exec, sN` that ends the region)
+    whose source was last written before the region's `s_and_saveexec_b64 sN` and whose destination is
+    read after the region before it is written again.  The move copies only the lanes inside the
+    region; the other lanes read the destination's stale contents (the round-5 float64 quad
+    miscompile)."""
+    code = [i for i in insts]
+    stack, out = [], []
+    last_label = 0
+    for k, (ln, lab, mn, ops, raw) in enumerate(code):
+        if lab is not None:
+            last_label = k
+            continue
+        o = ops.replace(" ", "")
+        if mn == "s_and_saveexec_b64":
+            stack.append((o.split(",")[0], k))
+        elif mn == "s_xor_b64" and stack and o.split(",")[1:] == ["exec", stack[-1][0]]:
+            stack[-1] = (o.split(",")[0], stack[-1][1])  # if / else: the else lanes' mask ends the region
+        elif mn == "s_or_b64" and o.startswith("exec,exec,"):
+            sp = o.split(",")[2]
+            at = [i for i, (r, _) in enumerate(stack) if r == sp]
+            if not at:
+                continue  # a loop's exit mask or an else arm: no s_and_saveexec of this pair is open
+            _, start = stack[at[-1]]
+            del stack[at[-1]:]
+            for j in range(max(last_label, start) + 1, k):
+                jl, _, jmn, jops, jraw = code[j]
+                parts = split_ops(jops)
+                slot = None
+                if jmn.startswith("scratch_store") and len(parts) >= 2 and not regs_of(parts[0]):
+                    # a spill of a live-through value under the region's EXEC (constant-offset slot)
+                    m = re.search(r"offset:(-?\d+)", jops)
+                    slot = set(range(int(m.group(1)) if m else 0, (int(m.group(1)) if m else 0) + width(jmn)))
+                    dst, src = [], regs_of(parts[1])
+                elif jmn in COPY:
+                    dst, src = regs_of(parts[0]), regs_of(",".join(parts[1:]))
+                    if not dst:
+                        continue
+                else:
+                    continue
+                if not src:
+                    continue
+                # the source's last write before the copy
+                sdef = None
+                for t in range(j - 1, -1, -1):
+                    tm = code[t][2]
+                    if tm is None:
+                        continue
+                    tops = split_ops(code[t][3])
+                    if tops and not tm.startswith(("s_", "v_cmp", "v_readlane", "v_readfirstlane")) and "store" not in tm \
+                            and not (tm.startswith("ds_") and "read" not in tm) and set(regs_of(tops[0])) & set(src):
+                        sdef = t
+                        break
+                if sdef is None or sdef >= start:
+                    continue
+                # the destination read after the region before a rewrite
+                for t in range(k + 1, len(code)):
+                    tm = code[t][2]
+                    if tm is None:
+                        continue
+                    tops = split_ops(code[t][3])
+                    if not tops:
+                        continue
+                    if slot is not None:
+                        if tm.startswith("scratch_") and len(tops) >= 2:
+                            m = re.search(r"offset:(-?\d+)", code[t][3])
+                            o = int(m.group(1)) if m else 0
+                            bytes_ = set(range(o, o + width(tm)))
+                            if "load" in tm and not regs_of(tops[1]) and bytes_ & slot:
+                                out.append((jl, jraw, code[sdef][0], code[start][0], code[k][0], code[t][0], code[t][4]))
+                                break
+                            if "store" in tm and not regs_of(tops[0]) and bytes_ >= slot:
+                                break
+                        continue
+                    defines = not tm.startswith(("s_", "v_cmp", "v_readlane", "v_readfirstlane")) and "store" not in tm \
+                        and not (tm.startswith("ds_") and "read" not in tm)
+                    reads = set(regs_of(",".join(tops[1:] if defines else tops)))
+                    if reads & set(dst):
+                        out.append((jl, jraw, code[sdef][0], code[start][0], code[k][0], code[t][0], code[t][4]))
+                        break
+                    if defines and set(regs_of(tops[0])) >= set(dst):
+                        break
+    return out
+
+
 def rname(r):
     return f"v{r}" if r < 256 else f"a{r - 256}"
 
@@ -250,8 +347,27 @@ def main():
     ap.add_argument("asm")
     ap.add_argument("--kernel", default="team_step_kernelINS_3F64IN10pbg_models3AntE")
     ap.add_argument("--show", type=int, default=40)
+    ap.add_argument("--exec-copies", action="store_true", help="only the partial-EXEC copy check; exit 1 on a hit")
+    ap.add_argument("--all", action="store_true", help="--exec-copies over every kernel of the file")
     a = ap.parse_args()
+    if a.all:
+        names = kernels(a.asm)
+        hits = 0
+        for k in names:
+            ec = exec_copies(parse(a.asm, k))
+            hits += len(ec)
+            print(f"{k[:110]}: {len(ec)} partial-EXEC copies read after their region")
+            for jl, raw, sdef, start, end, rl, rraw in ec[: a.show]:
+                print(f"  line {jl}: {raw}   (source written at line {sdef}, region {start}..{end}, read at line {rl}: {rraw})")
+        print(f"{a.asm}: {len(names)} kernels, {hits} partial-EXEC copies")
+        sys.exit(1 if hits else 0)
     insts = parse(a.asm, a.kernel)
+    ec = exec_copies(insts)
+    print(f"{a.asm}: {len(ec)} copies of a live-through value under a region's partial EXEC, read after the region")
+    for jl, raw, sdef, start, end, rl, rraw in ec[: a.show]:
+        print(f"  line {jl}: {raw}   (source written at line {sdef}, region {start}..{end}, read at line {rl}: {rraw})")
+    if a.exec_copies:
+        sys.exit(1 if ec else 0)
     blocks, reps = analyse(insts)
     nin = sum(1 for i in insts if i[2])
     print(f"{a.asm}: {nin} instructions, {len(blocks)} blocks, {len(reps)} reads of a register / scratch "
