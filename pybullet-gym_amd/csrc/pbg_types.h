@@ -72,7 +72,11 @@ struct F64 : R0 {
 // cross-check of the others, keeps the trigonometry it was validated with.
 template <class R0>
 struct F64L : F64<R0> {
+#ifdef PBG_DEV_LANE_OWN_TRIG  // diagnostic ISA only (tests/test_isa_exec_copies.py): the round-6 variant
+  static constexpr bool lib_trig = false;
+#else
   static constexpr bool lib_trig = true;
+#endif
 };
 template <class R, class = void>
 struct LibTrig {

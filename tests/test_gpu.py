@@ -1014,20 +1014,30 @@ def test_checkpoint_restore_is_bitwise_across_resets():
     ("HumanoidPyBulletEnv-v0", 32, {}), ("HumanoidPyBulletEnv-v0", 64, {}), ("HumanoidPyBulletEnv-v0", 32, {"lds_rows": 0}),
     ("HumanoidFlagrunHarderPyBulletEnv-v0", 32, {}), ("HalfCheetahMuJoCoEnv-v0", 64, {}),
     ("HopperPyBulletEnv-v0", 64, {"kernel": 0}), ("HalfCheetahPyBulletEnv-v0", 32, {"kernel": 0}),
-    ("AtlasPyBulletEnv-v0", 32, {}), ("InvertedDoublePendulumPyBulletEnv-v0", 64, {})])
+    ("AtlasPyBulletEnv-v0", 32, {}), ("InvertedDoublePendulumPyBulletEnv-v0", 64, {}),
+    ("HopperPyBulletEnv-v0", 64, {}), ("HumanoidFlagrunHarderPyBulletEnv-v0", 32, {"gang_lanes": 32}),
+    ("HumanoidPyBulletEnv-v0", 64, {"kernel": 0}), ("AntMuJoCoEnv-v0", 64, {})])
 def test_uninitialised_memory_invariance(env_id, precision, opts):
     """Every kernel writes what it reads within a launch.  pbg_debug_poison fills every CU's LDS and the
     handle's device workspace with a pattern before each step (float NaN 0x7FC00000 -- a double NaN
-    too when paired --, zero, 0x5A5A5A5A): states, observations and rewards must be bit-identical
+    too when paired --, zero, 0x5A5A5A5A), and tools/libvgpr_poison.so every SIMD's register file
+    (the round-5 bug read stale AGPR lanes): states, observations and rewards must be bit-identical
     across the patterns, for the quad, gang and lane kernels at both precisions, LDS and workspace
     rows.  (Round 5's float64 quad build under the default machine schedule read memory it had not
     written in that launch: its wrong results changed from box to box and stayed put within one
     process sequence)"""
+    import ctypes
     from pybulletgym_amd import _native
     from pybulletgym_amd.vec_env import _stream
+    vp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libvgpr_poison.so")
+    assert os.path.exists(vp), "tools/libvgpr_poison.so: run __graft_entry__.build()"
+    VL = ctypes.CDLL(vp)
+    VL.vgpr_poison.argtypes = [ctypes.c_uint32, ctypes.c_int]
     n = 64 if env_id.startswith("Atlas") else 256
     runs = []
-    for pat in (0x7FC00000, 0x00000000, 0x5A5A5A5A):
+    # LDS + workspace pattern, and the register-file base (every SIMD's 256 VGPRs + 256 AGPRs = base | index:
+    # a NaN high word, zero, 1.0's high word) set right before each step
+    for pat, reg in ((0x7FC00000, 0x7FF80000), (0x00000000, 0x00000000), (0x5A5A5A5A, 0x3FF00000)):
         e = VecEnv(env_id, n, seed=9, autoreset=True, precision=precision, **opts)
         e.reset()
         gen = torch.Generator(device="cuda").manual_seed(3)
@@ -1035,6 +1045,8 @@ def test_uninitialised_memory_invariance(env_id, precision, opts):
         for _ in range(12):
             a = torch.rand((n, e.info.action_dim), device="cuda", generator=gen) * 2 - 1
             _native.check(_native.lib().pbg_debug_poison(e._h, pat, _stream(e.device)), "pbg_debug_poison")
+            torch.cuda.synchronize()
+            assert VL.vgpr_poison(reg, 8192) == 0
             r = e.step(a, want_reward64=True)
             st.append(e.get_state()[0].clone())
             ob.append(r.obs.clone())

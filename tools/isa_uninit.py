@@ -261,6 +261,22 @@ def exec_copies(insts):
     miscompile)."""
     code = [i for i in insts]
     stack, out = [], []
+    label_at = {c[1]: t for t, c in enumerate(code) if c[1] is not None and c[1].startswith(".LBB")}
+    branches = [(t, c[3].strip()) for t, c in enumerate(code) if c[2] and c[2].startswith(("s_branch", "s_cbranch"))]
+
+    def sese(a, b):
+        """Single entry, single exit: no branch inside [a, b] leaves it (other than to the label right
+        after b) and no branch from outside targets a label strictly inside it."""
+        for t, tgt in branches:
+            d = label_at.get(tgt)
+            if d is None:
+                continue
+            inside_src, inside_dst = a < t < b, a < d < b
+            if inside_src and not inside_dst and d != b + 1:
+                return False
+            if not inside_src and inside_dst:
+                return False
+        return True
     last_label = 0
     for k, (ln, lab, mn, ops, raw) in enumerate(code):
         if lab is not None:
@@ -278,6 +294,8 @@ def exec_copies(insts):
                 continue  # a loop's exit mask or an else arm: no s_and_saveexec of this pair is open
             _, start = stack[at[-1]]
             del stack[at[-1]:]
+            if not sese(start, k):
+                continue  # an unstructured region (branches in or out): its lanes are not one mask
             for j in range(max(last_label, start) + 1, k):
                 jl, _, jmn, jops, jraw = code[j]
                 parts = split_ops(jops)
