@@ -248,10 +248,11 @@ static int launch_lane(const Buffers& B, const StepIO& io, float* scratch, const
 // ---- the float64 quad kernel (Team<R64>::ok: Ant, AntMuJoCo) is its own translation unit
 // (-DPBG_TEAM64_TU, Makefile T64FLAGS).  Round 5 compiled it with the AMDGPU register-pressure trackers
 // in the machine scheduler: under the default schedule the round-5 source computed NaN velocities in
-// every env.  Round 6 reproduced that on the round-5 source and localised it to the pre-RA machine
-// scheduler's reordering (opt-bisect; every other schedule tried is wrong too, instrumented builds are
-// right); the current source is exact under both schedules and ships on the default one (DESIGN.md
-// section 4, tools/f64_quad_trace.py).
+// every env.  Round 6 found the cause, a backend bug: the register allocator placed the VGPR->AGPR split
+// copies of two live-through doubles in a divergent region's join block before its EXEC restore, so
+// lanes outside the region read stale AGPRs (register-file poisoning on the GPU; DESIGN.md section 4,
+// tools/isa_uninit.py --exec-copies, tests/test_isa_exec_copies.py).  The current source has no such
+// copy under either schedule and ships on the default one.
 template <class RR>
 constexpr bool team64_ok() { return Team<RR>::ok; }
 int PBG_FN(plan_team64_)(int n_envs, int cus, Geometry* g);
