@@ -100,3 +100,19 @@ def test_product_float64_quad_kernel_has_no_partial_exec_copies(tmp_path, robot)
     assert names, "no quad kernel in the ISA"
     for k in names:
         assert isa_uninit.exec_copies(isa_uninit.parse(str(out), k)) == [], k
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None or not os.path.isdir(os.path.join(REPO, ".git")),
+                    reason="needs hipcc and the git history")
+def test_round5_source_reproduces_the_faulting_copies(tmp_path):
+    """The real instance: the round-5 source (commit 4428492) on the default schedule has the split
+    copies of a54 / a55 / a180 / a181 before the region's EXEC restore -- the registers the GPU
+    register-file bisection found (profiles/r06_f64_quad_miscompile/register_bisect.txt) -- and the
+    trackers build it shipped with has none (tools/repro_r05_miscompile.sh)."""
+    out = subprocess.run(["bash", os.path.join(REPO, "tools", "repro_r05_miscompile.sh"), str(tmp_path / "w")],
+                         capture_output=True, text=True, timeout=800).stdout
+    default, trackers = out.split("trackers.s:")
+    for reg in ("a54, v", "a55, v", "a180, v", "a181, v"):
+        assert f"v_accvgpr_write_b32 {reg}" in default, (reg, out)
+    assert trackers.strip().startswith("0 copies"), out
